@@ -1,0 +1,121 @@
+/*
+ * sed.h — C-ABI of libsed.so, the MI355X (gfx950) engine for the weighted
+ * Wagner–Fischer edit distance and its canonical edit script.
+ *
+ * It replaces the compute inside the reference's Python module
+ * StringEditDistance (plsakr/rna-sequence-diff-patch):
+ *   wagnerFisher(str1, str2, userCosts)   StringEditDistance.py:133-224  -> sed_run_batch / sed_batch_*
+ *   min_cost / cost (per-cell recurrence) StringEditDistance.py:76-128   -> the DP kernels
+ *   create_paths(dp)[0] (canonical path)  StringEditDistance.py:228-271  -> SED_WANT_SCRIPT traceback
+ *   generate_es op sequence               StringEditDistance.py:274-334  -> packed op codes
+ *   wf_score distance                     IRMethods.py:435-440           -> out_dist
+ * The reference has no FFI; its boundary is the Python module itself.  The
+ * Python shim (rna-sequence-diff-patch_amd/StringEditDistance.py) keeps that
+ * module's names and calls this ABI through ctypes (binding shown in
+ * INTEGRATION.md).
+ *
+ * Conventions
+ *   - Sequences are passed as per-call alphabet codes (uint8, 0..K-1); the
+ *     caller resolves characters -> codes and the reference's cost() into a
+ *     K x K matrix (value + "is a Python int" flag) and raises the
+ *     reference's KeyError itself before calling.
+ *   - Every host buffer is caller-allocated.  The context owns device memory
+ *     and its HIP stream.  No C++ exception crosses this ABI; functions return
+ *     SED_OK or a negative SED_E_* code, with text in sed_last_error().
+ *   - Threading: one context per thread and device; calls on one context are
+ *     serialised by the caller; distinct contexts are independent.
+ *   - Op codes of a script, origin -> sink order, 2 bits each, 16 per uint32
+ *     (op p at bits 2*(p%16) of word p/16): 0 insert, 1 delete, 2 update.
+ */
+#ifndef SED_H
+#define SED_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    SED_OK = 0,
+    SED_E_ARG = -1,       /* bad argument (NULL, negative length, non-finite cost ...) */
+    SED_E_DEVICE = -2,    /* HIP error */
+    SED_E_OOM = -3,       /* device allocation failed */
+    SED_E_RANGE = -4,     /* forced integer mode but the packed key would overflow */
+    SED_E_ALPHABET = -5,  /* alphabet larger than the kernel supports (K > 32) */
+    SED_E_STATE = -6      /* call order (no costs set, batch not run ...) */
+};
+
+/* flags for sed_run_batch / sed_batch_create */
+#define SED_WANT_SCRIPT 1u
+
+/* sed_set_option keys */
+#define SED_OPT_MODE 1          /* 0 auto, 1 packed-integer kernel, 2 fp64 kernel, 3 fp64 + int-typing */
+#define SED_OPT_ROWS_PER_LANE 2 /* 0 auto, else 1,2,4,8,16,32 (integer) / 1,2,4,8 (fp64) */
+
+/* modes reported by sed_batch_mode */
+#define SED_MODE_I32 1
+#define SED_MODE_F64 2
+#define SED_MODE_F64_TYPED 3
+
+typedef struct sed_ctx sed_ctx;
+typedef struct sed_batch sed_batch;
+
+const char *sed_version(void);
+
+/* Create a context on HIP device `device` (NULL on failure). */
+sed_ctx *sed_create(int device);
+void sed_destroy(sed_ctx *ctx);
+const char *sed_last_error(const sed_ctx *ctx);
+int sed_set_option(sed_ctx *ctx, int key, int value);
+
+/* Cost model (replaces default_costs / user_costs lookups, StringEditDistance.py:6-18,76-99).
+ * sub[a*K+b] = cost(symbol a -> symbol b) as the reference's cost() returns it
+ * (0 for case-insensitive matches), sub_int[a*K+b] = 1 when that value is a Python int. */
+int sed_set_costs(sed_ctx *ctx, int K, const double *sub, const uint8_t *sub_int,
+                  double ins, int ins_is_int, double del, int del_is_int);
+
+/* One-shot batch: host inputs, host outputs (blocking).
+ * Pair p: str1 = codes_a[off_a[p] .. +len_a[p]), str2 = codes_b[off_b[p] .. +len_b[p]).
+ * out_dist[p]  = dp[n][m].value as fp64; out_is_int[p] = 1 when it is a Python int.
+ * out_len[p]   = number of ops in the canonical script.
+ * With SED_WANT_SCRIPT: out_ops + ops_off[p] receives ceil((n+m)/16) words for pair p. */
+int sed_run_batch(sed_ctx *ctx,
+                  const uint8_t *codes_a, const int64_t *off_a, const int32_t *len_a,
+                  const uint8_t *codes_b, const int64_t *off_b, const int32_t *len_b,
+                  int32_t npairs, uint32_t flags,
+                  double *out_dist, uint8_t *out_is_int, int32_t *out_len,
+                  uint32_t *out_ops, const int64_t *ops_off);
+
+/* Device-resident batch: upload once, run many times (bench), fetch results. */
+sed_batch *sed_batch_create(sed_ctx *ctx,
+                            const uint8_t *codes_a, const int64_t *off_a, const int32_t *len_a,
+                            const uint8_t *codes_b, const int64_t *off_b, const int32_t *len_b,
+                            int32_t npairs, uint32_t flags);
+void sed_batch_destroy(sed_batch *b);
+int sed_batch_mode(const sed_batch *b);               /* SED_MODE_* chosen for this batch */
+int sed_batch_rows_per_lane(const sed_batch *b);
+int sed_batch_run(sed_batch *b);                      /* enqueue on the context stream, returns at once */
+int sed_batch_sync(sed_batch *b);                     /* wait for the last run */
+/* device time of the last run, from HIP events on the launching stream (ms) */
+int sed_batch_last_times(const sed_batch *b, float *dp_ms, float *traceback_ms);
+int sed_batch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32_t *out_len,
+                      uint32_t *out_ops, const int64_t *ops_off);
+/* Device pointers of the result arrays (for an RCCL gather); any may be NULL. */
+int sed_batch_device_results(const sed_batch *b, uint64_t *d_dist, uint64_t *d_is_int,
+                             uint64_t *d_len, uint64_t *d_ops, uint64_t *ops_words);
+/* Algorithmic counts of one run: DP cells (sum n*m) and HBM bytes (inputs + traceback + outputs). */
+int sed_batch_work(const sed_batch *b, double *cells, double *algo_bytes);
+
+/* Full DP matrix of one pair (the dp object the GUI renders, StringEditDistance.py:143-224):
+ * D[i*(m+1)+j] = dp[i][j].value, M[...] = optimal incoming edges (1 insert, 2 delete,
+ * 4 update) | (1 << 3 when the value is a Python int).  Always runs the fp64 kernel. */
+int sed_full_matrix(sed_ctx *ctx, const uint8_t *codes_a, int32_t n, const uint8_t *codes_b, int32_t m,
+                    double *D, uint8_t *M);
+
+/* Kernel self-test on the device (DPP lane shifts, byte permute); 0 = pass, else a failure bitmask. */
+int sed_selftest(sed_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SED_H */

@@ -1,0 +1,65 @@
+// sed_internal.h — structures shared by the kernels and the runtime (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SED_MAX_K 32
+
+// Per-pair descriptor in device memory (64 bytes).
+struct sed_pair_desc {
+    uint64_t a_off;    // str1: word offset (integer kernel, 2-bit packed) or byte offset (fp64 kernel)
+    uint64_t b_off;    // str2: same
+    uint64_t tb_off;   // traceback codes: uint32 word offset
+    uint64_t bnd_off;  // stripe bottom-row buffer: uint32 word offset
+    uint64_t ops_off;  // packed script: uint32 word offset
+    int32_t n, m;
+    int32_t pad[4];
+};
+
+// Per-pair result (16 bytes).
+struct sed_result {
+    double dist;     // dp[n][m].value
+    int32_t len;     // ops in the canonical script (L at the sink)
+    uint8_t is_int;  // 1 when the reference's value is a Python int
+    uint8_t pad[3];
+};
+
+// Integer kernel constants: costrow[a] byte b = cost(a -> b); kins = (insert << 16) + 4,
+// kdel = (delete << 16) + 5 (see the key layout in sed_kernels.hip).
+struct sed_i32_params {
+    uint32_t costrow[4];
+    uint32_t kins, kdel;
+    uint32_t ins, del;
+};
+
+struct sed_f64_params {
+    double ins, del;
+    int32_t ins_int, del_int;
+    int32_t K;
+    int32_t pad;
+};
+
+// Full-matrix output (dp proxy materialisation): D[i*(m+1)+j], M = edge mask (1 ins, 2 del, 4 upd) | int << 3.
+struct sed_full_out {
+    double *D;
+    uint8_t *M;
+    int32_t n, m;
+};
+
+struct sed_launch {
+    const sed_pair_desc *pd;
+    int npairs;
+    const void *seqa, *seqb;
+    uint32_t *tb;   // nullptr -> distance only
+    uint32_t *bnd;
+    sed_result *res;
+    int R;
+    hipStream_t stream;
+};
+
+hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm);
+hipError_t sed_launch_f64(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed);
+hipError_t sed_launch_f64_full(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed,
+                               const sed_full_out &fo);
+hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops);
+hipError_t sed_launch_selftest(uint32_t *d_out, hipStream_t stream);

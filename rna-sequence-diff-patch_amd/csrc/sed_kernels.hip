@@ -1,0 +1,630 @@
+// sed_kernels.hip — gfx950 (MI355X / CDNA4) kernels for the weighted
+// Wagner–Fischer DP and its canonical traceback.
+//
+// Reference semantics (plsakr/rna-sequence-diff-patch, StringEditDistance.py):
+//   border cells :146-182, recurrence min_cost :92-128 (candidates insert,
+//   delete, update; one fp64 add each; first minimal value), canonical path =
+//   create_paths(dp)[0] :228-271 (shortest co-optimal path, ties
+//   insert < delete < update read from the sink), script ops :274-334.
+//
+// Work decomposition: one wave64 per sequence pair.  A pair's
+// rows are cut into stripes of 64*R rows; lane t of the wave owns R
+// consecutive rows and sweeps the columns one step behind lane t-1
+// (a systolic anti-diagonal wavefront).  Per step a lane receives the cell
+// above its band from lane t-1 through a DPP wave_shr:1 move, so there is no
+// LDS traffic and no barrier in the inner loop.  Lane 0 takes its "above"
+// value from a 64-entry chunk register that is rotated by DPP wave_rol:1 each
+// step; lane 63's bottom row is collected the same way (wave_shl:1) and written
+// once per 64 steps as the next stripe's top row.
+//
+// Integer kernel (the exact fast path).  When every cost is
+// an integral positive Python float (or the int 0 of a match), the reference's
+// fp64 values are exact integers and the per-cell decision
+//    (distance, path length, op)   lexicographically minimal
+// is one unsigned min over packed keys
+//    V = D << 16 | L << 2 | op,   candidates V_pred + (cost << 16) + 4 + op
+// with op 0 insert, 1 delete, 2 update.  Cells are stored as Y = V >> 2
+// (= D << 14 | L); one v_perm_b32 looks the update cost up from a per-row byte
+// vector, so a cell is 7 VALU instructions: 3 v_lshl_add, v_perm, v_min3,
+// v_lshr and v_alignbit (which packs the 2-bit op for the traceback).
+//
+// fp64 kernel (the general path): fp64 candidates added exactly as the
+// reference does, equality ties, L tie-break on an integer key, and an
+// optional int/float typing bit.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "sed_internal.h"
+
+#define DPP_WAVE_SHL1 0x130  // lane i <- lane i+1, lane 63 keeps `old`
+#define DPP_WAVE_ROL1 0x134  // lane i <- lane i+1, lane 63 <- lane 0
+#define DPP_WAVE_SHR1 0x138  // lane i <- lane i-1, lane 0 keeps `old`
+
+__device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)src, DPP_WAVE_SHR1, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_shl1(uint32_t old, uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)src, DPP_WAVE_SHL1, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_rol1(uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)src, (int)src, DPP_WAVE_ROL1, 0xf, 0xf, false);
+}
+__device__ __forceinline__ double dpp_shr1_f64(double old, double src) {
+    const uint64_t o = __double_as_longlong(old), s = __double_as_longlong(src);
+    const uint32_t lo = dpp_shr1((uint32_t)o, (uint32_t)s);
+    const uint32_t hi = dpp_shr1((uint32_t)(o >> 32), (uint32_t)(s >> 32));
+    return __longlong_as_double(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double dpp_shl1_f64(double old, double src) {
+    const uint64_t o = __double_as_longlong(old), s = __double_as_longlong(src);
+    const uint32_t lo = dpp_shl1((uint32_t)o, (uint32_t)s);
+    const uint32_t hi = dpp_shl1((uint32_t)(o >> 32), (uint32_t)(s >> 32));
+    return __longlong_as_double(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double dpp_rol1_f64(double src) {
+    const uint64_t s = __double_as_longlong(src);
+    const uint32_t lo = dpp_rol1((uint32_t)s), hi = dpp_rol1((uint32_t)(s >> 32));
+    return __longlong_as_double(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) { return min(min(a, b), c); }
+
+// relaxed agent-scope load = global_load sc1: bypasses this CU's L1 so a
+// stripe reads the bottom row its own wave stored during the previous stripe.
+__device__ __forceinline__ uint32_t load_sc1(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t load_sc1_u64(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// tb words a lane stores per 4-step group: 4 steps * R rows * 2 bits / 32.
+template <int R> struct TbWords { static constexpr int N = R / 4; };
+
+template <int NW>
+__device__ __forceinline__ void store_tb(uint32_t *p, const uint32_t (&w)[NW]) {
+    if constexpr (NW == 1) {
+        p[0] = w[0];
+    } else if constexpr (NW == 2) {
+        *reinterpret_cast<uint2 *>(p) = make_uint2(w[0], w[1]);
+    } else {
+#pragma unroll
+        for (int h = 0; h < NW; h += 4)
+            *reinterpret_cast<uint4 *>(p + h) = make_uint4(w[h], w[h + 1], w[h + 2], w[h + 3]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Integer (packed-key) kernel
+// ---------------------------------------------------------------------------
+template <int R, bool TB, bool MASKED>
+__device__ __forceinline__ void i32_step(uint32_t (&Y)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
+                                         uint32_t &bottom, uint32_t &selv, uint32_t &tch, uint32_t &sch,
+                                         uint32_t &outc, uint32_t (&W)[TbWords<R>::N], const int u,
+                                         const uint32_t kins, const uint32_t kdel, const bool active) {
+    const uint32_t topv = dpp_shr1(tch, bottom);  // cell above the band, this column
+    selv = dpp_shr1(sch, selv);                   // perm selector of this column's str2 symbol
+    tch = dpp_rol1(tch);
+    sch = dpp_rol1(sch);
+    uint32_t up = topv, diag = top_prev;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t left = Y[r];
+        const uint32_t ci = (left << 2) + kins;                                  // insert  (op 0)
+        const uint32_t cd = (up << 2) + kdel;                                    // delete  (op 1)
+        const uint32_t cu = (diag << 2) + __builtin_amdgcn_perm(cv[r], 6u, selv);  // update (op 2)
+        const uint32_t mm = umin3(ci, cd, cu);
+        const uint32_t yn = mm >> 2;
+        if constexpr (TB) {
+            const int c = u * R + r;  // compile-time after unrolling
+            W[c >> 4] = __builtin_amdgcn_alignbit(mm, W[c >> 4], 2);
+        }
+        diag = left;
+        up = yn;
+        if constexpr (MASKED) Y[r] = active ? yn : left;
+        else Y[r] = yn;
+    }
+    if constexpr (MASKED) top_prev = active ? topv : top_prev;
+    else top_prev = topv;
+    bottom = Y[R - 1];
+    outc = dpp_shl1(bottom, outc);
+}
+
+template <int R, bool TB, bool MASKED>
+__device__ __forceinline__ void i32_group(uint32_t (&Y)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
+                                          uint32_t &bottom, uint32_t &selv, uint32_t &tch, uint32_t &sch,
+                                          uint32_t &outc, uint32_t (&W)[TbWords<R>::N], const int s0,
+                                          const int lane, const int m, const uint32_t kins, const uint32_t kdel) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int j = s0 + u - lane + 1;  // column this lane computes at step s0+u
+        const bool active = (j >= 1) && (j <= m);
+        i32_step<R, TB, MASKED>(Y, cv, top_prev, bottom, selv, tch, sch, outc, W, u, kins, kdel, active);
+    }
+}
+
+template <int R, bool TB>
+__global__ __launch_bounds__(256) void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
+                                                         const uint32_t *__restrict__ seqa,
+                                                         const uint32_t *__restrict__ seqb,
+                                                         uint32_t *__restrict__ tb, uint32_t *__restrict__ bnd,
+                                                         sed_result *__restrict__ res, sed_i32_params prm) {
+    constexpr int ROWS = 64 * R;
+    constexpr int NW = TbWords<R>::N;
+    const int lane = threadIdx.x & 63;
+    const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (pair >= npairs) return;
+    const sed_pair_desc d = pd[pair];
+    const int n = d.n, m = d.m;
+    if (n == 0 || m == 0) {
+        if (lane == 0) {
+            const uint32_t D = (n == 0) ? (uint32_t)m * prm.ins : (uint32_t)n * prm.del;
+            res[pair].dist = (double)D;
+            res[pair].len = n + m;
+            res[pair].is_int = (D == 0);
+        }
+        return;
+    }
+    const int nstripes = (n + ROWS - 1) / ROWS;
+    const int S4 = (m + 63 + 3) & ~3;
+    const int nchunks = (S4 + 63) >> 6;
+    uint32_t *bndp = bnd + d.bnd_off;
+    const uint32_t *pa = seqa + d.a_off;
+    const uint32_t *pb = seqb + d.b_off;
+
+    for (int k = 0; k < nstripes; ++k) {
+        const int row0 = k * ROWS + lane * R;  // 0-based str1 index of this lane's first row
+        uint32_t cv[R], Y[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int ri = row0 + r;
+            const uint32_t a = (pa[ri >> 4] >> ((ri & 15) * 2)) & 3u;
+            cv[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
+            const uint32_t i = (uint32_t)(ri + 1);
+            Y[r] = ((i * prm.del) << 14) | i;  // column 0: D = i*delete, L = i
+        }
+        uint32_t top_prev = (((uint32_t)row0 * prm.del) << 14) | (uint32_t)row0;
+        uint32_t bottom = 0, selv = 0, outc = 0;
+        uint32_t W[NW];
+#pragma unroll
+        for (int h = 0; h < NW; ++h) W[h] = 0;
+
+        auto load_top = [&](int c) -> uint32_t {
+            const int j = 64 * c + lane + 1;
+            if (k == 0) return (((uint32_t)j * prm.ins) << 14) | (uint32_t)j;  // row 0: D = j*insert, L = j
+            return load_sc1(bndp + j + 64);
+        };
+        auto load_sel = [&](int c) -> uint32_t {
+            const int ci = 64 * c + lane;
+            const uint32_t b = (pb[ci >> 4] >> ((ci & 15) * 2)) & 3u;
+            return 0x0C000100u | ((4u + b) << 16);  // perm: byte2 <- cost byte b, bytes1:0 <- 6
+        };
+        uint32_t tch = load_top(0), sch = load_sel(0);
+        uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(S4 >> 2) * 64u * NW;
+        const bool last = (k == nstripes - 1);
+        int s = 0;
+        for (int c = 0; c < nchunks; ++c) {
+            uint32_t tnx = 0, snx = 0;
+            if (c + 1 < nchunks) { tnx = load_top(c + 1); snx = load_sel(c + 1); }
+            for (int g = 0; g < 16 && s < S4; ++g, s += 4) {
+                const bool full = (s >= 63) && (s + 3 < m);
+                if (full)
+                    i32_group<R, TB, false>(Y, cv, top_prev, bottom, selv, tch, sch, outc, W, s, lane, m,
+                                            prm.kins, prm.kdel);
+                else
+                    i32_group<R, TB, true>(Y, cv, top_prev, bottom, selv, tch, sch, outc, W, s, lane, m,
+                                           prm.kins, prm.kdel);
+                if constexpr (TB) store_tb<NW>(tbk + ((uint64_t)(s >> 2) * 64u + lane) * NW, W);
+            }
+            // lane i holds lane 63's bottom cell of step s-64+i, i.e. column s-126+i at bnd index col+64
+            if (!last) bndp[s - 62 + lane] = outc;
+            tch = tnx;
+            sch = snx;
+        }
+        if (!last) __builtin_amdgcn_s_waitcnt(0);  // own bottom-row stores done before the next stripe reads them
+        else {
+            const int w = (n - 1) % ROWS;
+            if (lane == w / R) {
+                const int rf = w % R;
+                uint32_t y = 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) y = (r == rf) ? Y[r] : y;
+                const uint32_t D = y >> 14;
+                res[pair].dist = (double)D;
+                res[pair].len = (int32_t)(y & 0x3FFFu);
+                res[pair].is_int = (D == 0);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// fp64 kernel (general costs).  State per row: D (fp64), Lk = L << 2,
+// optional int-typing bit T (TYPED).  Cost table in LDS:
+//   tab[a*K + b] = {cost value, is-int flag}
+// ---------------------------------------------------------------------------
+struct f64_cell_in {
+    double d;
+    uint32_t lk;
+    uint32_t t;
+};
+
+template <int R, bool TB, bool TYPED, bool MASKED, bool FULL>
+__device__ __forceinline__ void f64_step(double (&D)[R], uint32_t (&LK)[R], uint32_t (&T)[R],
+                                         const uint32_t (&rowbase)[R], const double2 *__restrict__ tab,
+                                         double &dtop_prev, uint32_t &ltop_prev, uint32_t &ttop_prev,
+                                         double &dbot, uint32_t &lbot, uint32_t &tbot, uint32_t &bsel,
+                                         double &dch, uint32_t &lch, uint32_t &tch, uint32_t &sch, double &doutc,
+                                         uint32_t &loutc, uint32_t &toutc, uint32_t (&W)[TbWords<R>::N], const int u,
+                                         const double cins, const double cdel, const uint32_t tins,
+                                         const uint32_t tdel, const bool active, const sed_full_out &fo,
+                                         const int i0, const int j) {
+    const double dtop = dpp_shr1_f64(dch, dbot);
+    const uint32_t ltop = dpp_shr1(lch, lbot);
+    uint32_t ttop = 0;
+    if constexpr (TYPED) ttop = dpp_shr1(tch, tbot);
+    bsel = dpp_shr1(sch, bsel);
+    dch = dpp_rol1_f64(dch);
+    lch = dpp_rol1(lch);
+    if constexpr (TYPED) tch = dpp_rol1(tch);
+    sch = dpp_rol1(sch);
+    double dup = dtop, ddiag = dtop_prev;
+    uint32_t lup = ltop, ldiag = ltop_prev, tup = ttop, tdiag = ttop_prev;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const double2 e = tab[rowbase[r] + bsel];  // x = cost, y = int flag (as double bits)
+        const double dl = D[r];
+        const double ca = dl + cins;
+        const double cb = dup + cdel;
+        const double cc = ddiag + e.x;
+        const double mn = fmin(ca, fmin(cb, cc));
+        const bool ea = (ca == mn), eb = (cb == mn), ec = (cc == mn);
+        const uint32_t ka = ea ? LK[r] + 4u : 0xFFFFFFFFu;
+        const uint32_t kb = eb ? lup + 5u : 0xFFFFFFFFu;
+        const uint32_t kc = ec ? ldiag + 6u : 0xFFFFFFFFu;
+        const uint32_t km = umin3(ka, kb, kc);
+        const uint32_t ln = km & ~3u;
+        uint32_t tn = 0;
+        if constexpr (TYPED) {
+            const uint32_t tc = (uint32_t)__double_as_longlong(e.y);
+            tn = ea ? (T[r] & tins) : (eb ? (tup & tdel) : (tdiag & tc));
+        }
+        if constexpr (TB) {
+            const int c = u * R + r;
+            W[c >> 4] = __builtin_amdgcn_alignbit(km, W[c >> 4], 2);
+        }
+        if constexpr (FULL) {  // full-matrix materialisation (dp proxy, GUI path): value, edge mask, typing
+            if (active && i0 + r <= fo.n) {
+                const uint64_t o = (uint64_t)(i0 + r) * (uint64_t)(fo.m + 1) + (uint64_t)j;
+                const uint32_t t = TYPED ? tn : (uint32_t)(mn == 0.0);
+                fo.D[o] = mn;
+                fo.M[o] = (uint8_t)((ea ? 1u : 0u) | (eb ? 2u : 0u) | (ec ? 4u : 0u) | (t << 3));
+            }
+        }
+        ddiag = dl;
+        ldiag = LK[r];
+        if constexpr (TYPED) tdiag = T[r];
+        dup = mn;
+        lup = ln;
+        if constexpr (TYPED) tup = tn;
+        if constexpr (MASKED) {
+            D[r] = active ? mn : dl;
+            LK[r] = active ? ln : LK[r];
+            if constexpr (TYPED) T[r] = active ? tn : T[r];
+        } else {
+            D[r] = mn;
+            LK[r] = ln;
+            if constexpr (TYPED) T[r] = tn;
+        }
+    }
+    if constexpr (MASKED) {
+        dtop_prev = active ? dtop : dtop_prev;
+        ltop_prev = active ? ltop : ltop_prev;
+        if constexpr (TYPED) ttop_prev = active ? ttop : ttop_prev;
+    } else {
+        dtop_prev = dtop;
+        ltop_prev = ltop;
+        if constexpr (TYPED) ttop_prev = ttop;
+    }
+    dbot = D[R - 1];
+    lbot = LK[R - 1];
+    if constexpr (TYPED) tbot = T[R - 1];
+    doutc = dpp_shl1_f64(dbot, doutc);
+    loutc = dpp_shl1(lbot, loutc);
+    if constexpr (TYPED) toutc = dpp_shl1(tbot, toutc);
+}
+
+template <int R, bool TB, bool TYPED, bool FULL>
+__global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
+                                                         const uint8_t *__restrict__ seqa,
+                                                         const uint8_t *__restrict__ seqb,
+                                                         uint32_t *__restrict__ tb, uint32_t *__restrict__ bnd,
+                                                         sed_result *__restrict__ res,
+                                                         const double *__restrict__ gtab, sed_f64_params prm,
+                                                         sed_full_out fo) {
+    constexpr int ROWS = 64 * R;
+    constexpr int NW = TbWords<R>::N;
+    __shared__ double2 tab[SED_MAX_K * SED_MAX_K];
+    const int K = prm.K;
+    for (int e = threadIdx.x; e < K * K; e += blockDim.x)
+        tab[e] = make_double2(gtab[2 * e], gtab[2 * e + 1]);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (pair >= npairs) return;
+    const sed_pair_desc d = pd[pair];
+    const int n = d.n, m = d.m;
+    if constexpr (FULL) {  // border cells: row 0 (insert edges) and column 0 (delete edges)
+        for (int j = lane; j <= m; j += 64) {
+            const double v = (double)j * prm.ins;
+            const uint32_t t = (j == 0) ? 1u : (TYPED ? (uint32_t)prm.ins_int : (uint32_t)(v == 0.0));
+            fo.D[j] = v;
+            fo.M[j] = (uint8_t)((j == 0 ? 0u : 1u) | (t << 3));
+        }
+        for (int i = 1 + lane; i <= n; i += 64) {
+            const double v = (double)i * prm.del;
+            const uint32_t t = TYPED ? (uint32_t)prm.del_int : (uint32_t)(v == 0.0);
+            fo.D[(uint64_t)i * (m + 1)] = v;
+            fo.M[(uint64_t)i * (m + 1)] = (uint8_t)(2u | (t << 3));
+        }
+    }
+    if (n == 0 || m == 0) {
+        if (lane == 0) {
+            res[pair].dist = (n == 0) ? (double)m * prm.ins : (double)n * prm.del;
+            res[pair].len = n + m;
+            res[pair].is_int = (n == 0 && m == 0) ? 1 : (n == 0 ? prm.ins_int : prm.del_int);
+        }
+        return;
+    }
+    const int nstripes = (n + ROWS - 1) / ROWS;
+    const int S4 = (m + 63 + 3) & ~3;
+    const int nchunks = (S4 + 63) >> 6;
+    // bottom-row buffer of a pair: [D as u64 | L as u32 | T as u32] planes
+    const uint64_t bwords = (uint64_t)(nchunks + 2) * 64u;
+    uint64_t *bndD = reinterpret_cast<uint64_t *>(bnd + d.bnd_off);
+    uint32_t *bndL = bnd + d.bnd_off + 2 * bwords;
+    uint32_t *bndT = bndL + bwords;
+    const uint8_t *pa = seqa + d.a_off;
+    const uint8_t *pb = seqb + d.b_off;
+    const uint32_t tins = (uint32_t)prm.ins_int, tdel = (uint32_t)prm.del_int;
+
+    for (int k = 0; k < nstripes; ++k) {
+        const int row0 = k * ROWS + lane * R;
+        double D[R];
+        uint32_t LK[R], T[R], rowbase[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int ri = row0 + r;
+            const uint32_t a = (ri < n) ? pa[ri] : 0u;
+            rowbase[r] = a * (uint32_t)K;
+            D[r] = (double)(ri + 1) * prm.del;
+            LK[r] = (uint32_t)(ri + 1) << 2;
+            T[r] = tdel;
+        }
+        double dtop_prev = (double)row0 * prm.del;
+        uint32_t ltop_prev = (uint32_t)row0 << 2;
+        uint32_t ttop_prev = (row0 == 0) ? 1u : tdel;
+        double dbot = 0.0, doutc = 0.0;
+        uint32_t lbot = 0, tbot = 0, bsel = 0, loutc = 0, toutc = 0;
+        uint32_t W[NW];
+#pragma unroll
+        for (int h = 0; h < NW; ++h) W[h] = 0;
+
+        auto load_d = [&](int c) -> double {
+            const int j = 64 * c + lane + 1;
+            if (k == 0) return (double)j * prm.ins;
+            return __longlong_as_double((long long)load_sc1_u64(bndD + j + 64));
+        };
+        auto load_l = [&](int c) -> uint32_t {
+            const int j = 64 * c + lane + 1;
+            if (k == 0) return (uint32_t)j << 2;
+            return load_sc1(bndL + j + 64);
+        };
+        auto load_t = [&](int c) -> uint32_t {
+            if (k == 0) return tins;
+            return load_sc1(bndT + 64 * c + lane + 65);
+        };
+        auto load_sel = [&](int c) -> uint32_t {
+            const int ci = 64 * c + lane;
+            return (ci < m) ? (uint32_t)pb[ci] : 0u;
+        };
+        double dch = load_d(0);
+        uint32_t lch = load_l(0), tch = TYPED ? load_t(0) : 0u, sch = load_sel(0);
+        uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(S4 >> 2) * 64u * NW;
+        const bool last = (k == nstripes - 1);
+        int s = 0;
+        for (int c = 0; c < nchunks; ++c) {
+            double dnx = 0.0;
+            uint32_t lnx = 0, tnx = 0, snx = 0;
+            if (c + 1 < nchunks) {
+                dnx = load_d(c + 1);
+                lnx = load_l(c + 1);
+                if (TYPED) tnx = load_t(c + 1);
+                snx = load_sel(c + 1);
+            }
+            for (int g = 0; g < 16 && s < S4; ++g, s += 4) {
+                const bool full = (s >= 63) && (s + 3 < m);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int j = s + u - lane + 1;
+                    const bool active = (j >= 1) && (j <= m);
+                    if (full)
+                        f64_step<R, TB, TYPED, false, FULL>(D, LK, T, rowbase, tab, dtop_prev, ltop_prev, ttop_prev,
+                                                            dbot, lbot, tbot, bsel, dch, lch, tch, sch, doutc, loutc,
+                                                            toutc, W, u, prm.ins, prm.del, tins, tdel, active, fo,
+                                                            row0 + 1, j);
+                    else
+                        f64_step<R, TB, TYPED, true, FULL>(D, LK, T, rowbase, tab, dtop_prev, ltop_prev, ttop_prev,
+                                                           dbot, lbot, tbot, bsel, dch, lch, tch, sch, doutc, loutc,
+                                                           toutc, W, u, prm.ins, prm.del, tins, tdel, active, fo,
+                                                           row0 + 1, j);
+                }
+                if constexpr (TB) store_tb<NW>(tbk + ((uint64_t)(s >> 2) * 64u + lane) * NW, W);
+            }
+            if (!last) {
+                bndD[s - 62 + lane] = (uint64_t)__double_as_longlong(doutc);
+                bndL[s - 62 + lane] = loutc;
+                if (TYPED) bndT[s - 62 + lane] = toutc;
+            }
+            dch = dnx;
+            lch = lnx;
+            tch = tnx;
+            sch = snx;
+        }
+        if (!last) __builtin_amdgcn_s_waitcnt(0);
+        else {
+            const int w = (n - 1) % ROWS;
+            if (lane == w / R) {
+                const int rf = w % R;
+                double dv = 0.0;
+                uint32_t lv = 0, tv = 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    dv = (r == rf) ? D[r] : dv;
+                    lv = (r == rf) ? LK[r] : lv;
+                    tv = (r == rf) ? T[r] : tv;
+                }
+                res[pair].dist = dv;
+                res[pair].len = (int32_t)(lv >> 2);
+                res[pair].is_int = TYPED ? (uint8_t)tv : (uint8_t)(dv == 0.0);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Traceback: one lane per pair walks the 2-bit choices from (n, m) to (0, 0)
+// and writes the op codes origin->sink, 16 per word.  The 16-byte group of
+// codes a lane stored is cached in registers while the path stays in it.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
+                                                           const uint32_t *__restrict__ tb,
+                                                           const sed_result *__restrict__ res,
+                                                           uint32_t *__restrict__ ops, int R) {
+    const int pair = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pair >= npairs) return;
+    const sed_pair_desc d = pd[pair];
+    const int n = d.n, m = d.m;
+    const int ROWS = 64 * R, NW = R / 4;
+    const int S4 = (m + 63 + 3) & ~3;
+    const uint64_t stripe_words = (uint64_t)(S4 >> 2) * 64u * NW;
+    const uint32_t *tbp = tb + d.tb_off;
+    uint32_t *out = ops + d.ops_off;
+    int q = res[pair].len;  // ops in the script; written from position q-1 down to 0
+    int i = n, j = m;
+    uint32_t acc = 0;
+    uint64_t cached = ~0ull;
+    uint32_t cw = 0;
+    auto emit = [&](uint32_t op) {
+        --q;
+        acc |= op << (2 * (q & 15));
+        if ((q & 15) == 0) {
+            out[q >> 4] = acc;
+            acc = 0;
+        }
+    };
+    while (i > 0 && j > 0) {
+        const int rr = i - 1;
+        const int kk = rr / ROWS, w = rr % ROWS;
+        const int t = w / R, r = w % R;
+        const int s = j - 1 + t;
+        const int c = (s & 3) * R + r;
+        const uint64_t widx = (uint64_t)kk * stripe_words + ((uint64_t)(s >> 2) * 64u + t) * NW + (c >> 4);
+        if (widx != cached) {
+            cw = tbp[widx];
+            cached = widx;
+        }
+        const uint32_t op = (cw >> (2 * (c & 15))) & 3u;
+        emit(op);
+        if (op != 1) --j;
+        if (op != 0) --i;
+    }
+    while (j > 0) { emit(0u); --j; }
+    while (i > 0) { emit(1u); --i; }
+}
+
+// ---------------------------------------------------------------------------
+// Self-test of the cross-lane primitives the kernels rely on.
+// ---------------------------------------------------------------------------
+__global__ void sed_selftest_kernel(uint32_t *out) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t v = 1000u + lane;
+    uint32_t fail = 0;
+    const uint32_t shr = dpp_shr1(7u, v);
+    if (shr != (lane == 0 ? 7u : 999u + lane)) fail |= 1;
+    const uint32_t shl = dpp_shl1(9u, v);
+    if (shl != (lane == 63 ? 9u : 1001u + lane)) fail |= 2;
+    const uint32_t rol = dpp_rol1(v);
+    if (rol != 1000u + ((lane + 1) & 63)) fail |= 4;
+    const uint32_t sel = 0x0C000100u | ((4u + (lane & 3)) << 16);
+    const uint32_t p = __builtin_amdgcn_perm(0x44332211u, 6u, sel);
+    if (p != ((((0x44332211u >> (8 * (lane & 3))) & 0xFFu) << 16) | 6u)) fail |= 8;
+    const uint32_t ab = __builtin_amdgcn_alignbit(0x3u + (lane << 2), 0x80000000u, 2);
+    if (ab != (0xE0000000u | 0x20000000u)) fail |= 16;
+    atomicOr(out, fail);
+}
+
+// ---------------------------------------------------------------------------
+// Launchers (host side, called from sed_runtime.cpp)
+// ---------------------------------------------------------------------------
+template <int R, bool TB>
+static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
+    const int grid = (L.npairs + 3) / 4;
+    hipLaunchKernelGGL((sed_wf_i32_kernel<R, TB>), dim3(grid), dim3(256), 0, L.stream, L.pd, L.npairs,
+                       (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res, prm);
+    return hipGetLastError();
+}
+
+hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm) {
+    const bool tb = L.tb != nullptr;
+    switch (L.R) {
+#define CASE(RR)                                                          \
+    case RR:                                                              \
+        return tb ? launch_i32_R<RR, true>(L, prm) : launch_i32_R<RR, false>(L, prm);
+        CASE(4) CASE(8) CASE(16) CASE(32)
+#undef CASE
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <int R, bool TB, bool TYPED, bool FULL = false>
+static hipError_t launch_f64_R(const sed_launch &L, const double *gtab, const sed_f64_params &prm,
+                               const sed_full_out &fo = sed_full_out{}) {
+    const int grid = (L.npairs + 3) / 4;
+    hipLaunchKernelGGL((sed_wf_f64_kernel<R, TB, TYPED, FULL>), dim3(grid), dim3(256), 0, L.stream, L.pd, L.npairs,
+                       (const uint8_t *)L.seqa, (const uint8_t *)L.seqb, L.tb, L.bnd, L.res, gtab, prm, fo);
+    return hipGetLastError();
+}
+
+hipError_t sed_launch_f64_full(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed,
+                               const sed_full_out &fo) {
+    if (L.R != 4 || L.tb) return hipErrorInvalidValue;
+    return typed ? launch_f64_R<4, false, true, true>(L, gtab, prm, fo)
+                 : launch_f64_R<4, false, false, true>(L, gtab, prm, fo);
+}
+
+hipError_t sed_launch_f64(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed) {
+    const bool tb = L.tb != nullptr;
+    switch (L.R) {
+#define CASE(RR)                                                                                    \
+    case RR:                                                                                        \
+        if (typed) return tb ? launch_f64_R<RR, true, true>(L, gtab, prm)                           \
+                             : launch_f64_R<RR, false, true>(L, gtab, prm);                         \
+        return tb ? launch_f64_R<RR, true, false>(L, gtab, prm) : launch_f64_R<RR, false, false>(L, gtab, prm);
+        CASE(4) CASE(8)
+#undef CASE
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops) {
+    const int grid = (L.npairs + 63) / 64;
+    hipLaunchKernelGGL(sed_traceback_kernel, dim3(grid), dim3(64), 0, L.stream, L.pd, L.npairs, L.tb, L.res, ops,
+                       L.R);
+    return hipGetLastError();
+}
+
+hipError_t sed_launch_selftest(uint32_t *d_out, hipStream_t stream) {
+    hipLaunchKernelGGL(sed_selftest_kernel, dim3(1), dim3(64), 0, stream, d_out);
+    return hipGetLastError();
+}

@@ -1,0 +1,594 @@
+// sed_runtime.cpp — the C-ABI of libsed.so (include/sed.h): contexts, the
+// cost model, mode selection, device-resident batches and the launch sequence
+//   DP kernel (integer or fp64)  ->  traceback kernel
+// on one HIP stream, timed with HIP events recorded on that stream.
+#include "../../include/sed.h"
+#include "sed_internal.h"
+
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    // grow-only; returns false on OOM
+    bool reserve(size_t bytes) {
+        if (bytes <= cap) return true;
+        release();
+        size_t want = std::max<size_t>(bytes, 256);
+        if (hipMalloc(&p, want) != hipSuccess) {
+            p = nullptr;
+            (void)hipGetLastError();
+            return false;
+        }
+        cap = want;
+        return true;
+    }
+};
+
+bool is_integral_small(double v, int lim) { return v == std::floor(v) && v >= 0 && v < lim; }
+
+}  // namespace
+
+struct sed_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // cost model
+    bool have_costs = false;
+    int K = 0;
+    std::vector<double> sub;
+    std::vector<uint8_t> sub_int;
+    double ins = 1, del = 1;
+    int ins_int = 0, del_int = 0;
+    DevBuf gtab;  // fp64 kernel table: per entry {value bits, is-int flag}
+    // options
+    int opt_mode = 0, opt_R = 0;
+    DevBuf selftest;
+    sed_batch *scratch = nullptr;
+
+    int fail(int code, const char *fmt, ...) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        err = buf;
+        return code;
+    }
+    int hipfail(hipError_t e, const char *what) {
+        return fail(SED_E_DEVICE, "%s: %s", what, hipGetErrorString(e));
+    }
+};
+
+struct sed_batch {
+    sed_ctx *ctx = nullptr;
+    int npairs = 0;
+    uint32_t flags = 0;
+    int mode = 0, R = 0;
+    std::vector<sed_pair_desc> pd;
+    std::vector<int32_t> n, m;
+    uint64_t tb_words = 0, bnd_words = 0, ops_words = 0;
+    double cells = 0, algo_bytes = 0;
+    DevBuf d_pd, d_seqa, d_seqb, d_tb, d_bnd, d_res, d_ops;
+    sed_i32_params ip{};
+    sed_f64_params fp{};
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    bool ran = false;
+    std::vector<sed_result> h_res;
+
+    ~sed_batch() {
+        d_pd.release(); d_seqa.release(); d_seqb.release(); d_tb.release();
+        d_bnd.release(); d_res.release(); d_ops.release();
+        for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+};
+
+namespace {
+
+int next_pow2(int x) {
+    int p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// Mode selection.  The packed-integer kernel is exact when
+// every value a cell can add is an integral positive Python float, or the int
+// 0 of a match; then a cell's Python value is an int exactly when it is 0.
+bool i32_eligible(const sed_ctx *c) {
+    if (c->K > 4) return false;
+    if (c->ins_int || c->del_int) return false;
+    if (!is_integral_small(c->ins, 256) || !is_integral_small(c->del, 256) || c->ins < 1 || c->del < 1) return false;
+    for (int e = 0; e < c->K * c->K; ++e) {
+        const double v = c->sub[e];
+        if (c->sub_int[e]) {
+            if (v != 0) return false;
+        } else if (!is_integral_small(v, 256) || v < 1) {
+            return false;
+        }
+    }
+    return true;
+}
+
+// "simple typing": a cell's value is an int exactly when it equals 0.
+bool simple_typing(const sed_ctx *c) {
+    if (c->ins_int || c->del_int || !(c->ins > 0) || !(c->del > 0)) return false;
+    for (int e = 0; e < c->K * c->K; ++e) {
+        if (c->sub_int[e] ? c->sub[e] != 0 : !(c->sub[e] > 0)) return false;
+    }
+    return true;
+}
+
+int choose_R(int mode, int max_n, int forced) {
+    if (forced) return forced;
+    const int want = next_pow2(std::max(1, (max_n + 63) / 64));
+    if (mode == SED_MODE_I32) return std::min(16, std::max(4, want));
+    return std::min(8, std::max(4, want));
+}
+
+int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const int32_t *len_a,
+               const uint8_t *codes_b, const int64_t *off_b, const int32_t *len_b, int32_t npairs,
+               uint32_t flags) {
+    sed_ctx *c = b->ctx;
+    if (!c->have_costs) return c->fail(SED_E_STATE, "sed_set_costs() was not called");
+    if (npairs < 0 || (npairs > 0 && (!codes_a || !off_a || !len_a || !codes_b || !off_b || !len_b)))
+        return c->fail(SED_E_ARG, "bad batch arguments");
+    b->npairs = npairs;
+    b->flags = flags;
+    b->ran = false;
+    b->n.assign(len_a, len_a + npairs);
+    b->m.assign(len_b, len_b + npairs);
+    int max_n = 0, max_m = 0;
+    for (int p = 0; p < npairs; ++p) {
+        if (len_a[p] < 0 || len_b[p] < 0) return c->fail(SED_E_ARG, "negative length at pair %d", p);
+        max_n = std::max(max_n, len_a[p]);
+        max_m = std::max(max_m, len_b[p]);
+        const uint8_t *pa = codes_a + off_a[p], *pb = codes_b + off_b[p];
+        for (int i = 0; i < len_a[p]; ++i)
+            if (pa[i] >= c->K) return c->fail(SED_E_ARG, "code %d >= K at pair %d", pa[i], p);
+        for (int j = 0; j < len_b[p]; ++j)
+            if (pb[j] >= c->K) return c->fail(SED_E_ARG, "code %d >= K at pair %d", pb[j], p);
+    }
+    // ---- mode ----
+    int mode;
+    const bool elig = i32_eligible(c);
+    switch (c->opt_mode) {
+    case 1:
+        if (!elig) return c->fail(SED_E_RANGE, "costs are not eligible for the integer kernel");
+        mode = SED_MODE_I32;
+        break;
+    case 2: mode = simple_typing(c) ? SED_MODE_F64 : SED_MODE_F64_TYPED; break;
+    case 3: mode = SED_MODE_F64_TYPED; break;
+    default: mode = elig ? SED_MODE_I32 : (simple_typing(c) ? SED_MODE_F64 : SED_MODE_F64_TYPED);
+    }
+    int R = choose_R(mode, max_n, c->opt_R);
+    if (mode == SED_MODE_I32) {
+        const int ROWS = 64 * R;
+        bool fits = true;
+        for (int p = 0; p < npairs && fits; ++p) {
+            const double npad = (double)((len_a[p] + ROWS - 1) / ROWS) * ROWS;
+            const double dmax = npad * c->del + (double)len_b[p] * c->ins;
+            if (dmax >= 65536.0 || npad + len_b[p] >= 16384.0) fits = false;
+        }
+        if (!fits) {
+            if (c->opt_mode == 1) return c->fail(SED_E_RANGE, "integer key would overflow (D < 2^16, L < 2^14)");
+            mode = simple_typing(c) ? SED_MODE_F64 : SED_MODE_F64_TYPED;
+            R = choose_R(mode, max_n, c->opt_R);
+        }
+    } else if (c->K > SED_MAX_K) {
+        return c->fail(SED_E_ALPHABET, "alphabet of %d symbols exceeds %d", c->K, SED_MAX_K);
+    }
+    if (mode == SED_MODE_I32 ? !(R == 4 || R == 8 || R == 16 || R == 32) : !(R == 4 || R == 8))
+        return c->fail(SED_E_ARG, "unsupported rows-per-lane %d for mode %d", R, mode);
+    b->mode = mode;
+    b->R = R;
+    const int ROWS = 64 * R;
+    const bool want_tb = (flags & SED_WANT_SCRIPT) != 0;
+
+    // ---- layout ----
+    b->pd.assign(npairs, sed_pair_desc{});
+    uint64_t aw = 0, bw = 0, tbw = 0, bndw = 0, opw = 0;
+    const bool packed = (mode == SED_MODE_I32);
+    double cells = 0, in_bytes = 0, tb_bytes = 0;
+    for (int p = 0; p < npairs; ++p) {
+        const int nn = len_a[p], mm = len_b[p];
+        sed_pair_desc &d = b->pd[p];
+        d.n = nn;
+        d.m = mm;
+        d.a_off = aw;
+        d.b_off = bw;
+        if (packed) {
+            aw += (nn + 15) / 16;
+            bw += (mm + 15) / 16;
+        } else {
+            aw += nn;
+            bw += mm;
+        }
+        d.tb_off = tbw;
+        d.bnd_off = bndw;
+        d.ops_off = opw;
+        if (nn > 0 && mm > 0) {
+            const uint64_t nstripes = (nn + ROWS - 1) / ROWS;
+            const uint64_t S4 = (mm + 63 + 3) & ~3ull;
+            const uint64_t nchunks = (S4 + 63) / 64;
+            if (want_tb) tbw += nstripes * (S4 / 4) * 64 * (R / 4);
+            if (nstripes > 1) bndw += (nchunks + 2) * 64 * (packed ? 1 : 4);
+        }
+        opw += (uint64_t)(nn + mm + 15) / 16;
+        cells += (double)nn * mm;
+        in_bytes += packed ? (nn + mm) / 4.0 : (double)(nn + mm);
+    }
+    tb_bytes = cells * 0.25;
+    b->tb_words = tbw;
+    b->bnd_words = bndw;
+    b->ops_words = opw;
+    b->cells = cells;
+    b->algo_bytes = in_bytes + (want_tb ? tb_bytes : 0) + 16.0 * npairs;
+
+    // ---- pack & upload ----
+    const uint64_t pad_words = (uint64_t)ROWS / 16 * 2 + 64;
+    std::vector<uint32_t> ha, hb;
+    std::vector<uint8_t> ha8, hb8;
+    if (packed) {
+        ha.assign(aw + pad_words, 0);
+        hb.assign(bw + pad_words, 0);
+        for (int p = 0; p < npairs; ++p) {
+            const uint8_t *pa = codes_a + off_a[p], *pb = codes_b + off_b[p];
+            uint32_t *qa = ha.data() + b->pd[p].a_off, *qb = hb.data() + b->pd[p].b_off;
+            for (int i = 0; i < len_a[p]; ++i) qa[i >> 4] |= (uint32_t)pa[i] << (2 * (i & 15));
+            for (int j = 0; j < len_b[p]; ++j) qb[j >> 4] |= (uint32_t)pb[j] << (2 * (j & 15));
+        }
+    } else {
+        ha8.assign(aw + 64, 0);
+        hb8.assign(bw + 64, 0);
+        for (int p = 0; p < npairs; ++p) {
+            if (len_a[p]) memcpy(ha8.data() + b->pd[p].a_off, codes_a + off_a[p], len_a[p]);
+            if (len_b[p]) memcpy(hb8.data() + b->pd[p].b_off, codes_b + off_b[p], len_b[p]);
+        }
+    }
+    const size_t sa = packed ? ha.size() * 4 : ha8.size(), sb = packed ? hb.size() * 4 : hb8.size();
+    if (!b->d_pd.reserve(sizeof(sed_pair_desc) * std::max(1, npairs)) || !b->d_seqa.reserve(sa) ||
+        !b->d_seqb.reserve(sb) || !b->d_res.reserve(sizeof(sed_result) * std::max(1, npairs)) ||
+        !b->d_ops.reserve(4 * std::max<uint64_t>(1, opw)) || !b->d_bnd.reserve(4 * std::max<uint64_t>(1, bndw)) ||
+        (want_tb && !b->d_tb.reserve(4 * std::max<uint64_t>(1, tbw))))
+        return c->fail(SED_E_OOM, "device allocation failed (traceback %.3f GB)", 4.0 * tbw / 1e9);
+    hipError_t e;
+    if ((e = hipMemcpyAsync(b->d_pd.p, b->pd.data(), sizeof(sed_pair_desc) * npairs, hipMemcpyHostToDevice,
+                            c->stream)) != hipSuccess)
+        return c->hipfail(e, "upload descriptors");
+    if ((e = hipMemcpyAsync(b->d_seqa.p, packed ? (void *)ha.data() : (void *)ha8.data(), sa, hipMemcpyHostToDevice,
+                            c->stream)) != hipSuccess)
+        return c->hipfail(e, "upload str1");
+    if ((e = hipMemcpyAsync(b->d_seqb.p, packed ? (void *)hb.data() : (void *)hb8.data(), sb, hipMemcpyHostToDevice,
+                            c->stream)) != hipSuccess)
+        return c->hipfail(e, "upload str2");
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hipfail(e, "upload sync");
+
+    // ---- kernel parameters ----
+    if (mode == SED_MODE_I32) {
+        sed_i32_params ip{};
+        for (int a = 0; a < 4; ++a) {
+            uint32_t row = 0;
+            for (int bb = 0; bb < 4; ++bb) {
+                const double v = (a < c->K && bb < c->K) ? c->sub[a * c->K + bb] : 0.0;
+                row |= (uint32_t)v << (8 * bb);
+            }
+            ip.costrow[a] = row;
+        }
+        ip.ins = (uint32_t)c->ins;
+        ip.del = (uint32_t)c->del;
+        ip.kins = (ip.ins << 16) + 4u;
+        ip.kdel = (ip.del << 16) + 5u;
+        b->ip = ip;
+    } else {
+        sed_f64_params fp{};
+        fp.ins = c->ins;
+        fp.del = c->del;
+        fp.ins_int = c->ins_int;
+        fp.del_int = c->del_int;
+        fp.K = c->K;
+        b->fp = fp;
+    }
+    for (auto &ev : b->ev)
+        if (!ev && (e = hipEventCreate(&ev)) != hipSuccess) return c->hipfail(e, "event create");
+    return SED_OK;
+}
+
+int run_batch(sed_batch *b) {
+    sed_ctx *c = b->ctx;
+    if (b->npairs == 0) {
+        b->ran = true;
+        return SED_OK;
+    }
+    sed_launch L{};
+    L.pd = (const sed_pair_desc *)b->d_pd.p;
+    L.npairs = b->npairs;
+    L.seqa = b->d_seqa.p;
+    L.seqb = b->d_seqb.p;
+    L.tb = (b->flags & SED_WANT_SCRIPT) ? (uint32_t *)b->d_tb.p : nullptr;
+    L.bnd = (uint32_t *)b->d_bnd.p;
+    L.res = (sed_result *)b->d_res.p;
+    L.R = b->R;
+    L.stream = c->stream;
+    hipError_t e;
+    if ((e = hipEventRecord(b->ev[0], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
+    if (b->mode == SED_MODE_I32)
+        e = sed_launch_i32(L, b->ip);
+    else
+        e = sed_launch_f64(L, (const double *)c->gtab.p, b->fp, b->mode == SED_MODE_F64_TYPED);
+    if (e != hipSuccess) return c->hipfail(e, "DP kernel launch");
+    if ((e = hipEventRecord(b->ev[1], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
+    if (L.tb) {
+        if ((e = sed_launch_traceback(L, (uint32_t *)b->d_ops.p)) != hipSuccess)
+            return c->hipfail(e, "traceback kernel launch");
+    }
+    if ((e = hipEventRecord(b->ev[2], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
+    b->ran = true;
+    return SED_OK;
+}
+
+int fetch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32_t *out_len, uint32_t *out_ops,
+                  const int64_t *ops_off) {
+    sed_ctx *c = b->ctx;
+    if (!b->ran) return c->fail(SED_E_STATE, "batch has not been run");
+    const int np = b->npairs;
+    hipError_t e;
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hipfail(e, "kernel execution");
+    b->h_res.resize(np);
+    if (np && (e = hipMemcpy(b->h_res.data(), b->d_res.p, sizeof(sed_result) * np, hipMemcpyDeviceToHost)) !=
+                  hipSuccess)
+        return c->hipfail(e, "download results");
+    for (int p = 0; p < np; ++p) {
+        if (out_dist) out_dist[p] = b->h_res[p].dist;
+        if (out_is_int) out_is_int[p] = b->h_res[p].is_int;
+        if (out_len) out_len[p] = b->h_res[p].len;
+    }
+    if (out_ops && ops_off && (b->flags & SED_WANT_SCRIPT) && np) {
+        std::vector<uint32_t> h(b->ops_words);
+        if ((e = hipMemcpy(h.data(), b->d_ops.p, 4 * b->ops_words, hipMemcpyDeviceToHost)) != hipSuccess)
+            return c->hipfail(e, "download scripts");
+        for (int p = 0; p < np; ++p) {
+            const uint64_t words = (uint64_t)(b->n[p] + b->m[p] + 15) / 16;
+            memcpy(out_ops + ops_off[p], h.data() + b->pd[p].ops_off, 4 * words);
+        }
+    }
+    return SED_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *sed_version(void) { return "libsed 0.1 (gfx950)"; }
+
+sed_ctx *sed_create(int device) {
+    if (hipSetDevice(device) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    sed_ctx *c = new sed_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+void sed_destroy(sed_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    delete c->scratch;
+    c->gtab.release();
+    c->selftest.release();
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char *sed_last_error(const sed_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int sed_set_option(sed_ctx *c, int key, int value) {
+    if (!c) return SED_E_ARG;
+    if (key == SED_OPT_MODE && value >= 0 && value <= 3) {
+        c->opt_mode = value;
+        return SED_OK;
+    }
+    if (key == SED_OPT_ROWS_PER_LANE && (value == 0 || value == 1 || value == 2 || value == 4 || value == 8 ||
+                                         value == 16 || value == 32)) {
+        c->opt_R = value;
+        return SED_OK;
+    }
+    return c->fail(SED_E_ARG, "bad option %d=%d", key, value);
+}
+
+int sed_set_costs(sed_ctx *c, int K, const double *sub, const uint8_t *sub_int, double ins, int ins_is_int,
+                  double del, int del_is_int) {
+    if (!c) return SED_E_ARG;
+    if (K < 1 || K > 255 || !sub || !sub_int) return c->fail(SED_E_ARG, "bad cost table (K=%d)", K);
+    if (!std::isfinite(ins) || !std::isfinite(del)) return c->fail(SED_E_ARG, "non-finite insert/delete cost");
+    for (int e = 0; e < K * K; ++e)
+        if (!std::isfinite(sub[e])) return c->fail(SED_E_ARG, "non-finite update cost at %d", e);
+    (void)hipSetDevice(c->device);
+    c->K = K;
+    c->sub.assign(sub, sub + K * K);
+    c->sub_int.assign(sub_int, sub_int + K * K);
+    c->ins = ins;
+    c->del = del;
+    c->ins_int = ins_is_int ? 1 : 0;
+    c->del_int = del_is_int ? 1 : 0;
+    if (K <= SED_MAX_K) {
+        std::vector<uint64_t> t(2 * K * K);
+        for (int e = 0; e < K * K; ++e) {
+            memcpy(&t[2 * e], &sub[e], 8);
+            t[2 * e + 1] = sub_int[e] ? 1 : 0;
+        }
+        if (!c->gtab.reserve(t.size() * 8)) return c->fail(SED_E_OOM, "cost table allocation");
+        hipError_t e = hipMemcpy(c->gtab.p, t.data(), t.size() * 8, hipMemcpyHostToDevice);
+        if (e != hipSuccess) return c->hipfail(e, "upload cost table");
+    }
+    c->have_costs = true;
+    return SED_OK;
+}
+
+sed_batch *sed_batch_create(sed_ctx *c, const uint8_t *codes_a, const int64_t *off_a, const int32_t *len_a,
+                            const uint8_t *codes_b, const int64_t *off_b, const int32_t *len_b, int32_t npairs,
+                            uint32_t flags) {
+    if (!c) return nullptr;
+    (void)hipSetDevice(c->device);
+    sed_batch *b = new sed_batch();
+    b->ctx = c;
+    if (fill_batch(b, codes_a, off_a, len_a, codes_b, off_b, len_b, npairs, flags) != SED_OK) {
+        delete b;
+        return nullptr;
+    }
+    return b;
+}
+
+void sed_batch_destroy(sed_batch *b) {
+    if (!b) return;
+    (void)hipSetDevice(b->ctx->device);
+    delete b;
+}
+
+int sed_batch_mode(const sed_batch *b) { return b ? b->mode : SED_E_ARG; }
+int sed_batch_rows_per_lane(const sed_batch *b) { return b ? b->R : SED_E_ARG; }
+
+int sed_batch_run(sed_batch *b) {
+    if (!b) return SED_E_ARG;
+    (void)hipSetDevice(b->ctx->device);
+    return run_batch(b);
+}
+
+int sed_batch_sync(sed_batch *b) {
+    if (!b) return SED_E_ARG;
+    hipError_t e = hipStreamSynchronize(b->ctx->stream);
+    return e == hipSuccess ? SED_OK : b->ctx->hipfail(e, "stream sync");
+}
+
+int sed_batch_last_times(const sed_batch *b, float *dp_ms, float *tb_ms) {
+    if (!b || !b->ran) return SED_E_STATE;
+    float a = 0, t = 0;
+    if (b->npairs) {
+        if (hipEventElapsedTime(&a, b->ev[0], b->ev[1]) != hipSuccess) return SED_E_DEVICE;
+        if (hipEventElapsedTime(&t, b->ev[1], b->ev[2]) != hipSuccess) return SED_E_DEVICE;
+    }
+    if (dp_ms) *dp_ms = a;
+    if (tb_ms) *tb_ms = t;
+    return SED_OK;
+}
+
+int sed_batch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32_t *out_len, uint32_t *out_ops,
+                      const int64_t *ops_off) {
+    if (!b) return SED_E_ARG;
+    (void)hipSetDevice(b->ctx->device);
+    return fetch_results(b, out_dist, out_is_int, out_len, out_ops, ops_off);
+}
+
+int sed_batch_device_results(const sed_batch *b, uint64_t *d_dist, uint64_t *d_is_int, uint64_t *d_len,
+                             uint64_t *d_ops, uint64_t *ops_words) {
+    if (!b) return SED_E_ARG;
+    const uint64_t base = (uint64_t)(uintptr_t)b->d_res.p;
+    if (d_dist) *d_dist = base + offsetof(sed_result, dist);
+    if (d_len) *d_len = base + offsetof(sed_result, len);
+    if (d_is_int) *d_is_int = base + offsetof(sed_result, is_int);
+    if (d_ops) *d_ops = (uint64_t)(uintptr_t)b->d_ops.p;
+    if (ops_words) *ops_words = b->ops_words;
+    return SED_OK;
+}
+
+int sed_batch_work(const sed_batch *b, double *cells, double *algo_bytes) {
+    if (!b) return SED_E_ARG;
+    if (cells) *cells = b->cells;
+    if (algo_bytes) *algo_bytes = b->algo_bytes;
+    return SED_OK;
+}
+
+int sed_run_batch(sed_ctx *c, const uint8_t *codes_a, const int64_t *off_a, const int32_t *len_a,
+                  const uint8_t *codes_b, const int64_t *off_b, const int32_t *len_b, int32_t npairs, uint32_t flags,
+                  double *out_dist, uint8_t *out_is_int, int32_t *out_len, uint32_t *out_ops,
+                  const int64_t *ops_off) {
+    if (!c) return SED_E_ARG;
+    (void)hipSetDevice(c->device);
+    if (!c->scratch) {
+        c->scratch = new sed_batch();
+        c->scratch->ctx = c;
+    }
+    int rc = fill_batch(c->scratch, codes_a, off_a, len_a, codes_b, off_b, len_b, npairs, flags);
+    if (rc != SED_OK) return rc;
+    if ((rc = run_batch(c->scratch)) != SED_OK) return rc;
+    return fetch_results(c->scratch, out_dist, out_is_int, out_len, out_ops, ops_off);
+}
+
+int sed_full_matrix(sed_ctx *c, const uint8_t *codes_a, int32_t n, const uint8_t *codes_b, int32_t m, double *D,
+                    uint8_t *M) {
+    if (!c) return SED_E_ARG;
+    if (n < 0 || m < 0 || !D || !M || (n && !codes_a) || (m && !codes_b)) return c->fail(SED_E_ARG, "bad arguments");
+    (void)hipSetDevice(c->device);
+    if (!c->have_costs) return c->fail(SED_E_STATE, "sed_set_costs() was not called");
+    const int save_mode = c->opt_mode, save_R = c->opt_R;
+    c->opt_mode = simple_typing(c) ? 2 : 3;
+    c->opt_R = 4;
+    sed_batch tmp;
+    tmp.ctx = c;
+    const int64_t zero = 0;
+    int rc = fill_batch(&tmp, codes_a, &zero, &n, codes_b, &zero, &m, 1, 0);
+    c->opt_mode = save_mode;
+    c->opt_R = save_R;
+    if (rc != SED_OK) return rc;
+    const size_t cells = (size_t)(n + 1) * (size_t)(m + 1);
+    DevBuf fD, fM;
+    if (!fD.reserve(8 * cells) || !fM.reserve(cells)) {
+        fD.release();
+        fM.release();
+        return c->fail(SED_E_OOM, "full matrix allocation (%zu cells)", cells);
+    }
+    sed_launch L{};
+    L.pd = (const sed_pair_desc *)tmp.d_pd.p;
+    L.npairs = 1;
+    L.seqa = tmp.d_seqa.p;
+    L.seqb = tmp.d_seqb.p;
+    L.tb = nullptr;
+    L.bnd = (uint32_t *)tmp.d_bnd.p;
+    L.res = (sed_result *)tmp.d_res.p;
+    L.R = 4;
+    L.stream = c->stream;
+    sed_full_out fo{(double *)fD.p, (uint8_t *)fM.p, n, m};
+    hipError_t e = sed_launch_f64_full(L, (const double *)c->gtab.p, tmp.fp, tmp.mode == SED_MODE_F64_TYPED, fo);
+    if (e == hipSuccess) e = hipMemcpyAsync(D, fD.p, 8 * cells, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(M, fM.p, cells, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    fD.release();
+    fM.release();
+    return e == hipSuccess ? SED_OK : c->hipfail(e, "full matrix");
+}
+
+int sed_selftest(sed_ctx *c) {
+    if (!c) return SED_E_ARG;
+    (void)hipSetDevice(c->device);
+    if (!c->selftest.reserve(4)) return c->fail(SED_E_OOM, "selftest buffer");
+    hipError_t e;
+    uint32_t h = 0;
+    if ((e = hipMemsetAsync(c->selftest.p, 0, 4, c->stream)) != hipSuccess) return c->hipfail(e, "memset");
+    if ((e = sed_launch_selftest((uint32_t *)c->selftest.p, c->stream)) != hipSuccess) return c->hipfail(e, "launch");
+    if ((e = hipMemcpyAsync(&h, c->selftest.p, 4, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+        return c->hipfail(e, "copy");
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hipfail(e, "sync");
+    return (int)h;
+}
+
+}  // extern "C"

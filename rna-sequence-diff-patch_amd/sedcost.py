@@ -1,0 +1,141 @@
+"""Cost tables -> per-call alphabet codes and a K x K cost matrix.
+
+Host-side half of the reference's cost model (StringEditDistance.py:6-27,
+76-99).  The reference looks costs up per DP cell in a dict of dicts; the
+engine instead resolves, once per call, every (str1 symbol, str2 symbol)
+combination into
+
+    sub[a][b]      the value cost(a, b) returns (int 0 when a.lower() == b.lower())
+    sub_int[a][b]  1 when that value is a Python int (typing of dp values)
+
+and raises the same KeyError the reference would raise at the first offending
+cell in row-major order (insert / delete keys first, as the border loops read
+them before any update lookup, StringEditDistance.py:156,174).
+"""
+import numpy as np
+
+UPDATE, INSERT, DELETE = "update", "insert", "delete"
+
+
+def _is_py_int(v):
+    return isinstance(v, int)
+
+
+class CostPlan:
+    """Alphabet + resolved cost matrix for a set of (str1, str2) pairs."""
+
+    __slots__ = ("alphabet", "code", "sub", "sub_int", "ins", "ins_int", "dele", "del_int", "_key", "_lut")
+
+    def __init__(self, alphabet, sub, sub_int, ins, ins_int, dele, del_int):
+        self.alphabet = alphabet
+        self.code = {c: k for k, c in enumerate(alphabet)}
+        self.sub = sub
+        self.sub_int = sub_int
+        self.ins, self.ins_int, self.dele, self.del_int = ins, ins_int, dele, del_int
+        self._key = (tuple(alphabet), sub.tobytes(), sub_int.tobytes(), ins, ins_int, dele, del_int)
+        lut = np.full(256, 255, dtype=np.uint8)
+        for c, k in self.code.items():
+            if len(c) == 1 and ord(c) < 256:
+                lut[ord(c)] = k
+        self._lut = lut
+
+    @property
+    def K(self):
+        return len(self.alphabet)
+
+    def key(self):
+        return self._key
+
+    def encode(self, s):
+        """uint8 codes of a sequence whose symbols are all in the alphabet."""
+        if isinstance(s, str):
+            try:
+                raw = np.frombuffer(s.encode("latin-1"), dtype=np.uint8)
+                out = self._lut[raw]
+                if not (out == 255).any():
+                    return out
+            except UnicodeEncodeError:
+                pass
+        return np.fromiter((self.code[c] for c in s), dtype=np.uint8, count=len(s))
+
+
+def _scalar(table, key):
+    v = table[key]  # KeyError(key) exactly like the reference
+    return float(v), 1 if _is_py_int(v) else 0
+
+
+def check_pair(table, s1, s2):
+    """Raise the reference's exception for wagnerFisher(s1, s2), if any.
+
+    Order (StringEditDistance.py:146-222): row 0 reads table['insert'] when
+    len(s2) >= 1, column 0 reads table['delete'] when len(s1) >= 1, then the
+    interior cells in row-major order call cost(s1[i-1], s2[j-1]).
+    """
+    n, m = len(s1), len(s2)
+    if m >= 1:
+        table[INSERT]
+    if n >= 1:
+        table[DELETE]
+    if n == 0 or m == 0:
+        return
+    first_j = {}
+    for j, c in enumerate(s2):
+        first_j.setdefault(c, j)
+    bad = {}  # str1 symbol -> (first offending j, exception)
+    for a in dict.fromkeys(s1):
+        best = None
+        for b, j in first_j.items():
+            if a.lower() == b.lower():
+                continue
+            try:
+                table[UPDATE][a][b]
+            except KeyError as ex:
+                if best is None or j < best[0]:
+                    best = (j, ex)
+        if best is not None:
+            bad[a] = best
+    if not bad:
+        return
+    for a in s1:
+        if a in bad:
+            raise bad[a][1]
+
+
+def build_plan(table, strs1, strs2):
+    """CostPlan over the union alphabet of the given sequences (already checked)."""
+    seen = {}
+    for s in strs1:
+        for c in dict.fromkeys(s):
+            seen.setdefault(c, 0)
+    syms1 = list(seen)
+    seen2 = {}
+    for s in strs2:
+        for c in dict.fromkeys(s):
+            seen2.setdefault(c, 0)
+    alphabet = syms1 + [c for c in seen2 if c not in seen]
+    set1, set2 = set(syms1), set(seen2)
+    K = len(alphabet)
+    sub = np.zeros((K, K), dtype=np.float64)
+    sub_int = np.ones((K, K), dtype=np.uint8)  # unreachable combinations: int 0
+    upd = None
+    for a_i, a in enumerate(alphabet):
+        if a not in set1:
+            continue
+        for b_i, b in enumerate(alphabet):
+            if b not in set2 or a.lower() == b.lower():
+                continue
+            if upd is None:
+                upd = table[UPDATE]
+            row = upd.get(a) if hasattr(upd, "get") else None
+            if row is None or b not in row:
+                continue  # never met as a (str1, str2) cell of a checked pair
+            v = row[b]
+            sub[a_i, b_i] = float(v)
+            sub_int[a_i, b_i] = 1 if _is_py_int(v) else 0
+    ins, ins_int = _scalar(table, INSERT) if INSERT in table else (1.0, 0)
+    dele, del_int = _scalar(table, DELETE) if DELETE in table else (1.0, 0)
+    if not K:
+        alphabet = ["A"]
+        sub = np.zeros((1, 1))
+        sub_int = np.ones((1, 1), dtype=np.uint8)
+    return CostPlan(alphabet, sub, sub_int, ins, ins_int, dele, del_int)

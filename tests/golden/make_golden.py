@@ -1,0 +1,292 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by importing the REFERENCE.
+
+This script runs only in the build container (it needs /root/reference); the
+fixtures it writes are small JSON files that travel with the repo.  Nothing on
+the GPU box reads /root/reference.
+
+    python -B tests/golden/make_golden.py            # G1, G2, G4, G5, G6
+    python -B tests/golden/make_golden.py --g3       # the 4096^2 config-2 pair (~2 min, ~12 GB RAM)
+
+Fixture sets:
+  G1  small pairs, every co-optimal path in reference order (create_paths),
+      the full DP matrix (value, int-typing, optimal-edge mask) and the ES list.
+  G2  medium pairs: distance, canonical ES and a digest of the full matrix.  The
+      canonical path is walked on the reference's OWN dp graph with the
+      (L, insert<delete<update) rule, which G1 verifies equals create_paths(dp)[0].
+  G3  config-2 pair (4096x4096 synthetic ACGU, user_costs): distance + canonical ES.
+  G4  25x25 wf_score matrix over test_input.xml (IRMethods.wf_score).
+  G5  generate_rev_es / generate_sequence_from_es / patching cases.
+  G6  error and typing cases (KeyError, IndexError, int-zero typing).
+"""
+import hashlib
+import io
+import json
+import os
+import random
+import signal
+import sys
+import contextlib
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "rna-sequence-diff-patch_amd"))
+import synth  # noqa: E402
+
+OPS = {"insert": "i", "delete": "d", "update": "u"}
+MASK = {"insert": 1, "delete": 2, "update": 4}
+IUPAC = "AGCUYRWSKMDVHBN"
+
+
+def load_reference():
+    os.chdir(REF)
+    sys.path.insert(0, REF)
+    with contextlib.redirect_stdout(io.StringIO()):
+        import StringEditDistance as S  # prints its smoke block on import
+        import IRMethods as IR
+        import import_xml as IX
+    return S, IR, IX
+
+
+def vrec(v):
+    return [float(v).hex(), isinstance(v, int) and not isinstance(v, bool)]
+
+
+def cell_mask(node):
+    m = 0
+    for e in node.incoming_edges:
+        m |= MASK[e.operation]
+    return m
+
+
+def path_ops(path):
+    out = []
+    for a, b in zip(path, path[1:]):
+        di, dj = b.i - a.i, b.j - a.j
+        out.append("u" if (di, dj) == (1, 1) else ("d" if di == 1 else "i"))
+    return "".join(out)
+
+
+def es_compact(es):
+    return [[OPS[e["operation"]], e["source"]["character"], e["source"]["index"],
+             e["destination"]["character"], e["destination"]["index"]] for e in es]
+
+
+def canonical_from_graph(dp):
+    """Shortest co-optimal path, ties insert<delete<update read from the sink.
+
+    Computed on the reference's own Node graph: L = min edge count from the
+    origin over optimal (incoming) edges; at each cell take the first incoming
+    edge (they are stored insert, delete, update) whose source has L = L-1.
+    Returns the node path origin->sink.
+    """
+    rows, cols = len(dp), len(dp[0])
+    L = [[0] * cols for _ in range(rows)]
+    for i in range(rows):
+        for j in range(cols):
+            if i == 0 and j == 0:
+                continue
+            n = dp[i][j]
+            L[i][j] = 1 + min(L[e.source.i + 1][e.source.j + 1] for e in n.incoming_edges)
+    i, j = rows - 1, cols - 1
+    path = [dp[i][j]]
+    while (i, j) != (0, 0):
+        n = dp[i][j]
+        for e in n.incoming_edges:
+            si, sj = e.source.i + 1, e.source.j + 1
+            if L[si][sj] == L[i][j] - 1:
+                i, j = si, sj
+                break
+        path.append(dp[i][j])
+    return path[::-1], L[rows - 1][cols - 1]
+
+
+def matrix_digest(dp):
+    h = hashlib.sha256()
+    for row in dp:
+        for n in row:
+            h.update(("%s|%d|%d;" % (float(n.value).hex(), int(isinstance(n.value, int)), cell_mask(n))).encode())
+    return h.hexdigest()
+
+
+class _Timeout(Exception):
+    pass
+
+
+def _alarm(signum, frame):
+    raise _Timeout()
+
+
+def create_paths_or_deadlock(S, dp, seconds=0.5):
+    signal.signal(signal.SIGALRM, _alarm)
+    signal.setitimer(signal.ITIMER_REAL, seconds)
+    try:
+        return S.create_paths(dp)
+    except _Timeout:
+        return None
+    finally:
+        signal.setitimer(signal.ITIMER_REAL, 0)
+
+
+def rand_str(rng, alphabet, lo, hi):
+    return "".join(rng.choice(alphabet) for _ in range(rng.randint(lo, hi)))
+
+
+def gen_g1(S):
+    rng = random.Random(1015)
+    cases = []
+    for user in (False, True):
+        for alpha in ("ACGU", IUPAC):
+            for _ in range(110):
+                s1, s2 = rand_str(rng, alpha, 0, 7), rand_str(rng, alpha, 0, 7)
+                cases.append((s1, s2, user))
+    # a few hand-picked ones: the survey's deadlock example and the smoke block
+    cases += [("ACGCGCG", "UUU", False), ("AGRGA", "AGGGAA", True), ("A", "CA", False),
+              ("", "", False), ("", "ACG", True), ("GU", "", False), ("AAAA", "AAAA", False)]
+    out = []
+    for s1, s2, user in cases:
+        dp = S.wagnerFisher(s1, s2, user)
+        rec = {"s1": s1, "s2": s2, "user": user, "dist": vrec(dp[-1][-1].value),
+               "cells": [[*vrec(n.value), cell_mask(n)] for row in dp for n in row]}
+        cpath, clen = canonical_from_graph(dp)
+        rec["canon"] = path_ops(cpath)
+        paths = create_paths_or_deadlock(S, dp)
+        if paths is None:
+            rec["paths"] = "deadlock"
+        else:
+            ops = [path_ops(p) for p in paths]
+            assert ops[0] == rec["canon"], (s1, s2, user)
+            rec["npaths"] = len(ops)
+            rec["paths"] = ops[:400]
+            es_list = []
+            for p in paths[:6]:
+                try:
+                    es_list.append(es_compact(S.generate_es(p, s1, s2)))
+                except Exception as ex:  # IndexError on empty strings
+                    es_list.append({"error": type(ex).__name__})
+            rec["es"] = es_list
+        out.append(rec)
+    return out
+
+
+def gen_g2(S):
+    specs = []
+    for n, m in ((64, 64), (96, 64), (256, 256), (200, 300)):
+        for user in (False, True):
+            specs.append(("rand", "ACGU", n, m, user))
+            specs.append(("related", "ACGU", n, n, user))
+            specs.append(("rand", IUPAC, n, m, user))
+    specs += [("rand", "ACGU", 1024, 1024, True), ("related", "ACGU", 1024, 1024, False),
+              ("rand", IUPAC, 1024, 1024, False)]
+    rng = random.Random(2026)
+    out = []
+    for kind, alpha, n, m, user in specs:
+        s1 = "".join(rng.choice(alpha) for _ in range(n))
+        if kind == "related":
+            s2 = "".join(c if rng.random() >= 0.1 else rng.choice(alpha) for c in s1)
+        else:
+            s2 = "".join(rng.choice(alpha) for _ in range(m))
+        dp = S.wagnerFisher(s1, s2, user)
+        cpath, clen = canonical_from_graph(dp)
+        es = S.generate_es(cpath, s1, s2)
+        out.append({"s1": s1, "s2": s2, "user": user, "kind": kind,
+                    "dist": vrec(dp[-1][-1].value), "canon": path_ops(cpath), "len": clen,
+                    "es_sha256": hashlib.sha256(json.dumps(es_compact(es)).encode()).hexdigest(),
+                    "digest": matrix_digest(dp)})
+        print("G2", kind, len(alpha), n, m, user, out[-1]["dist"], file=sys.stderr)
+    return out
+
+
+def gen_g3(S):
+    s1, s2 = synth.pair_strings(0, 4096, 4096)
+    dp = S.wagnerFisher(s1, s2, True)
+    cpath, clen = canonical_from_graph(dp)
+    ops = path_ops(cpath)
+    es = es_compact(S.generate_es(cpath, s1, s2))
+    return {"pair_id": 0, "base_seed": synth.BASE_SEED, "n": 4096, "m": 4096, "user": True,
+            "s1_sha256": hashlib.sha256(s1.encode()).hexdigest(),
+            "s2_sha256": hashlib.sha256(s2.encode()).hexdigest(),
+            "dist": vrec(dp[-1][-1].value), "len": clen, "canon": ops,
+            "es_sha256": hashlib.sha256(json.dumps(es).encode()).hexdigest()}
+
+
+def gen_g4(IR, IX):
+    seqs = IX.import_xml(os.path.join(REF, "test_input.xml"))
+    ids = list(seqs)
+    rec = {"ids": ids, "seqs": [seqs[k] for k in ids]}
+    for user in (False, True):
+        rec["wf_score_user" if user else "wf_score"] = [
+            [float(IR.wf_score(seqs[a], seqs[b], user)).hex() for b in ids] for a in ids]
+    return rec
+
+
+def gen_g5(S):
+    rng = random.Random(55)
+    out = []
+    pairs = [("ACG", "AG"), ("AGRGA", "AGGGAA"), ("A", "CA"), ("GAUUACA", "GCAUGCU"), ("AAAA", "AAAA")]
+    for _ in range(60):
+        alpha = rng.choice(("ACGU", IUPAC))
+        pairs.append((rand_str(rng, alpha, 1, 12), rand_str(rng, alpha, 1, 12)))
+    for s1, s2 in pairs:
+        for user in (False, True):
+            dp = S.wagnerFisher(s1, s2, user)
+            cpath, _ = canonical_from_graph(dp)
+            es = S.generate_es(cpath, s1, s2)
+            rev = S.generate_rev_es(es)
+            probes = [s1, s2, s1 + "A", s1[:-1], "UUUU", "", s1[::-1]]
+            rec = {"s1": s1, "s2": s2, "user": user, "es": es_compact(es), "rev": es_compact(rev),
+                   "seq_from_es": S.generate_sequence_from_es(es),
+                   "seq_from_rev": S.generate_sequence_from_es(rev),
+                   "patch_es": [[p, *S.patching(es, p)] for p in probes],
+                   "patch_rev": [[p, *S.patching(rev, p)] for p in probes]}
+            out.append(rec)
+    return out
+
+
+def gen_g6(S):
+    cases = [("a", "G", False), ("A", "T", False), ("A", "T", True), ("T", "T", False),
+             ("a", "A", False), ("A", "A", False), ("AT", "GA", False), ("GA", "AT", False),
+             ("ACGx", "ACGU", False), ("ACGU", "xyz", False), ("aC", "Ac", False), ("", "", False),
+             ("", "ACG", False), ("ACG", "", True), ("N", "N", True), ("NNA", "ANN", True),
+             ("AC", "ACGT", False), ("UUx", "UU", True), ("Tx", "AG", False)]
+    out = []
+    for s1, s2, user in cases:
+        rec = {"s1": s1, "s2": s2, "user": user}
+        try:
+            dp = S.wagnerFisher(s1, s2, user)
+            rec["dist"] = vrec(dp[-1][-1].value)
+            rec["repr"] = repr(dp[-1][-1])
+            rec["matrix_repr"] = repr(dp) if len(s1) * len(s2) <= 64 else None
+            try:
+                paths = S.create_paths(dp)
+                rec["es0"] = es_compact(S.generate_es(paths[0], s1, s2))
+            except Exception as ex:
+                rec["es_error"] = [type(ex).__name__, [str(a) for a in ex.args]]
+        except Exception as ex:
+            rec["error"] = [type(ex).__name__, [str(a) for a in ex.args]]
+        out.append(rec)
+    return out
+
+
+def dump(name, obj):
+    path = os.path.join(HERE, name)
+    with open(path, "w") as f:
+        json.dump(obj, f, separators=(",", ":"))
+    print("wrote", path, os.path.getsize(path), "bytes", file=sys.stderr)
+
+
+def main():
+    S, IR, IX = load_reference()
+    if "--g3" in sys.argv:
+        dump("g3_config2.json", gen_g3(S))
+        return
+    dump("g1_small.json", gen_g1(S))
+    dump("g6_errors.json", gen_g6(S))
+    dump("g5_patching.json", gen_g5(S))
+    dump("g4_wf_score.json", gen_g4(IR, IX))
+    dump("g2_medium.json", gen_g2(S))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,131 @@
+"""GPU parity: libsed.so (HIP, gfx950) against the golden fixtures generated
+from the reference and against the C oracle on seeded inputs.
+
+Bar: bit-exact — fp64 distance bits, Python int/float typing, script length
+and every op of the canonical edit script.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+import oracle
+import sedcost
+import sedgpu
+import synth
+
+pytestmark = pytest.mark.gpu
+OPCH = "idu"
+IUPAC = "AGCUYRWSKMDVHBN"
+
+
+def gpu_run(ctx, table, pairs, mode=0, R=0, script=True):
+    """Run (s1, s2) pairs through the engine; returns [(dist, is_int, len, opstr)]."""
+    plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
+    ctx.set_mode(mode)
+    ctx.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, R)
+    ctx.set_costs(plan)
+    packed = sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs], [plan.encode(b) for _, b in pairs])
+    dist, is_int, ln, ops = ctx.run(packed, script)
+    out = []
+    for p in range(len(pairs)):
+        s = None
+        if script:
+            s = "".join(OPCH[c] for c in sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln[p])))
+        out.append((float(dist[p]), bool(is_int[p]), int(ln[p]), s))
+    ctx.set_mode(0)
+    ctx.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
+    return out
+
+
+def test_selftest(gpu):
+    assert gpu.selftest() == 0
+
+
+@pytest.mark.parametrize("mode", [0, 2, 3])
+def test_g1_small_all_modes(gpu, tables, mode):
+    g1 = load_golden("g1_small.json")
+    for user in (False, True):
+        for alpha in ("acgu", "iupac"):
+            recs = [r for r in g1 if r["user"] == user and
+                    (set(r["s1"] + r["s2"]) <= set("ACGU")) == (alpha == "acgu")]
+            got = gpu_run(gpu, tables[user], [(r["s1"], r["s2"]) for r in recs], mode=mode)
+            for r, (d, ii, ln, s) in zip(recs, got):
+                assert (float.fromhex(r["dist"][0]), r["dist"][1]) == (d, ii), (r["s1"], r["s2"], user)
+                assert s == r["canon"], (r["s1"], r["s2"], user, s, r["canon"])
+                assert ln == len(r["canon"])
+
+
+def test_g2_medium(gpu, tables):
+    for r in load_golden("g2_medium.json"):
+        for mode in (0, 2):
+            (d, ii, ln, s), = gpu_run(gpu, tables[r["user"]], [(r["s1"], r["s2"])], mode=mode)
+            assert (d, ii) == (float.fromhex(r["dist"][0]), r["dist"][1])
+            assert ln == r["len"] and s == r["canon"], (r["kind"], len(r["s1"]), mode)
+
+
+def test_g3_config2_pair(gpu, tables):
+    g3 = load_golden("g3_config2.json")
+    s1, s2 = synth.pair_strings(g3["pair_id"], g3["n"], g3["m"], g3["base_seed"])
+    assert hashlib.sha256(s1.encode()).hexdigest() == g3["s1_sha256"]
+    for R in (0, 4, 8, 32):
+        (d, ii, ln, s), = gpu_run(gpu, tables[True], [(s1, s2)], R=R)
+        assert d == float.fromhex(g3["dist"][0]) and not ii
+        assert ln == g3["len"] and s == g3["canon"], R
+
+
+def _random_pairs(seed, count, alphabet, lo, hi, related=False):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(count):
+        n, m = rng.integers(lo, hi + 1, size=2)
+        a = "".join(rng.choice(list(alphabet), size=n))
+        if related:
+            b = "".join(c if rng.random() > 0.1 else rng.choice(list(alphabet)) for c in a)
+        else:
+            b = "".join(rng.choice(list(alphabet), size=m))
+        out.append((a, b))
+    return out
+
+
+def _oracle_check(table, pairs, got):
+    plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
+    cs = oracle.Costs.from_plan(plan)
+    for (a, b), (d, ii, ln, s) in zip(pairs, got):
+        o = oracle.pair(cs, plan.encode(a), plan.encode(b))
+        assert (d, ii, ln) == (o["dist"], bool(o["is_int"]), o["len"]), (len(a), len(b))
+        assert s == oracle.ops_to_str(o["ops"]), (len(a), len(b))
+
+
+@pytest.mark.parametrize("user", [False, True])
+@pytest.mark.parametrize("related", [False, True])
+def test_random_ragged_acgu_vs_oracle(gpu, tables, user, related):
+    pairs = _random_pairs(7 + user + 2 * related, 96, "ACGU", 0, 700, related)
+    for R in (0, 4, 16):
+        _oracle_check(tables[user], pairs, gpu_run(gpu, tables[user], pairs, R=R))
+
+
+@pytest.mark.parametrize("user", [False, True])
+def test_random_iupac_fp64_vs_oracle(gpu, tables, user):
+    pairs = _random_pairs(11 + user, 64, IUPAC, 1, 520, related=True)
+    for mode in (0, 3):
+        _oracle_check(tables[user], pairs, gpu_run(gpu, tables[user], pairs, mode=mode))
+
+
+def test_edge_lengths(gpu, tables):
+    pairs = [("", ""), ("", "A"), ("A", ""), ("ACGU", ""), ("", "GGGG"), ("A", "A"), ("A", "C")]
+    pairs += [("A" * n, "C" * m) for n in (1, 63, 64, 65, 255, 256, 257) for m in (1, 2, 61, 62, 63, 64, 65, 127)]
+    for user in (False, True):
+        for mode in (0, 2):
+            _oracle_check(tables[user], pairs, gpu_run(gpu, tables[user], pairs, mode=mode))
+
+
+def test_full_matrix_g1(gpu, tables):
+    for r in load_golden("g1_small.json")[::3]:
+        plan = sedcost.build_plan(tables[r["user"]], [r["s1"]], [r["s2"]])
+        gpu.set_costs(plan)
+        D, M = gpu.full_matrix(plan.encode(r["s1"]), plan.encode(r["s2"]))
+        want = [[float.fromhex(h), bool(ii), mk] for h, ii, mk in r["cells"]]
+        have = [[float(d), bool(mm >> 3), int(mm & 7)] for d, mm in zip(D.ravel(), M.ravel())]
+        assert want == have, (r["s1"], r["s2"])
