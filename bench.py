@@ -1,0 +1,276 @@
+#!/usr/bin/env python3
+"""Throughput bench: DP cells/s + edit-script bit-exact rate on MI355X.
+
+Default workload (BASELINE.json config 4, per-GPU shard; weak scaling):
+  8192 synthetic ACGU pairs of 4096 x 4096 per GPU, user_costs.json,
+  one step = the integer DP kernel + the device traceback over the whole
+  batch (distance AND canonical edit script for every pair), inputs resident
+  in HBM.  At --gpus 8 that is exactly config 4 (64k pairs).
+
+    python bench.py [--gpus N --steps K --warmup W] [--workload c4|c3|c2]
+
+For N > 1 run under torch.distributed.run (one rank per GPU); each rank
+generates its own pair-index shard (no input scatter), the steps run with no
+data-path collective, and the per-pair results are gathered to rank 0 over
+RCCL once, after the timed region (timed separately as gather_ms).
+Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "rna-sequence-diff-patch_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+import sedcost  # noqa: E402
+import sedgpu  # noqa: E402
+import synth  # noqa: E402
+
+METRIC = "DP cells/sec (whole node) + edit-script bit-exact rate, 4k×4k RNA pairs"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
+VALU_PEAK = 256 * 4 * 32 * 2.4e9  # lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz
+VALU_OPS_PER_CELL = {("i32", True): 7, ("i32", False): 6}
+
+WORKLOADS = {
+    # name: (pairs per GPU, n, m, cost table, description)
+    "c4": (8192, 4096, 4096, "user_costs.json",
+           "config 4 shard: 8192 pairs/GPU of 4096x4096 synthetic ACGU, user_costs.json, distance + edit script"),
+    "c3": (65536, 512, 512, "costs.json",
+           "config 3: 65536 pairs of 512x512 synthetic ACGU, costs.json, distance + edit script"),
+    "c2": (1, 4096, 4096, "user_costs.json",
+           "config 2: 1 pair 4096x4096 synthetic ACGU, user_costs.json, distance + edit script"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def gen_codes(pair_ids, n, m):
+    A = np.empty((len(pair_ids), n), np.uint8)
+    B = np.empty((len(pair_ids), m), np.uint8)
+    for s in range(0, len(pair_ids), 512):
+        ids = pair_ids[s:s + 512]
+        A[s:s + len(ids)] = synth.pair_codes(ids, n, 0)
+        B[s:s + len(ids)] = synth.pair_codes(ids, m, 1)
+    return A, B
+
+
+def script_costs(plan, A, B, ln, ops, ops_off):
+    """Vectorised property check over ALL pairs: the script is a monotone
+    alignment consuming exactly n rows and m columns and its summed cost equals
+    the distance.  Returns (valid mask, cost)."""
+    P, n = A.shape
+    m = B.shape[1]
+    Lmax = n + m
+    W = (Lmax + 15) // 16
+    words = ops[(ops_off[:P, None] + np.arange(W)[None, :])]
+    codes = ((words[:, :, None] >> (2 * np.arange(16, dtype=np.uint32))[None, None, :]) & 3).reshape(P, -1)[:, :Lmax]
+    live = np.arange(Lmax)[None, :] < ln[:, None]
+    ins = (codes == 0) & live
+    dele = (codes == 1) & live
+    upd = (codes == 2) & live
+    rows = np.cumsum(dele | upd, axis=1)  # rows consumed after each op
+    cols = np.cumsum(ins | upd, axis=1)
+    ok = (rows[:, -1] == n) & (cols[:, -1] == m) & (((codes == 3) & live).sum(1) == 0)
+    ri = np.clip(rows - 1, 0, n - 1)
+    cj = np.clip(cols - 1, 0, m - 1)
+    a_sym = np.take_along_axis(A, ri, axis=1)
+    b_sym = np.take_along_axis(B, cj, axis=1)
+    sub = plan.sub[a_sym, b_sym]
+    cost = ins.sum(1) * plan.ins + dele.sum(1) * plan.dele + (sub * upd).sum(1)
+    return ok, cost
+
+
+def cpu_baseline(plan, A, B, seconds, threads):
+    """Oracle (C restatement, test infrastructure) on a bounded sample."""
+    import oracle
+    cs = oracle.Costs.from_plan(plan)
+    n, m = A.shape[1], B.shape[1]
+    t0 = time.perf_counter()
+    oracle.pair(cs, A[0], B[0], want_ops=True)
+    t1 = time.perf_counter() - t0
+    per_thread = max(1, int(seconds / max(t1, 1e-6)))
+    count = min(len(A), per_thread * threads)
+    la = np.full(count, n, np.int32)
+    lb = np.full(count, m, np.int32)
+    offa = np.arange(count, dtype=np.int64) * n
+    offb = np.arange(count, dtype=np.int64) * m
+    t0 = time.perf_counter()
+    dist, is_int, ln, ops, ops_off = oracle.batch(cs, np.ascontiguousarray(A[:count]), offa, la,
+                                                  np.ascontiguousarray(B[:count]), offb, lb, count,
+                                                  want_ops=True, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": count * n * m / dt, "seconds": dt, "count": count, "dist": dist, "len": ln, "ops": ops,
+            "ops_off": ops_off}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
+    ap.add_argument("--pairs", type=int, default=0, help="override pairs per GPU")
+    ap.add_argument("--no-script", action="store_true", help="distance only (no traceback)")
+    ap.add_argument("--rows-per-lane", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-json", default="", help="per-launch HBM traffic from a rocprofv3 PMC pass")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    P, n, m, costs_file, desc = WORKLOADS[args.workload]
+    if args.pairs:
+        P = args.pairs
+    want_script = not args.no_script
+    with open(os.path.join(REPO, "tests", "golden", costs_file)) as f:
+        table = json.load(f)
+    plan = sedcost.build_plan(table, ["ACGU"], ["ACGU"])
+    ids = np.arange(rank * P, (rank + 1) * P, dtype=np.uint64)
+    t0 = time.perf_counter()
+    A, B = gen_codes(ids, n, m)
+    log("rank %d: generated %d pairs in %.1fs" % (rank, P, time.perf_counter() - t0))
+
+    ctx = sedgpu.Context(local)
+    if args.rows_per_lane:
+        ctx.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, args.rows_per_lane)
+    ctx.set_costs(plan)
+    packed = sedgpu.PackedPairs.from_arrays(A, B)
+    t0 = time.perf_counter()
+    batch = sedgpu.Batch(ctx, packed, want_script)
+    log("rank %d: batch resident in %.1fs (mode %s, R=%d)" % (rank, time.perf_counter() - t0, batch.mode,
+                                                             batch.rows_per_lane))
+    cells, algo_bytes = batch.work()
+
+    for _ in range(args.warmup):
+        batch.run()
+        batch.sync()
+    dp_ms, tb_ms = [], []
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        batch.run()
+        batch.sync()
+        a, b = batch.last_times()
+        dp_ms.append(a)
+        tb_ms.append(b)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = cells * world * args.steps / elapsed
+
+    # ---- results: gather to rank 0 over RCCL (timed separately) ----
+    gather_ms = None
+    if dist is not None:
+        words = int(packed.ops_off[P])
+        t_dist = torch.empty(P, dtype=torch.float64, device="cuda")
+        t_len = torch.empty(P, dtype=torch.int32, device="cuda")
+        t_ops = torch.empty(max(words, 1), dtype=torch.int32, device="cuda")
+        batch.export(t_dist.data_ptr(), t_len.data_ptr(), t_ops.data_ptr() if want_script else 0)
+        barrier()
+        g0 = time.perf_counter()
+        outs = []
+        for t in (t_dist, t_len, t_ops):
+            lst = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+            dist.gather(t, lst, dst=0)
+            outs.append(lst)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - g0) * 1e3
+        if rank == 0:
+            all_dist = torch.cat(outs[0]).cpu().numpy()
+            log("rank 0: gathered %d results (%.2f ms)" % (len(all_dist), gather_ms))
+
+    # ---- verification (untimed) ----
+    d_gpu, ii_gpu, ln_gpu, ops = batch.results()
+    check = {}
+    if want_script:
+        good = 0
+        for s0 in range(0, P, 256):
+            sl = slice(s0, min(P, s0 + 256))
+            ok, cost = script_costs(plan, A[sl], B[sl], ln_gpu[sl], ops, packed.ops_off[sl])
+            same = (cost == d_gpu[sl]) if batch.mode == "i32" else np.isclose(cost, d_gpu[sl], rtol=1e-12)
+            good += int((ok & same).sum())
+        check["script_valid_rate"] = good / P
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            threads = min(16, len(os.sched_getaffinity(0)))
+        except AttributeError:
+            threads = min(16, os.cpu_count() or 1)
+        cpu = cpu_baseline(plan, A, B, args.cpu_seconds, threads)
+        c = cpu["count"]
+        exact = (cpu["dist"] == d_gpu[:c]) & (cpu["len"] == ln_gpu[:c])
+        if want_script:
+            for p in range(c):
+                if exact[p]:
+                    g = sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln_gpu[p]))
+                    o = cpu["ops"][cpu["ops_off"][p]: cpu["ops_off"][p] + cpu["len"][p]]
+                    exact[p] = np.array_equal(g, o)
+        check["script_exact_rate"] = float(exact.mean())
+        check["script_exact_sample"] = int(c)
+        cpu_obj = {"value": cpu["value"], "unit": "cells/s", "cores": threads, "kind": "port",
+                   "sample": "%d of the %d pairs (%dx%d, %s), C oracle sed_oracle.c, %.1f s"
+                             % (c, P, n, m, costs_file, cpu["seconds"])}
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    dp_avg = float(np.mean(dp_ms))
+    achieved = algo_bytes / (dp_avg * 1e-3) / 1e9
+    traffic = None
+    if args.pmc_json and os.path.exists(args.pmc_json):
+        with open(args.pmc_json) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    ops_cell = VALU_OPS_PER_CELL.get((batch.mode, want_script))
+    line = {
+        "metric": METRIC, "value": value, "unit": "cells/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32" if batch.mode == "i32" else "f64", "data": "synthetic",
+        "config": {"workload": desc, "pairs_per_gpu": P, "n": n, "m": m, "costs": costs_file,
+                   "script": want_script, "mode": batch.mode, "rows_per_lane": batch.rows_per_lane,
+                   "parallelism": "dp%d" % world},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "sed_wf_i32_kernel" if batch.mode == "i32" else "sed_wf_f64_kernel",
+                     "kernel_ms": dp_avg, "algo_bytes_per_launch": algo_bytes},
+        "valu": None if ops_cell is None else {
+            "ops_per_cell": ops_cell, "achieved": cells / (dp_avg * 1e-3) * ops_cell, "peak": VALU_PEAK,
+            "frac": cells / (dp_avg * 1e-3) * ops_cell / VALU_PEAK, "unit": "lane-ops/s"},
+        "traceback_ms": float(np.mean(tb_ms)) if want_script else None,
+        "gather_ms": gather_ms,
+        "cpu_baseline": cpu_obj if cpu is not None else None,
+    }
+    line.update(check)
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -103,6 +103,9 @@ int sed_batch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32
 /* Device pointers of the result arrays (for an RCCL gather); any may be NULL. */
 int sed_batch_device_results(const sed_batch *b, uint64_t *d_dist, uint64_t *d_is_int,
                              uint64_t *d_len, uint64_t *d_ops, uint64_t *ops_words);
+/* Copy dist (f64[npairs]), len (i32[npairs]) and the packed scripts (u32[ops_words]) of the last
+ * run into caller device memory (e.g. tensors an RCCL gather sends); any pointer may be 0. Blocking. */
+int sed_batch_export(sed_batch *b, uint64_t d_dist, uint64_t d_len, uint64_t d_ops);
 /* Algorithmic counts of one run: DP cells (sum n*m) and HBM bytes (inputs + traceback + outputs). */
 int sed_batch_work(const sed_batch *b, double *cells, double *algo_bytes);
 

@@ -511,6 +511,25 @@ int sed_batch_device_results(const sed_batch *b, uint64_t *d_dist, uint64_t *d_i
     return SED_OK;
 }
 
+int sed_batch_export(sed_batch *b, uint64_t d_dist, uint64_t d_len, uint64_t d_ops) {
+    if (!b) return SED_E_ARG;
+    sed_ctx *c = b->ctx;
+    (void)hipSetDevice(c->device);
+    if (!b->ran) return c->fail(SED_E_STATE, "batch has not been run");
+    const int np = b->npairs;
+    hipError_t e = hipSuccess;
+    if (np && d_dist)
+        e = hipMemcpy2DAsync((void *)(uintptr_t)d_dist, sizeof(double), (const char *)b->d_res.p + offsetof(sed_result, dist),
+                             sizeof(sed_result), sizeof(double), np, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess && np && d_len)
+        e = hipMemcpy2DAsync((void *)(uintptr_t)d_len, sizeof(int32_t), (const char *)b->d_res.p + offsetof(sed_result, len),
+                             sizeof(sed_result), sizeof(int32_t), np, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess && d_ops && (b->flags & SED_WANT_SCRIPT) && b->ops_words)
+        e = hipMemcpyAsync((void *)(uintptr_t)d_ops, b->d_ops.p, 4 * b->ops_words, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return e == hipSuccess ? SED_OK : c->hipfail(e, "export results");
+}
+
 int sed_batch_work(const sed_batch *b, double *cells, double *algo_bytes) {
     if (!b) return SED_E_ARG;
     if (cells) *cells = b->cells;

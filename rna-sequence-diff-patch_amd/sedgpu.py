@@ -41,6 +41,7 @@ SIGNATURES = [
     ("sed_batch_last_times", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("sed_batch_results", C.c_int, [C.c_void_p, _f64p, _u8p, _i32p, C.c_void_p, C.c_void_p]),
     ("sed_batch_device_results", C.c_int, [C.c_void_p] + [C.POINTER(C.c_uint64)] * 5),
+    ("sed_batch_export", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64]),
     ("sed_batch_work", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     ("sed_selftest", C.c_int, [C.c_void_p]),
     ("sed_full_matrix", C.c_int, [C.c_void_p, _u8p, C.c_int32, _u8p, C.c_int32, _f64p, _u8p]),
@@ -246,6 +247,10 @@ class Batch:
         vals = [C.c_uint64() for _ in range(5)]
         self._lib.sed_batch_device_results(self.ptr, *[C.byref(v) for v in vals])
         return [v.value for v in vals]
+
+    def export(self, d_dist=0, d_len=0, d_ops=0):
+        """Device-to-device copy of the results into caller memory (raw device pointers)."""
+        self.ctx._check(self._lib.sed_batch_export(self.ptr, d_dist, d_len, d_ops), "sed_batch_export")
 
     def results(self):
         P = self.packed.npairs
