@@ -34,8 +34,11 @@ import synth  # noqa: E402
 
 METRIC = "DP cells/sec (whole node) + edit-script bit-exact rate, 4k×4k RNA pairs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
-VALU_PEAK = 256 * 4 * 32 * 2.4e9  # lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz
-VALU_OPS_PER_CELL = {("i32", True): 7, ("i32", False): 6}
+# VALU ceiling of the integer kernel, from tools/ubench/valu_rate.hip on MI355X:
+# wave64 v_add/v_and issue every ~2.5 cycles per SIMD, VOP3-only ops (v_min3, v_perm,
+# v_alignbit) every ~4.4.  A script-mode cell is 4 of the former + 3 of the latter.
+SIMDS, CLOCK = 1024, 2.4e9
+CELL_CYCLES = {("i32", True): 4 * 2.5 + 3 * 4.4, ("i32", False): 4 * 2.5 + 2 * 4.4}  # per 64 cells
 
 WORKLOADS = {
     # name: (pairs per GPU, n, m, cost table, description)
@@ -119,6 +122,8 @@ def main():
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     ap.add_argument("--pairs", type=int, default=0, help="override pairs per GPU")
     ap.add_argument("--no-script", action="store_true", help="distance only (no traceback)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="run DP and traceback back to back on one stream (no overlap across steps)")
     ap.add_argument("--rows-per-lane", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -158,25 +163,24 @@ def main():
     ctx.set_costs(plan)
     packed = sedgpu.PackedPairs.from_arrays(A, B)
     t0 = time.perf_counter()
-    batch = sedgpu.Batch(ctx, packed, want_script)
+    pipeline = want_script and not args.no_pipeline
+    batch = sedgpu.Batch(ctx, packed, want_script, pipeline=pipeline)
     log("rank %d: batch resident in %.1fs (mode %s, R=%d)" % (rank, time.perf_counter() - t0, batch.mode,
                                                              batch.rows_per_lane))
     cells, algo_bytes = batch.work()
 
     for _ in range(args.warmup):
         batch.run()
-        batch.sync()
-    dp_ms, tb_ms = [], []
+    batch.sync()
+    batch.reset_times()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        batch.run()
-        batch.sync()
-        a, b = batch.last_times()
-        dp_ms.append(a)
-        tb_ms.append(b)
+        batch.run()  # DP(k) on the DP stream; traceback(k) on a second stream overlaps DP(k+1)
+    batch.sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    dp_ms, tb_ms = batch.times()
     if dist is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -247,21 +251,24 @@ def main():
     if args.pmc_json and os.path.exists(args.pmc_json):
         with open(args.pmc_json) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
-    ops_cell = VALU_OPS_PER_CELL.get((batch.mode, want_script))
+    cyc = CELL_CYCLES.get((batch.mode, want_script))
+    rate = cells / (dp_avg * 1e-3)
     line = {
         "metric": METRIC, "value": value, "unit": "cells/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u32" if batch.mode == "i32" else "f64", "data": "synthetic",
         "config": {"workload": desc, "pairs_per_gpu": P, "n": n, "m": m, "costs": costs_file,
-                   "script": want_script, "mode": batch.mode, "rows_per_lane": batch.rows_per_lane,
+                   "script": want_script, "pipeline": pipeline, "mode": batch.mode,
+                   "rows_per_lane": batch.rows_per_lane,
                    "parallelism": "dp%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "sed_wf_i32_kernel" if batch.mode == "i32" else "sed_wf_f64_kernel",
                      "kernel_ms": dp_avg, "algo_bytes_per_launch": algo_bytes},
-        "valu": None if ops_cell is None else {
-            "ops_per_cell": ops_cell, "achieved": cells / (dp_avg * 1e-3) * ops_cell, "peak": VALU_PEAK,
-            "frac": cells / (dp_avg * 1e-3) * ops_cell / VALU_PEAK, "unit": "lane-ops/s"},
+        "valu": None if cyc is None else {
+            "model": "per 64 cells: 4 full-rate + %d half-rate VALU (tools/ubench/valu_rate.hip)" % (3 if want_script else 2),
+            "achieved": rate, "peak": SIMDS * CLOCK * 64 / cyc, "unit": "cells/s",
+            "frac": rate / (SIMDS * CLOCK * 64 / cyc)},
         "traceback_ms": float(np.mean(tb_ms)) if want_script else None,
         "gather_ms": gather_ms,
         "cpu_baseline": cpu_obj if cpu is not None else None,

@@ -47,6 +47,9 @@ enum {
 
 /* flags for sed_run_batch / sed_batch_create */
 #define SED_WANT_SCRIPT 1u
+/* sed_batch only: two traceback/result buffers and a second stream, so the traceback of
+ * run k overlaps the DP kernel of run k+1 (device memory for the traceback doubles). */
+#define SED_PIPELINE 2u
 
 /* sed_set_option keys */
 #define SED_OPT_MODE 1          /* 0 auto, 1 packed-integer kernel, 2 fp64 kernel, 3 fp64 + int-typing */
@@ -98,6 +101,10 @@ int sed_batch_run(sed_batch *b);                      /* enqueue on the context 
 int sed_batch_sync(sed_batch *b);                     /* wait for the last run */
 /* device time of the last run, from HIP events on the launching stream (ms) */
 int sed_batch_last_times(const sed_batch *b, float *dp_ms, float *traceback_ms);
+/* Device times of every run since the last sed_batch_reset_times (waits for them):
+ * dp_ms[i] / traceback_ms[i] for run i; returns the number of runs reported (<= max_runs). */
+int sed_batch_times(sed_batch *b, float *dp_ms, float *traceback_ms, int max_runs);
+int sed_batch_reset_times(sed_batch *b);
 int sed_batch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32_t *out_len,
                       uint32_t *out_ops, const int64_t *ops_off);
 /* Device pointers of the result arrays (for an RCCL gather); any may be NULL. */

@@ -94,56 +94,96 @@ __device__ __forceinline__ void store_tb(uint32_t *p, const uint32_t (&w)[NW]) {
 }
 
 // ---------------------------------------------------------------------------
-// Integer (packed-key) kernel
+// Integer (packed-key) kernel.  Cells live in "V space":
+//     V = D << 16 | L << 2        (D < 2^16, L < 2^14)
+// candidate = V_pred + K, K = (cost << 16) + 4 + op, op 0 insert / 1 delete / 2 update;
+// mm = min3(candidates) carries the winning op in its low 2 bits and V_new = mm & ~3.
+// Lanes run unmasked all the time: a lane that has not reached column 1 yet is
+// reset to its column-0 state right before its first step, and a lane past
+// column m computes columns that nothing reads.
 // ---------------------------------------------------------------------------
-template <int R, bool TB, bool MASKED>
-__device__ __forceinline__ void i32_step(uint32_t (&Y)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
+template <int R, bool TB>
+__device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                          uint32_t &bottom, uint32_t &selv, uint32_t &tch, uint32_t &sch,
                                          uint32_t &outc, uint32_t (&W)[TbWords<R>::N], const int u,
-                                         const uint32_t kins, const uint32_t kdel, const bool active) {
-    const uint32_t topv = dpp_shr1(tch, bottom);  // cell above the band, this column
+                                         const uint32_t kins, const uint32_t kdel) {
+    const uint32_t topv = dpp_shr1(tch, bottom);  // cell above the band, this column (lane 0: chunk)
     selv = dpp_shr1(sch, selv);                   // perm selector of this column's str2 symbol
     tch = dpp_rol1(tch);
     sch = dpp_rol1(sch);
     uint32_t up = topv, diag = top_prev;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const uint32_t left = Y[r];
-        const uint32_t ci = (left << 2) + kins;                                  // insert  (op 0)
-        const uint32_t cd = (up << 2) + kdel;                                    // delete  (op 1)
-        const uint32_t cu = (diag << 2) + __builtin_amdgcn_perm(cv[r], 6u, selv);  // update (op 2)
-        const uint32_t mm = umin3(ci, cd, cu);
-        const uint32_t yn = mm >> 2;
+        const uint32_t left = V[r];
+        const uint32_t mm = umin3(left + kins,                                     // insert (op 0)
+                                  up + kdel,                                       // delete (op 1)
+                                  diag + __builtin_amdgcn_perm(cv[r], 6u, selv));  // update (op 2)
         if constexpr (TB) {
             const int c = u * R + r;  // compile-time after unrolling
             W[c >> 4] = __builtin_amdgcn_alignbit(mm, W[c >> 4], 2);
         }
         diag = left;
-        up = yn;
-        if constexpr (MASKED) Y[r] = active ? yn : left;
-        else Y[r] = yn;
+        up = mm & ~3u;
+        V[r] = up;
     }
-    if constexpr (MASKED) top_prev = active ? topv : top_prev;
-    else top_prev = topv;
-    bottom = Y[R - 1];
+    top_prev = topv;
+    bottom = V[R - 1];
     outc = dpp_shl1(bottom, outc);
 }
 
-template <int R, bool TB, bool MASKED>
-__device__ __forceinline__ void i32_group(uint32_t (&Y)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
-                                          uint32_t &bottom, uint32_t &selv, uint32_t &tch, uint32_t &sch,
-                                          uint32_t &outc, uint32_t (&W)[TbWords<R>::N], const int s0,
-                                          const int lane, const int m, const uint32_t kins, const uint32_t kdel) {
+__device__ __forceinline__ uint32_t i32_border(uint32_t i, uint32_t cost) { return ((i * cost) << 16) | (i << 2); }
+
+template <int R>
+__device__ __forceinline__ void i32_reset(uint32_t (&V)[R], uint32_t &top_prev, int row0, uint32_t del) {
+    uint32_t v = i32_border((uint32_t)row0, del);
+    const uint32_t step = (del << 16) | 4u;
+    top_prev = v;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int j = s0 + u - lane + 1;  // column this lane computes at step s0+u
-        const bool active = (j >= 1) && (j <= m);
-        i32_step<R, TB, MASKED>(Y, cv, top_prev, bottom, selv, tch, sch, outc, W, u, kins, kdel, active);
+    for (int r = 0; r < R; ++r) {
+        v += step;
+        V[r] = v;
     }
 }
 
+// SLOW groups: ramp-up (the lane that starts next step is reset to column 0)
+// and the group that produces the sink cell (captured).  Branch-free selects,
+// so no value lives across a basic-block boundary.
+template <int R, bool TB, bool SLOW>
+__device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
+                                          uint32_t &bottom, uint32_t &selv, uint32_t &tch, uint32_t &sch,
+                                          uint32_t &outc, uint32_t (&W)[TbWords<R>::N], const int s0,
+                                          const int lane, const int row0, const uint32_t kins, const uint32_t kdel,
+                                          const uint32_t del, const int cap_step, const int cap_lane,
+                                          const int cap_row, uint32_t &cap) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        i32_step<R, TB>(V, cv, top_prev, bottom, selv, tch, sch, outc, W, u, kins, kdel);
+        if constexpr (SLOW) {
+            const int s = s0 + u;
+            const bool hit = (s == cap_step) && (lane == cap_lane);
+#pragma unroll
+            for (int r = 0; r < R; ++r) cap = (hit && r == cap_row) ? V[r] : cap;
+            const bool start = (lane == s + 1);
+            int rr = row0;
+            uint32_t dd = del;
+            asm volatile("" : "+v"(rr), "+s"(dd));  // keep the column-0 values from being hoisted (VGPRs)
+            uint32_t v = i32_border((uint32_t)rr, dd);
+            const uint32_t st = (dd << 16) | 4u;
+            top_prev = start ? v : top_prev;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                v += st;
+                V[r] = start ? v : V[r];
+            }
+        }
+    }
+}
+
+#ifndef SED_I32_WAVES_PER_EU
+#define SED_I32_WAVES_PER_EU 6  // 80 VGPRs at R=16: measured fastest (tools/sweep.sh)
+#endif
 template <int R, bool TB>
-__global__ __launch_bounds__(256) void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SED_I32_WAVES_PER_EU))) void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
                                                          const uint32_t *__restrict__ seqa,
                                                          const uint32_t *__restrict__ seqb,
                                                          uint32_t *__restrict__ tb, uint32_t *__restrict__ bnd,
@@ -170,19 +210,22 @@ __global__ __launch_bounds__(256) void sed_wf_i32_kernel(const sed_pair_desc *__
     uint32_t *bndp = bnd + d.bnd_off;
     const uint32_t *pa = seqa + d.a_off;
     const uint32_t *pb = seqb + d.b_off;
+    // the sink cell (n, m): last stripe, lane (n-1)%ROWS / R, row (n-1)%R, computed at step m-1+lane
+    const int wsink = (n - 1) % ROWS;
+    const int cap_lane = wsink / R, cap_row = wsink % R;
+    uint32_t cap = 0;
 
     for (int k = 0; k < nstripes; ++k) {
         const int row0 = k * ROWS + lane * R;  // 0-based str1 index of this lane's first row
-        uint32_t cv[R], Y[R];
+        uint32_t cv[R], V[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int ri = row0 + r;
             const uint32_t a = (pa[ri >> 4] >> ((ri & 15) * 2)) & 3u;
             cv[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
-            const uint32_t i = (uint32_t)(ri + 1);
-            Y[r] = ((i * prm.del) << 14) | i;  // column 0: D = i*delete, L = i
         }
-        uint32_t top_prev = (((uint32_t)row0 * prm.del) << 14) | (uint32_t)row0;
+        uint32_t top_prev;
+        i32_reset<R>(V, top_prev, row0, prm.del);
         uint32_t bottom = 0, selv = 0, outc = 0;
         uint32_t W[NW];
 #pragma unroll
@@ -190,7 +233,7 @@ __global__ __launch_bounds__(256) void sed_wf_i32_kernel(const sed_pair_desc *__
 
         auto load_top = [&](int c) -> uint32_t {
             const int j = 64 * c + lane + 1;
-            if (k == 0) return (((uint32_t)j * prm.ins) << 14) | (uint32_t)j;  // row 0: D = j*insert, L = j
+            if (k == 0) return i32_border((uint32_t)j, prm.ins);  // row 0: D = j*insert, L = j
             return load_sc1(bndp + j + 64);
         };
         auto load_sel = [&](int c) -> uint32_t {
@@ -201,18 +244,18 @@ __global__ __launch_bounds__(256) void sed_wf_i32_kernel(const sed_pair_desc *__
         uint32_t tch = load_top(0), sch = load_sel(0);
         uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(S4 >> 2) * 64u * NW;
         const bool last = (k == nstripes - 1);
+        const int cap_step = last ? m - 1 + cap_lane : -1;
         int s = 0;
         for (int c = 0; c < nchunks; ++c) {
             uint32_t tnx = 0, snx = 0;
             if (c + 1 < nchunks) { tnx = load_top(c + 1); snx = load_sel(c + 1); }
             for (int g = 0; g < 16 && s < S4; ++g, s += 4) {
-                const bool full = (s >= 63) && (s + 3 < m);
-                if (full)
-                    i32_group<R, TB, false>(Y, cv, top_prev, bottom, selv, tch, sch, outc, W, s, lane, m,
-                                            prm.kins, prm.kdel);
+                if (s < 63 || (cap_step >= s && cap_step < s + 4))
+                    i32_group<R, TB, true>(V, cv, top_prev, bottom, selv, tch, sch, outc, W, s, lane, row0, prm.kins,
+                                           prm.kdel, prm.del, cap_step, cap_lane, cap_row, cap);
                 else
-                    i32_group<R, TB, true>(Y, cv, top_prev, bottom, selv, tch, sch, outc, W, s, lane, m,
-                                           prm.kins, prm.kdel);
+                    i32_group<R, TB, false>(V, cv, top_prev, bottom, selv, tch, sch, outc, W, s, lane, row0,
+                                            prm.kins, prm.kdel, prm.del, cap_step, cap_lane, cap_row, cap);
                 if constexpr (TB) store_tb<NW>(tbk + ((uint64_t)(s >> 2) * 64u + lane) * NW, W);
             }
             // lane i holds lane 63's bottom cell of step s-64+i, i.e. column s-126+i at bnd index col+64
@@ -221,19 +264,12 @@ __global__ __launch_bounds__(256) void sed_wf_i32_kernel(const sed_pair_desc *__
             sch = snx;
         }
         if (!last) __builtin_amdgcn_s_waitcnt(0);  // own bottom-row stores done before the next stripe reads them
-        else {
-            const int w = (n - 1) % ROWS;
-            if (lane == w / R) {
-                const int rf = w % R;
-                uint32_t y = 0;
-#pragma unroll
-                for (int r = 0; r < R; ++r) y = (r == rf) ? Y[r] : y;
-                const uint32_t D = y >> 14;
-                res[pair].dist = (double)D;
-                res[pair].len = (int32_t)(y & 0x3FFFu);
-                res[pair].is_int = (D == 0);
-            }
-        }
+    }
+    if (lane == cap_lane) {
+        const uint32_t D = cap >> 16;
+        res[pair].dist = (double)D;
+        res[pair].len = (int32_t)((cap >> 2) & 0x3FFFu);
+        res[pair].is_int = (D == 0);
     }
 }
 
@@ -494,27 +530,27 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
 
 // ---------------------------------------------------------------------------
 // Traceback: one lane per pair walks the 2-bit choices from (n, m) to (0, 0)
-// and writes the op codes origin->sink, 16 per word.  The 16-byte group of
-// codes a lane stored is cached in registers while the path stays in it.
+// and writes the op codes origin->sink, 16 per word.  Position bookkeeping is
+// incremental (stripe k, lane t, row r, step s) with power-of-two R, and the
+// 16-byte aligned block of codes last read is kept in registers: a diagonal
+// run stays in it for up to four steps.
 // ---------------------------------------------------------------------------
+template <int R>
 __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
                                                            const uint32_t *__restrict__ tb,
                                                            const sed_result *__restrict__ res,
-                                                           uint32_t *__restrict__ ops, int R) {
+                                                           uint32_t *__restrict__ ops) {
+    constexpr int NW = R / 4;
     const int pair = blockIdx.x * blockDim.x + threadIdx.x;
     if (pair >= npairs) return;
     const sed_pair_desc d = pd[pair];
     const int n = d.n, m = d.m;
-    const int ROWS = 64 * R, NW = R / 4;
     const int S4 = (m + 63 + 3) & ~3;
     const uint64_t stripe_words = (uint64_t)(S4 >> 2) * 64u * NW;
-    const uint32_t *tbp = tb + d.tb_off;
     uint32_t *out = ops + d.ops_off;
     int q = res[pair].len;  // ops in the script; written from position q-1 down to 0
     int i = n, j = m;
     uint32_t acc = 0;
-    uint64_t cached = ~0ull;
-    uint32_t cw = 0;
     auto emit = [&](uint32_t op) {
         --q;
         acc |= op << (2 * (q & 15));
@@ -523,21 +559,40 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
             acc = 0;
         }
     };
-    while (i > 0 && j > 0) {
+    if (i > 0 && j > 0) {
         const int rr = i - 1;
-        const int kk = rr / ROWS, w = rr % ROWS;
-        const int t = w / R, r = w % R;
-        const int s = j - 1 + t;
-        const int c = (s & 3) * R + r;
-        const uint64_t widx = (uint64_t)kk * stripe_words + ((uint64_t)(s >> 2) * 64u + t) * NW + (c >> 4);
-        if (widx != cached) {
-            cw = tbp[widx];
-            cached = widx;
+        int k = rr / (64 * R);
+        int t = (rr >> __builtin_ctz(R)) & 63;
+        int r = rr & (R - 1);
+        const uint32_t *base = tb + d.tb_off + (uint64_t)k * stripe_words;
+        uint64_t cached = ~0ull;
+        uint4 cw = make_uint4(0, 0, 0, 0);
+        while (true) {
+            const int s = j - 1 + t;
+            const int c = (s & 3) * R + r;
+            const uint64_t widx = ((uint64_t)(s >> 2) * 64u + t) * NW + (c >> 4);
+            if ((widx & ~3ull) != cached) {
+                cached = widx & ~3ull;
+                cw = *reinterpret_cast<const uint4 *>(base + cached);
+            }
+            const uint32_t wv = (widx & 2) ? ((widx & 1) ? cw.w : cw.z) : ((widx & 1) ? cw.y : cw.x);
+            const uint32_t op = (wv >> (2 * (c & 15))) & 3u;
+            emit(op);
+            if (op != 1) --j;
+            if (op != 0) {  // move up one row
+                --i;
+                if (--r < 0) {
+                    r = R - 1;
+                    if (--t < 0) {
+                        t = 63;
+                        --k;
+                        base -= stripe_words;
+                        cached = ~0ull;
+                    }
+                }
+            }
+            if (i == 0 || j == 0) break;
         }
-        const uint32_t op = (cw >> (2 * (c & 15))) & 3u;
-        emit(op);
-        if (op != 1) --j;
-        if (op != 0) --i;
     }
     while (j > 0) { emit(0u); --j; }
     while (i > 0) { emit(1u); --i; }
@@ -619,8 +674,16 @@ hipError_t sed_launch_f64(const sed_launch &L, const double *gtab, const sed_f64
 
 hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops) {
     const int grid = (L.npairs + 63) / 64;
-    hipLaunchKernelGGL(sed_traceback_kernel, dim3(grid), dim3(64), 0, L.stream, L.pd, L.npairs, L.tb, L.res, ops,
-                       L.R);
+    switch (L.R) {
+#define CASE(RR)                                                                                              \
+    case RR:                                                                                                  \
+        hipLaunchKernelGGL(sed_traceback_kernel<RR>, dim3(grid), dim3(64), 0, L.stream, L.pd, L.npairs, L.tb, \
+                           L.res, ops);                                                                      \
+        break;
+        CASE(4) CASE(8) CASE(16) CASE(32)
+#undef CASE
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

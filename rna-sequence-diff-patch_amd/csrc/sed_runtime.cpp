@@ -7,6 +7,7 @@
 
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -83,18 +84,36 @@ struct sed_batch {
     std::vector<int32_t> n, m;
     uint64_t tb_words = 0, bnd_words = 0, ops_words = 0;
     double cells = 0, algo_bytes = 0;
-    DevBuf d_pd, d_seqa, d_seqb, d_tb, d_bnd, d_res, d_ops;
+    DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops;
+    // SED_PIPELINE: run k uses traceback/result buffer k&1, so the traceback of
+    // run k (second stream) overlaps the DP of run k+1.
+    int nbuf = 1;
+    DevBuf d_tb[2], d_res[2];
+    hipStream_t tb_stream = nullptr;
+    // events per buffer: DP start/end on the DP stream, traceback start/end on the traceback stream
+    hipEvent_t ev_dp0[2] = {}, ev_dp1[2] = {}, ev_tb0[2] = {}, ev_tb1[2] = {};
+    long runs = 0;
+    bool ran = false;
+    // per-run event log (sed_batch_times): {dp start, dp end, tb start, tb end}
+    std::vector<std::array<hipEvent_t, 4>> log;
+    size_t nlog = 0;
     sed_i32_params ip{};
     sed_f64_params fp{};
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-    bool ran = false;
     std::vector<sed_result> h_res;
 
+    int cur() const { return (int)((runs - 1) & (nbuf - 1)); }
     ~sed_batch() {
-        d_pd.release(); d_seqa.release(); d_seqb.release(); d_tb.release();
-        d_bnd.release(); d_res.release(); d_ops.release();
-        for (auto &e : ev)
-            if (e) (void)hipEventDestroy(e);
+        d_pd.release(); d_seqa.release(); d_seqb.release(); d_bnd.release(); d_ops.release();
+        for (int i = 0; i < 2; ++i) {
+            d_tb[i].release();
+            d_res[i].release();
+            for (hipEvent_t e : {ev_dp0[i], ev_dp1[i], ev_tb0[i], ev_tb1[i]})
+                if (e) (void)hipEventDestroy(e);
+        }
+        if (tb_stream) (void)hipStreamDestroy(tb_stream);
+        for (auto &a : log)
+            for (hipEvent_t e : a)
+                if (e) (void)hipEventDestroy(e);
     }
 };
 
@@ -150,6 +169,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     b->npairs = npairs;
     b->flags = flags;
     b->ran = false;
+    b->runs = 0;
+    b->nbuf = (flags & SED_PIPELINE) ? 2 : 1;
     b->n.assign(len_a, len_a + npairs);
     b->m.assign(len_b, len_b + npairs);
     int max_n = 0, max_m = 0;
@@ -261,11 +282,14 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         }
     }
     const size_t sa = packed ? ha.size() * 4 : ha8.size(), sb = packed ? hb.size() * 4 : hb8.size();
-    if (!b->d_pd.reserve(sizeof(sed_pair_desc) * std::max(1, npairs)) || !b->d_seqa.reserve(sa) ||
-        !b->d_seqb.reserve(sb) || !b->d_res.reserve(sizeof(sed_result) * std::max(1, npairs)) ||
-        !b->d_ops.reserve(4 * std::max<uint64_t>(1, opw)) || !b->d_bnd.reserve(4 * std::max<uint64_t>(1, bndw)) ||
-        (want_tb && !b->d_tb.reserve(4 * std::max<uint64_t>(1, tbw))))
-        return c->fail(SED_E_OOM, "device allocation failed (traceback %.3f GB)", 4.0 * tbw / 1e9);
+    bool okalloc = b->d_pd.reserve(sizeof(sed_pair_desc) * std::max(1, npairs)) && b->d_seqa.reserve(sa) &&
+                   b->d_seqb.reserve(sb) && b->d_ops.reserve(4 * std::max<uint64_t>(1, opw)) &&
+                   b->d_bnd.reserve(4 * std::max<uint64_t>(1, bndw));
+    for (int i = 0; i < b->nbuf && okalloc; ++i)
+        okalloc = b->d_res[i].reserve(sizeof(sed_result) * std::max(1, npairs)) &&
+                  (!want_tb || b->d_tb[i].reserve(4 * std::max<uint64_t>(1, tbw)));
+    if (!okalloc)
+        return c->fail(SED_E_OOM, "device allocation failed (traceback %d x %.3f GB)", b->nbuf, 4.0 * tbw / 1e9);
     hipError_t e;
     if ((e = hipMemcpyAsync(b->d_pd.p, b->pd.data(), sizeof(sed_pair_desc) * npairs, hipMemcpyHostToDevice,
                             c->stream)) != hipSuccess)
@@ -303,8 +327,12 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         fp.K = c->K;
         b->fp = fp;
     }
-    for (auto &ev : b->ev)
-        if (!ev && (e = hipEventCreate(&ev)) != hipSuccess) return c->hipfail(e, "event create");
+    for (int i = 0; i < 2; ++i)
+        for (hipEvent_t *ev : {&b->ev_dp0[i], &b->ev_dp1[i], &b->ev_tb0[i], &b->ev_tb1[i]})
+            if (!*ev && (e = hipEventCreate(ev)) != hipSuccess) return c->hipfail(e, "event create");
+    if (b->nbuf == 2 && !b->tb_stream &&
+        (e = hipStreamCreateWithFlags(&b->tb_stream, hipStreamNonBlocking)) != hipSuccess)
+        return c->hipfail(e, "traceback stream");
     return SED_OK;
 }
 
@@ -312,33 +340,63 @@ int run_batch(sed_batch *b) {
     sed_ctx *c = b->ctx;
     if (b->npairs == 0) {
         b->ran = true;
+        ++b->runs;
         return SED_OK;
     }
+    const int k = (int)(b->runs & (b->nbuf - 1));
+    const bool want_tb = (b->flags & SED_WANT_SCRIPT) != 0;
+    hipError_t e;
+    if (b->nlog == b->log.size()) {
+        std::array<hipEvent_t, 4> a{};
+        for (auto &x : a)
+            if ((e = hipEventCreate(&x)) != hipSuccess) return c->hipfail(e, "event create");
+        b->log.push_back(a);
+    }
+    const std::array<hipEvent_t, 4> &lg = b->log[b->nlog++];
+    hipStream_t ts = b->nbuf == 2 ? b->tb_stream : c->stream;
     sed_launch L{};
     L.pd = (const sed_pair_desc *)b->d_pd.p;
     L.npairs = b->npairs;
     L.seqa = b->d_seqa.p;
     L.seqb = b->d_seqb.p;
-    L.tb = (b->flags & SED_WANT_SCRIPT) ? (uint32_t *)b->d_tb.p : nullptr;
+    L.tb = want_tb ? (uint32_t *)b->d_tb[k].p : nullptr;
     L.bnd = (uint32_t *)b->d_bnd.p;
-    L.res = (sed_result *)b->d_res.p;
+    L.res = (sed_result *)b->d_res[k].p;
     L.R = b->R;
     L.stream = c->stream;
-    hipError_t e;
-    if ((e = hipEventRecord(b->ev[0], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
+    // buffer k was last read by the traceback of run runs-2
+    if (b->nbuf == 2 && b->runs >= 2 && (e = hipStreamWaitEvent(c->stream, b->ev_tb1[k], 0)) != hipSuccess)
+        return c->hipfail(e, "stream wait");
+    if ((e = hipEventRecord(b->ev_dp0[k], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
+    (void)hipEventRecord(lg[0], c->stream);
     if (b->mode == SED_MODE_I32)
         e = sed_launch_i32(L, b->ip);
     else
         e = sed_launch_f64(L, (const double *)c->gtab.p, b->fp, b->mode == SED_MODE_F64_TYPED);
     if (e != hipSuccess) return c->hipfail(e, "DP kernel launch");
-    if ((e = hipEventRecord(b->ev[1], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
-    if (L.tb) {
+    if ((e = hipEventRecord(b->ev_dp1[k], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
+    (void)hipEventRecord(lg[1], c->stream);
+    if (ts != c->stream && (e = hipStreamWaitEvent(ts, b->ev_dp1[k], 0)) != hipSuccess)
+        return c->hipfail(e, "stream wait");
+    if ((e = hipEventRecord(b->ev_tb0[k], ts)) != hipSuccess) return c->hipfail(e, "event record");
+    (void)hipEventRecord(lg[2], ts);
+    if (want_tb) {
+        L.stream = ts;
         if ((e = sed_launch_traceback(L, (uint32_t *)b->d_ops.p)) != hipSuccess)
             return c->hipfail(e, "traceback kernel launch");
     }
-    if ((e = hipEventRecord(b->ev[2], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
+    if ((e = hipEventRecord(b->ev_tb1[k], ts)) != hipSuccess) return c->hipfail(e, "event record");
+    (void)hipEventRecord(lg[3], ts);
+    ++b->runs;
     b->ran = true;
     return SED_OK;
+}
+
+int sync_batch(sed_batch *b) {
+    sed_ctx *c = b->ctx;
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess && b->tb_stream) e = hipStreamSynchronize(b->tb_stream);
+    return e == hipSuccess ? SED_OK : c->hipfail(e, "kernel execution");
 }
 
 int fetch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32_t *out_len, uint32_t *out_ops,
@@ -347,9 +405,11 @@ int fetch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32_t *
     if (!b->ran) return c->fail(SED_E_STATE, "batch has not been run");
     const int np = b->npairs;
     hipError_t e;
-    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hipfail(e, "kernel execution");
+    int rc = sync_batch(b);
+    if (rc != SED_OK) return rc;
     b->h_res.resize(np);
-    if (np && (e = hipMemcpy(b->h_res.data(), b->d_res.p, sizeof(sed_result) * np, hipMemcpyDeviceToHost)) !=
+    if (np && (e = hipMemcpy(b->h_res.data(), b->d_res[b->cur()].p, sizeof(sed_result) * np,
+                             hipMemcpyDeviceToHost)) !=
                   hipSuccess)
         return c->hipfail(e, "download results");
     for (int p = 0; p < np; ++p) {
@@ -476,19 +536,41 @@ int sed_batch_run(sed_batch *b) {
 
 int sed_batch_sync(sed_batch *b) {
     if (!b) return SED_E_ARG;
-    hipError_t e = hipStreamSynchronize(b->ctx->stream);
-    return e == hipSuccess ? SED_OK : b->ctx->hipfail(e, "stream sync");
+    return sync_batch(b);
 }
 
 int sed_batch_last_times(const sed_batch *b, float *dp_ms, float *tb_ms) {
     if (!b || !b->ran) return SED_E_STATE;
     float a = 0, t = 0;
     if (b->npairs) {
-        if (hipEventElapsedTime(&a, b->ev[0], b->ev[1]) != hipSuccess) return SED_E_DEVICE;
-        if (hipEventElapsedTime(&t, b->ev[1], b->ev[2]) != hipSuccess) return SED_E_DEVICE;
+        const int k = b->cur();
+        if (hipEventElapsedTime(&a, b->ev_dp0[k], b->ev_dp1[k]) != hipSuccess) return SED_E_DEVICE;
+        if (hipEventElapsedTime(&t, b->ev_tb0[k], b->ev_tb1[k]) != hipSuccess) return SED_E_DEVICE;
     }
     if (dp_ms) *dp_ms = a;
     if (tb_ms) *tb_ms = t;
+    return SED_OK;
+}
+
+int sed_batch_times(sed_batch *b, float *dp_ms, float *tb_ms, int max_runs) {
+    if (!b) return SED_E_ARG;
+    int rc = sync_batch(b);
+    if (rc != SED_OK) return rc;
+    const int cnt = (int)std::min<size_t>(b->nlog, (size_t)std::max(0, max_runs));
+    for (int i = 0; i < cnt; ++i) {
+        float a = 0, t = 0;
+        if (hipEventElapsedTime(&a, b->log[i][0], b->log[i][1]) != hipSuccess ||
+            hipEventElapsedTime(&t, b->log[i][2], b->log[i][3]) != hipSuccess)
+            return b->ctx->fail(SED_E_DEVICE, "event timing");
+        if (dp_ms) dp_ms[i] = a;
+        if (tb_ms) tb_ms[i] = t;
+    }
+    return cnt;
+}
+
+int sed_batch_reset_times(sed_batch *b) {
+    if (!b) return SED_E_ARG;
+    b->nlog = 0;
     return SED_OK;
 }
 
@@ -502,7 +584,7 @@ int sed_batch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32
 int sed_batch_device_results(const sed_batch *b, uint64_t *d_dist, uint64_t *d_is_int, uint64_t *d_len,
                              uint64_t *d_ops, uint64_t *ops_words) {
     if (!b) return SED_E_ARG;
-    const uint64_t base = (uint64_t)(uintptr_t)b->d_res.p;
+    const uint64_t base = (uint64_t)(uintptr_t)b->d_res[b->runs ? b->cur() : 0].p;
     if (d_dist) *d_dist = base + offsetof(sed_result, dist);
     if (d_len) *d_len = base + offsetof(sed_result, len);
     if (d_is_int) *d_is_int = base + offsetof(sed_result, is_int);
@@ -517,12 +599,15 @@ int sed_batch_export(sed_batch *b, uint64_t d_dist, uint64_t d_len, uint64_t d_o
     (void)hipSetDevice(c->device);
     if (!b->ran) return c->fail(SED_E_STATE, "batch has not been run");
     const int np = b->npairs;
+    int rc = sync_batch(b);
+    if (rc != SED_OK) return rc;
+    const void *resp = b->d_res[b->cur()].p;
     hipError_t e = hipSuccess;
     if (np && d_dist)
-        e = hipMemcpy2DAsync((void *)(uintptr_t)d_dist, sizeof(double), (const char *)b->d_res.p + offsetof(sed_result, dist),
+        e = hipMemcpy2DAsync((void *)(uintptr_t)d_dist, sizeof(double), (const char *)resp + offsetof(sed_result, dist),
                              sizeof(sed_result), sizeof(double), np, hipMemcpyDeviceToDevice, c->stream);
     if (e == hipSuccess && np && d_len)
-        e = hipMemcpy2DAsync((void *)(uintptr_t)d_len, sizeof(int32_t), (const char *)b->d_res.p + offsetof(sed_result, len),
+        e = hipMemcpy2DAsync((void *)(uintptr_t)d_len, sizeof(int32_t), (const char *)resp + offsetof(sed_result, len),
                              sizeof(sed_result), sizeof(int32_t), np, hipMemcpyDeviceToDevice, c->stream);
     if (e == hipSuccess && d_ops && (b->flags & SED_WANT_SCRIPT) && b->ops_words)
         e = hipMemcpyAsync((void *)(uintptr_t)d_ops, b->d_ops.p, 4 * b->ops_words, hipMemcpyDeviceToDevice, c->stream);
@@ -583,7 +668,7 @@ int sed_full_matrix(sed_ctx *c, const uint8_t *codes_a, int32_t n, const uint8_t
     L.seqb = tmp.d_seqb.p;
     L.tb = nullptr;
     L.bnd = (uint32_t *)tmp.d_bnd.p;
-    L.res = (sed_result *)tmp.d_res.p;
+    L.res = (sed_result *)tmp.d_res[0].p;
     L.R = 4;
     L.stream = c->stream;
     sed_full_out fo{(double *)fD.p, (uint8_t *)fM.p, n, m};

@@ -12,6 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SED_LIBRARY", os.path.join(HERE, "libsed.so"))
 
 SED_WANT_SCRIPT = 1
+SED_PIPELINE = 2
 SED_OPT_MODE = 1
 SED_OPT_ROWS_PER_LANE = 2
 MODE_NAMES = {1: "i32", 2: "f64", 3: "f64-typed"}
@@ -21,6 +22,7 @@ _i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
 _i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
 _u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
 _f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
 
 # (name, restype, argtypes) — every symbol include/sed.h declares
 SIGNATURES = [
@@ -39,6 +41,8 @@ SIGNATURES = [
     ("sed_batch_run", C.c_int, [C.c_void_p]),
     ("sed_batch_sync", C.c_int, [C.c_void_p]),
     ("sed_batch_last_times", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+    ("sed_batch_times", C.c_int, [C.c_void_p, _f32p, _f32p, C.c_int]),
+    ("sed_batch_reset_times", C.c_int, [C.c_void_p]),
     ("sed_batch_results", C.c_int, [C.c_void_p, _f64p, _u8p, _i32p, C.c_void_p, C.c_void_p]),
     ("sed_batch_device_results", C.c_int, [C.c_void_p] + [C.POINTER(C.c_uint64)] * 5),
     ("sed_batch_export", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64]),
@@ -196,14 +200,14 @@ def unpack_ops(ops_words, ops_off, p, length):
 class Batch:
     """Device-resident batch (sed_batch_*): upload once, run many times."""
 
-    def __init__(self, ctx, packed, want_script):
+    def __init__(self, ctx, packed, want_script, pipeline=False):
         self.ctx = ctx
         self._lib = ctx._lib
         self.packed = packed
         self.want_script = want_script
+        flags = (SED_WANT_SCRIPT if want_script else 0) | (SED_PIPELINE if pipeline else 0)
         self.ptr = self._lib.sed_batch_create(ctx.ptr, packed.codes_a, packed.off_a, packed.len_a, packed.codes_b,
-                                              packed.off_b, packed.len_b, packed.npairs,
-                                              SED_WANT_SCRIPT if want_script else 0)
+                                              packed.off_b, packed.len_b, packed.npairs, flags)
         if not self.ptr:
             msg = self._lib.sed_last_error(ctx.ptr)
             raise SedError("sed_batch_create failed: %s" % (msg.decode() if msg else ""))
@@ -237,6 +241,18 @@ class Batch:
         a, b = C.c_float(), C.c_float()
         self.ctx._check(self._lib.sed_batch_last_times(self.ptr, C.byref(a), C.byref(b)), "sed_batch_last_times")
         return a.value, b.value
+
+    def times(self, max_runs=4096):
+        """(dp_ms[], traceback_ms[]) of every run since reset_times(), from HIP events."""
+        a = np.zeros(max_runs, np.float32)
+        b = np.zeros(max_runs, np.float32)
+        cnt = self._lib.sed_batch_times(self.ptr, a, b, max_runs)
+        if cnt < 0:
+            self.ctx._check(cnt, "sed_batch_times")
+        return a[:cnt].astype(np.float64), b[:cnt].astype(np.float64)
+
+    def reset_times(self):
+        self._lib.sed_batch_reset_times(self.ptr)
 
     def work(self):
         a, b = C.c_double(), C.c_double()
