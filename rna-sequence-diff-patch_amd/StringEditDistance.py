@@ -1,0 +1,564 @@
+"""StringEditDistance — drop-in replacement for the reference module of the
+same name (plsakr/rna-sequence-diff-patch, StringEditDistance.py), backed by
+the MI355X engine (libsed.so, HIP kernels for gfx950).
+
+Same names, same argument meaning, same globals and the same exceptions, so
+gui.py, IRMethods.py, timing.py and performance.py run unchanged with this
+directory on sys.path (or as the CWD):
+
+    default_costs, user_costs, reload_user_costs()       StringEditDistance.py:6-27
+    Edge, Node                                            :31-71
+    cost(char1, char2, userCosts=False)                   :76-89
+    min_cost(dp, i, j, str1, str2, userCosts=False)       :92-128
+    wagnerFisher(str1, str2, userCosts=False) -> dp       :133-224
+    create_paths(dp) -> paths                             :228-271
+    generate_es(path, str1, str2) -> edit script          :274-334
+    generate_rev_es(es), generate_sequence_from_es(es)    :338-377
+    patching(es, str1) -> (error_code, str)               :380-457
+
+What runs where.  wagnerFisher checks the cost table (raising the reference's
+KeyError) and asks the GPU for dp[n][m]; the returned dp is a lazy matrix:
+len(dp), len(dp[0]) and dp[n][m].value need nothing more, any other cell
+materialises the whole matrix (values, int/float typing and the co-optimal
+edges) with one fp64 kernel.  create_paths(dp)[0] — the path the GUI and
+every edit-script consumer takes first — comes from the device traceback;
+later paths are enumerated on the host in the reference's BFS order over the
+materialised edges.  Deliberate differences: no import-time demo print
+(:463-471), and create_paths never blocks (the reference's bounded Queue
+deadlocks once live paths exceed (n+1)(m+1), :237,265).
+
+There is no CPU fallback for the DP: without libsed.so or a HIP device the
+functions raise sedgpu.SedError.
+"""
+import json
+from collections import deque
+
+import numpy as np
+
+import sedcost
+import sedgpu
+
+# Step 1 (reference :6-18): cost tables from the current working directory, at import.
+with open('costs.json', 'r') as f:
+    default_costs = json.load(f)
+
+try:
+    with open('user_costs.json', 'r') as f:
+        user_costs = json.load(f)
+except (OSError, IOError):
+    user_costs = default_costs
+    print('Could not find user costs file')
+
+
+def reload_user_costs():
+    """Re-read user_costs.json into the module global (reference :24-27)."""
+    global user_costs
+    with open('user_costs.json', 'r') as f:
+        user_costs = json.load(f)
+
+
+def _table(userCosts):
+    return user_costs if userCosts else default_costs
+
+
+class Edge:
+    """source -> destination via operation ('insert' | 'delete' | 'update')."""
+
+    def __init__(self, source, destination, operation):
+        self.source = source
+        self.destination = destination
+        self.operation = operation
+
+
+class Node:
+    """A DP cell: i/j are string indices (row-1, col-1), value the cell cost."""
+
+    def __init__(self, i, j, value=0):
+        self.i = i
+        self.j = j
+        self.value = value
+        self.edges = []
+        self.incoming_edges = []
+        self.visited = False
+
+    def add_neighbor(self, dest, operation):
+        e = Edge(self, dest, operation)
+        self.edges.append(e)
+        dest.incoming_edges.append(e)
+
+    def __repr__(self):
+        return str(self.value)
+
+
+def cost(char1, char2, userCosts=False):
+    """int 0 for a case-insensitive match, else the table's update cost (reference :76-89)."""
+    if char1.lower() == char2.lower():
+        return 0
+    return _table(userCosts)['update'][char1][char2]
+
+
+def min_cost(dp, i, j, str1, str2, userCosts=False):
+    """(value, [insert, delete, update] op tuples or None) for cell (i, j) (reference :92-128)."""
+    table = _table(userCosts)
+    cands = [dp[i][j - 1].value + table['insert'],
+             dp[i - 1][j].value + table['delete'],
+             dp[i - 1][j - 1].value + cost(str1[i - 1], str2[j - 1], userCosts)]
+    val = min(cands)
+    ops = [None, None, None]
+    if cands[0] == val:
+        ops[0] = (i, j - 1, 'insert')
+    if cands[1] == val:
+        ops[1] = (i - 1, j, 'delete')
+    if cands[2] == val:
+        ops[2] = (i - 1, j - 1, 'update')
+    return val, ops
+
+
+# ---------------------------------------------------------------------------
+# the lazy dp matrix
+# ---------------------------------------------------------------------------
+_OPNAME = ('insert', 'delete', 'update')
+_MASKBIT = {'insert': 1, 'delete': 2, 'update': 4}
+
+
+class Cell(Node):
+    """Node view of cell (row, col) of a DPMatrix; identical surface to Node."""
+
+    __slots__ = ('_dp', 'row', 'col', 'visited', '_in', '_out')
+
+    def __init__(self, dp, row, col):  # noqa: D401 — Node.__init__ deliberately not called
+        self._dp = dp
+        self.row = row
+        self.col = col
+        self.visited = False
+        self._in = None
+        self._out = None
+
+    @property
+    def i(self):
+        return self.row - 1
+
+    @property
+    def j(self):
+        return self.col - 1
+
+    @property
+    def value(self):
+        return self._dp._value(self.row, self.col)
+
+    @property
+    def incoming_edges(self):
+        if self._in is None:
+            self._in = self._dp._incoming(self.row, self.col)
+        return self._in
+
+    @property
+    def edges(self):
+        if self._out is None:
+            self._out = self._dp._outgoing(self.row, self.col)
+        return self._out
+
+    def add_neighbor(self, dest, operation):
+        e = Edge(self, dest, operation)
+        self.edges.append(e)
+        dest.incoming_edges.append(e)
+
+    def __repr__(self):
+        return str(self.value)
+
+
+class _Row:
+    __slots__ = ('_dp', '_r')
+
+    def __init__(self, dp, r):
+        self._dp = dp
+        self._r = r
+
+    def __len__(self):
+        return self._dp.m + 1
+
+    def __getitem__(self, j):
+        w = self._dp.m + 1
+        if isinstance(j, slice):
+            return [self._dp.cell(self._r, k) for k in range(*j.indices(w))]
+        if j < 0:
+            j += w
+        if not 0 <= j < w:
+            raise IndexError('list index out of range')
+        return self._dp.cell(self._r, j)
+
+    def __iter__(self):
+        for j in range(self._dp.m + 1):
+            yield self._dp.cell(self._r, j)
+
+    def __repr__(self):
+        return '[' + ', '.join(repr(c) for c in self) + ']'
+
+
+class DPMatrix:
+    """(n+1) x (m+1) matrix of Cell views; what wagnerFisher returns."""
+
+    def __init__(self, str1, str2, plan):
+        self.str1, self.str2 = str1, str2
+        self.n, self.m = len(str1), len(str2)
+        self._plan = plan
+        self._codes = (plan.encode(str1), plan.encode(str2))
+        self._final = None
+        self._full = None
+        self._script = None
+        self._cells = {}
+        self._edges = {}
+        self._rows = {}
+
+    # -- engine calls --
+    def _run(self, want_script):
+        ctx = sedgpu.context()
+        ctx.set_costs(self._plan)
+        packed = sedgpu.PackedPairs([self._codes[0]], [self._codes[1]])
+        dist, is_int, ln, ops = ctx.run(packed, want_script)
+        d = float(dist[0])
+        self._final = int(d) if is_int[0] else d
+        if want_script:
+            self._script = sedgpu.unpack_ops(ops, packed.ops_off, 0, int(ln[0]))
+
+    def _materialise(self):
+        if self._full is None:
+            ctx = sedgpu.context()
+            ctx.set_costs(self._plan)
+            D, M = ctx.full_matrix(self._codes[0], self._codes[1])
+            self._full = (D, M)
+        return self._full
+
+    def script(self):
+        """Canonical op codes (0 insert, 1 delete, 2 update), origin -> sink."""
+        if self._script is None:
+            self._run(True)
+        return self._script
+
+    # -- cell access --
+    def _value(self, r, c):
+        if r == self.n and c == self.m and self._final is not None:
+            return self._final
+        D, M = self._materialise()
+        v = float(D[r, c])
+        return int(v) if M[r, c] & 8 else v
+
+    def _edge(self, r, c, op):
+        key = (r, c, op)
+        e = self._edges.get(key)
+        if e is None:
+            pr, pc = (r, c - 1) if op == 'insert' else ((r - 1, c) if op == 'delete' else (r - 1, c - 1))
+            e = Edge(self.cell(pr, pc), self.cell(r, c), op)
+            self._edges[key] = e
+        return e
+
+    def _incoming(self, r, c):
+        M = self._materialise()[1]
+        mask = int(M[r, c]) & 7
+        return [self._edge(r, c, op) for op in _OPNAME if mask & _MASKBIT[op]]
+
+    def _outgoing(self, r, c):
+        M = self._materialise()[1]
+        out = []
+        # reference creation order: row 0 first, then column 0, then the interior row-major
+        cand = [('insert', r, c + 1), ('delete', r + 1, c), ('update', r + 1, c + 1)]
+        if c == 0 and r > 0:
+            cand = [cand[1], cand[0], cand[2]]
+        for op, rr, cc in cand:
+            if rr <= self.n and cc <= self.m and int(M[rr, cc]) & _MASKBIT[op]:
+                out.append(self._edge(rr, cc, op))
+        return out
+
+    def cell(self, r, c):
+        k = (r, c)
+        x = self._cells.get(k)
+        if x is None:
+            x = Cell(self, r, c)
+            self._cells[k] = x
+        return x
+
+    # -- list protocol --
+    def __len__(self):
+        return self.n + 1
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[k] for k in range(*i.indices(self.n + 1))]
+        if i < 0:
+            i += self.n + 1
+        if not 0 <= i <= self.n:
+            raise IndexError('list index out of range')
+        row = self._rows.get(i)
+        if row is None:
+            row = self._rows[i] = _Row(self, i)
+        return row
+
+    def __iter__(self):
+        for i in range(self.n + 1):
+            yield self[i]
+
+    def __repr__(self):
+        return '[' + ', '.join(repr(r) for r in self) + ']'
+
+
+def wagnerFisher(str1, str2, userCosts=False):
+    """Weighted Wagner–Fischer matrix of str1 (rows) -> str2 (columns) (reference :133-224)."""
+    table = _table(userCosts)
+    sedcost.check_pair(table, str1, str2)
+    dp = DPMatrix(str1, str2, sedcost.build_plan(table, [str1], [str2]))
+    dp._run(False)
+    return dp
+
+
+# ---------------------------------------------------------------------------
+# paths
+# ---------------------------------------------------------------------------
+class Path(list):
+    """A co-optimal path (list of Cell, origin -> sink) with its op codes."""
+
+    def __init__(self, cells, ops=None):
+        super().__init__(cells)
+        self.ops = ops
+
+
+def _cells_of_script(dp, ops):
+    r = c = 0
+    cells = [dp.cell(0, 0)]
+    for op in ops:
+        if op != 1:
+            c += 1
+        if op != 0:
+            r += 1
+        cells.append(dp.cell(r, c))
+    return Path(cells, ops)
+
+
+def _bfs_paths(dp):
+    """Every co-optimal path in the reference's order (BFS from the sink over
+    incoming edges stored insert, delete, update), without its queue bound."""
+    M = dp._materialise()[1]
+    q = deque([((dp.n, dp.m),)])
+    while q:
+        p = q.popleft()
+        r, c = p[-1]
+        if r == 0 and c == 0:
+            yield p
+        mask = int(M[r, c]) & 7
+        for bit, (pr, pc) in ((1, (r, c - 1)), (2, (r - 1, c)), (4, (r - 1, c - 1))):
+            if mask & bit:
+                q.append(p + ((pr, pc),))
+
+
+class PathList:
+    """Lazy result of create_paths(dp): element 0 is the device's canonical
+    path; the rest are enumerated on demand, in the reference's order."""
+
+    def __init__(self, dp):
+        self._dp = dp
+        self._done = []
+        self._gen = None
+        self._exhausted = False
+
+    def _next(self):
+        if not self._done:
+            self._done.append(_cells_of_script(self._dp, self._dp.script()))
+            return True
+        if self._exhausted:
+            return False
+        if self._gen is None:
+            self._gen = _bfs_paths(self._dp)
+            next(self._gen)  # the first BFS path is the canonical one already returned
+        try:
+            p = next(self._gen)
+        except StopIteration:
+            self._exhausted = True
+            return False
+        cells = [self._dp.cell(r, c) for r, c in reversed(p)]
+        ops = []
+        for a, b in zip(cells, cells[1:]):
+            ops.append(2 if (b.row > a.row and b.col > a.col) else (1 if b.row > a.row else 0))
+        self._done.append(Path(cells, np.array(ops, np.uint8)))
+        return True
+
+    def __getitem__(self, k):
+        if isinstance(k, slice):
+            return list(self)[k]
+        if k < 0:
+            return list(self)[k]
+        while len(self._done) <= k:
+            if not self._next():
+                raise IndexError('list index out of range')
+        return self._done[k]
+
+    def __iter__(self):
+        k = 0
+        while True:
+            if k >= len(self._done) and not self._next():
+                return
+            yield self._done[k]
+            k += 1
+
+    def __len__(self):
+        while self._next():
+            pass
+        return len(self._done)
+
+    def __bool__(self):
+        return True  # a dp always has at least one co-optimal path
+
+
+def create_paths(dp):
+    """All co-optimal paths, shortest first (reference :228-271)."""
+    if isinstance(dp, DPMatrix):
+        dp[dp.n][dp.m].visited = True
+        return PathList(dp)
+    return _create_paths_graph(dp)
+
+
+def _create_paths_graph(dp):
+    """The same enumeration over a caller-built Node graph (list of lists)."""
+    goal = dp[0][0]
+    src = dp[len(dp) - 1][len(dp[0]) - 1]
+    src.visited = True
+    q = deque([[src]])
+    out = []
+    while q:
+        p = q.popleft()
+        if p[-1] is goal:
+            out.append(p)
+        for e in p[-1].incoming_edges:
+            if not any(x is e.source for x in p):
+                q.append(p + [e.source])
+    return [p[::-1] for p in out]
+
+
+# ---------------------------------------------------------------------------
+# edit scripts
+# ---------------------------------------------------------------------------
+def _op_record(op, str1, str2, ni, nj):
+    return {"operation": op,
+            "source": {"character": str1[ni], "index": ni},
+            "destination": {"character": str2[nj], "index": nj}}
+
+
+def generate_es(path, str1, str2):
+    """One dict per edge of the path, origin -> sink (reference :274-334).
+    source/destination describe the edge's destination cell (i, j); index -1
+    (row 0 / column 0) reads str[-1], the last character, as the reference does."""
+    if len(path) < 2:
+        path[1]  # IndexError, as the reference's `next = path[1]`
+    ops = getattr(path, 'ops', None)
+    es = []
+    if ops is not None and len(ops) == len(path) - 1:
+        for op, nxt in zip(ops, path[1:]):
+            es.append(_op_record(_OPNAME[op], str1, str2, nxt.i, nxt.j))
+        return es
+    for cur, nxt in zip(path, path[1:]):
+        edge = [e for e in cur.edges if e.source is cur and e.destination is nxt]
+        if not edge:
+            edge = [e for e in cur.edges if e.source == cur and e.destination == nxt]
+        es.append(_op_record(edge[0].operation, str1, str2, nxt.i, nxt.j))  # IndexError if not an edge
+    return es
+
+
+def generate_rev_es(es):
+    """The script that turns str2 back into str1 (reference :338-369)."""
+    out = []
+    for e in es:
+        op = e['operation']
+        if op == 'insert':
+            new = {'operation': 'delete', 'source': e['destination'], 'destination': e['source']}
+        elif op == 'delete':
+            new = {'operation': 'insert',
+                   'source': {'index': e['destination']['index'] - 1, 'character': e['destination']['character']},
+                   'destination': e['source']}
+        elif op == 'update':
+            new = {'operation': 'update', 'source': e['destination'], 'destination': e['source']}
+        else:  # the reference reuses the previous iteration's bindings (or raises NameError on the first)
+            new = {'operation': out[-1]['operation'], 'source': out[-1]['source'],
+                   'destination': out[-1]['destination']} if out else None
+            if new is None:
+                raise UnboundLocalError("local variable 'new_operation' referenced before assignment")
+        out.append(new)
+    return out
+
+
+def generate_sequence_from_es(es):
+    """The source string a script was generated from (reference :371-377)."""
+    return ''.join(op['source']['character'] for op in es if op['operation'] != 'insert')
+
+
+def patching(es, str1):
+    """Apply an edit script to str1 -> (error_code, patched) (reference :380-457).
+    error_code: 0 str1 is the script's source, 1 str1 is at least as long (warn),
+    -1 str1 is shorter (returns (-1, ''))."""
+    original = generate_sequence_from_es(es)
+    if str1 == original:
+        error_code = 0
+    elif len(str1) >= len(original):
+        error_code = 1
+    else:
+        return (-1, '')
+    out = str1
+    removed = inserted = 0
+    for rec in es:
+        op = rec['operation']
+        if op != 'insert':
+            at = rec['source']['index'] + removed + inserted
+        else:
+            at = rec['destination']['index']
+        if op == 'update':
+            out = out[:at] + rec['destination']['character'] + out[at + 1:]
+        elif op == 'delete':
+            out = out[:at] + out[at + 1:]
+            removed -= 1
+        elif op == 'insert':
+            out = out[:at] + rec['destination']['character'] + out[at:]
+            inserted += 1
+    return (error_code, out)
+
+
+# ---------------------------------------------------------------------------
+# batch extensions (not in the reference): one launch for many pairs
+# ---------------------------------------------------------------------------
+def distance_batch(strs1, strs2, userCosts=False):
+    """[dp[n][m].value for each (str1, str2)] — one GPU launch; same typing and KeyErrors."""
+    table = _table(userCosts)
+    for a, b in zip(strs1, strs2):
+        sedcost.check_pair(table, a, b)
+    if not strs1:
+        return []
+    plan = sedcost.build_plan(table, strs1, strs2)
+    ctx = sedgpu.context()
+    ctx.set_costs(plan)
+    packed = sedgpu.PackedPairs([plan.encode(a) for a in strs1], [plan.encode(b) for b in strs2])
+    dist, is_int, _, _ = ctx.run(packed, False)
+    return [int(d) if t else float(d) for d, t in zip(dist.tolist(), is_int.tolist())]
+
+
+def edit_script_batch(strs1, strs2, userCosts=False):
+    """[(value, generate_es(create_paths(dp)[0], s1, s2))] for each pair — one GPU launch."""
+    table = _table(userCosts)
+    for a, b in zip(strs1, strs2):
+        sedcost.check_pair(table, a, b)
+    if not strs1:
+        return []
+    plan = sedcost.build_plan(table, strs1, strs2)
+    ctx = sedgpu.context()
+    ctx.set_costs(plan)
+    packed = sedgpu.PackedPairs([plan.encode(a) for a in strs1], [plan.encode(b) for b in strs2])
+    dist, is_int, ln, ops = ctx.run(packed, True)
+    out = []
+    for p, (a, b) in enumerate(zip(strs1, strs2)):
+        codes = sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln[p]))
+        r = c = 0
+        es = []
+        for op in codes:
+            if op != 1:
+                c += 1
+            if op != 0:
+                r += 1
+            es.append(_op_record(_OPNAME[op], a, b, r - 1, c - 1))
+        v = float(dist[p])
+        out.append((int(v) if is_int[p] else v, es))
+    return out

@@ -1,0 +1,136 @@
+"""GPU: the drop-in StringEditDistance module end to end (wagnerFisher on the
+device, the dp proxy, create_paths, generate_es ...) against the golden
+fixtures generated from the reference, including the callers' idioms
+(IRMethods.wf_score, the GUI's table / script loops)."""
+import hashlib
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def SED():
+    cwd = os.getcwd()
+    os.chdir(GOLDEN)
+    try:
+        sys.modules.pop("StringEditDistance", None)
+        mod = importlib.import_module("StringEditDistance")
+    finally:
+        os.chdir(cwd)
+    return mod
+
+
+def es_compact(es):
+    return [[e["operation"][0], e["source"]["character"], e["source"]["index"],
+             e["destination"]["character"], e["destination"]["index"]] for e in es]
+
+
+def wf_score(SED, seq1, seq2, user_cost=False):
+    """IRMethods.wf_score's body (IRMethods.py:435-440), verbatim in behaviour."""
+    dp = SED.wagnerFisher(seq1, seq2, user_cost)
+    cost = dp[len(dp) - 1][len(dp[0]) - 1].value
+    return 1 / (1 + cost)
+
+
+def test_g1_through_the_module(SED):
+    for r in load_golden("g1_small.json"):
+        dp = SED.wagnerFisher(r["s1"], r["s2"], r["user"])
+        v = dp[len(dp) - 1][len(dp[0]) - 1].value
+        assert (float(v), isinstance(v, int)) == (float.fromhex(r["dist"][0]), r["dist"][1])
+        paths = SED.create_paths(dp)
+        first = "".join("idu"[o] for o in paths[0].ops)
+        assert first == r["canon"]
+        # the GUI loop: every cell value, then every path's script
+        cells = [[float(c.value), isinstance(c.value, int)] for row in dp for c in row]
+        assert cells == [[float.fromhex(h), bool(ii)] for h, ii, _ in r["cells"]]
+        if r["paths"] != "deadlock":
+            ops = ["".join("idu"[o] for o in p.ops) for p in paths]
+            assert ops == r["paths"][:len(ops)] and len(ops) == r["npaths"]
+            for p, es in zip(paths, r["es"]):
+                if isinstance(es, dict):
+                    with pytest.raises(IndexError):
+                        SED.generate_es(p, r["s1"], r["s2"])
+                else:
+                    assert es_compact(SED.generate_es(p, r["s1"], r["s2"])) == es
+
+
+def test_g6_errors_typing_repr(SED):
+    for r in load_golden("g6_errors.json"):
+        if "error" in r:
+            with pytest.raises(KeyError) as ei:
+                SED.wagnerFisher(r["s1"], r["s2"], r["user"])
+            assert [str(a) for a in ei.value.args] == r["error"][1]
+            continue
+        dp = SED.wagnerFisher(r["s1"], r["s2"], r["user"])
+        v = dp[-1][-1].value
+        assert (float(v), isinstance(v, int)) == (float.fromhex(r["dist"][0]), r["dist"][1])
+        assert repr(dp[-1][-1]) == r["repr"]
+        if r.get("matrix_repr") is not None:
+            assert repr(dp) == r["matrix_repr"]
+        if "es0" in r:
+            assert es_compact(SED.generate_es(SED.create_paths(dp)[0], r["s1"], r["s2"])) == r["es0"]
+        if "es_error" in r:
+            with pytest.raises(IndexError):
+                SED.generate_es(SED.create_paths(dp)[0], r["s1"], r["s2"])
+
+
+def test_g2_canonical_scripts(SED):
+    for r in load_golden("g2_medium.json"):
+        dp = SED.wagnerFisher(r["s1"], r["s2"], r["user"])
+        assert dp[-1][-1].value == float.fromhex(r["dist"][0])
+        es = SED.generate_es(SED.create_paths(dp)[0], r["s1"], r["s2"])
+        assert hashlib.sha256(json.dumps(es_compact(es)).encode()).hexdigest() == r["es_sha256"]
+        assert SED.patching(es, r["s1"]) == (0, r["s2"])
+        assert SED.patching(SED.generate_rev_es(es), r["s2"]) == (0, r["s1"])
+
+
+def test_g4_wf_score_all_vs_all(SED):
+    g4 = load_golden("g4_wf_score.json")
+    seqs = g4["seqs"]
+    for user, key in ((False, "wf_score"), (True, "wf_score_user")):
+        want = [[float.fromhex(x) for x in row] for row in g4[key]]
+        got = [[wf_score(SED, a, b, user) for b in seqs] for a in seqs]
+        assert got == want
+        # one launch for the whole matrix
+        vals = SED.distance_batch([a for a in seqs for _ in seqs], [b for _ in seqs for b in seqs], user)
+        assert [[1 / (1 + vals[i * len(seqs) + j]) for j in range(len(seqs))] for i in range(len(seqs))] == want
+
+
+def test_all_vs_all_single_rank(SED):
+    import sedshard
+    g4 = load_golden("g4_wf_score.json")
+    M = sedshard.all_vs_all(g4["seqs"], False)
+    want = np.array([[1 / float.fromhex(x) - 1 for x in row] for row in g4["wf_score"]])
+    assert np.allclose(M, want, rtol=0, atol=1e-9)
+
+
+def test_edit_script_batch_matches_single_calls(SED):
+    g5 = load_golden("g5_patching.json")
+    for user in (False, True):
+        recs = [r for r in g5 if r["user"] == user]
+        out = SED.edit_script_batch([r["s1"] for r in recs], [r["s2"] for r in recs], user)
+        for r, (v, es) in zip(recs, out):
+            assert es_compact(es) == r["es"]
+
+
+def test_reload_user_costs(SED, tmp_path, monkeypatch):
+    table = json.load(open(os.path.join(GOLDEN, "user_costs.json")))
+    table["insert"] = 5.0
+    (tmp_path / "user_costs.json").write_text(json.dumps(table))
+    monkeypatch.chdir(tmp_path)
+    old = SED.user_costs
+    try:
+        SED.reload_user_costs()
+        assert SED.wagnerFisher("", "AC", True)[-1][-1].value == 10.0
+        SED.user_costs["insert"] = 1.0  # the GUI edits the dict in place
+        assert SED.wagnerFisher("", "AC", True)[-1][-1].value == 2.0
+    finally:
+        SED.user_costs = old
