@@ -127,18 +127,27 @@ def main():
     ap.add_argument("--rows-per-lane", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-json", default="", help="per-launch HBM traffic from a rocprofv3 PMC pass")
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_dp_i32_c4.json"),
+                    help="per-launch HBM traffic of the DP kernel from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
+                         "(tools/profile_round.sh + tools/summarize_profile.py); used when its workload matches")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (default); gloo only to rehearse ranks sharing one GPU")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
+    local = local % max(1, torch.cuda.device_count())  # ranks > GPUs only in a gloo rehearsal
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    tdev = torch.device("cuda", local) if args.dist_backend == "nccl" else torch.device("cpu")
 
     def barrier():
         if dist is not None:
@@ -182,7 +191,7 @@ def main():
     elapsed = time.perf_counter() - t0
     dp_ms, tb_ms = batch.times()
     if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_per_step = elapsed * 1e3 / args.steps
@@ -191,23 +200,22 @@ def main():
     # ---- results: gather to rank 0 over RCCL (timed separately) ----
     gather_ms = None
     if dist is not None:
+        import sedshard
         words = int(packed.ops_off[P])
         t_dist = torch.empty(P, dtype=torch.float64, device="cuda")
         t_len = torch.empty(P, dtype=torch.int32, device="cuda")
         t_ops = torch.empty(max(words, 1), dtype=torch.int32, device="cuda")
         batch.export(t_dist.data_ptr(), t_len.data_ptr(), t_ops.data_ptr() if want_script else 0)
+        sends = [t.to(tdev) for t in (t_dist, t_len, t_ops)]
         barrier()
         g0 = time.perf_counter()
-        outs = []
-        for t in (t_dist, t_len, t_ops):
-            lst = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
-            dist.gather(t, lst, dst=0)
-            outs.append(lst)
+        got = sedshard.gather_to_rank0(sends, world, rank)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - g0) * 1e3
         if rank == 0:
-            all_dist = torch.cat(outs[0]).cpu().numpy()
-            log("rank 0: gathered %d results (%.2f ms)" % (len(all_dist), gather_ms))
+            log("rank 0: gathered %d results + %d script words over %s (%.2f ms)"
+                % (got[0].numel(), got[2].numel(), args.dist_backend, gather_ms))
+            assert got[0].numel() == P * world
 
     # ---- verification (untimed) ----
     d_gpu, ii_gpu, ln_gpu, ops = batch.results()
@@ -250,7 +258,9 @@ def main():
     traffic = None
     if args.pmc_json and os.path.exists(args.pmc_json):
         with open(args.pmc_json) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            pm = json.load(f)
+        if pm.get("workload") == desc and batch.mode == "i32" and want_script and P == WORKLOADS[args.workload][0]:
+            traffic = pm.get("hbm_bytes_per_launch")
     cyc = CELL_CYCLES.get((batch.mode, want_script))
     rate = cells / (dp_avg * 1e-3)
     line = {
