@@ -48,6 +48,11 @@ WORKLOADS = {
            "config 3: 65536 pairs of 512x512 synthetic ACGU, costs.json, distance + edit script"),
     "c2": (1, 4096, 4096, "user_costs.json",
            "config 2: 1 pair 4096x4096 synthetic ACGU, user_costs.json, distance + edit script"),
+    "iupac": (8192, 1024, 1024, "costs.json",
+              "fp64 path: 8192 pairs of 1024x1024 synthetic 15-symbol IUPAC, costs.json, distance + edit script"),
+    "c5": (500, 0, 0, "costs.json",
+           "config 5 (synthetic): all-vs-all wf_score over 500 ACGU sequences of length U[24,32], costs.json, "
+           "250000 ordered pairs, distance only"),
 }
 
 
@@ -55,14 +60,23 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def gen_codes(pair_ids, n, m):
+def gen_codes(pair_ids, n, m, iupac=False):
+    gen = synth.iupac_codes if iupac else synth.pair_codes
     A = np.empty((len(pair_ids), n), np.uint8)
     B = np.empty((len(pair_ids), m), np.uint8)
     for s in range(0, len(pair_ids), 512):
         ids = pair_ids[s:s + 512]
-        A[s:s + len(ids)] = synth.pair_codes(ids, n, 0)
-        B[s:s + len(ids)] = synth.pair_codes(ids, m, 1)
+        A[s:s + len(ids)] = gen(ids, n, 0)
+        B[s:s + len(ids)] = gen(ids, m, 1)
     return A, B
+
+
+def gen_all_vs_all(nseq, lo=24, hi=32):
+    """Config 5 stand-in: nseq synthetic ACGU sequences, every ordered pair (query = str1)."""
+    ids = np.arange(nseq, dtype=np.uint64)
+    ln = synth.lengths(ids, lo, hi)
+    seqs = [synth.pair_codes([i], int(l), 0)[0] for i, l in zip(ids, ln)]
+    return [seqs[a] for a in range(nseq) for _ in range(nseq)], [seqs[b] for _ in range(nseq) for b in range(nseq)]
 
 
 def script_costs(plan, A, B, ln, ops, ops_off):
@@ -157,20 +171,31 @@ def main():
     P, n, m, costs_file, desc = WORKLOADS[args.workload]
     if args.pairs:
         P = args.pairs
-    want_script = not args.no_script
+    want_script = not args.no_script and args.workload != "c5"
+    iupac = args.workload == "iupac"
     with open(os.path.join(REPO, "tests", "golden", costs_file)) as f:
         table = json.load(f)
-    plan = sedcost.build_plan(table, ["ACGU"], ["ACGU"])
-    ids = np.arange(rank * P, (rank + 1) * P, dtype=np.uint64)
+    alpha = synth.IUPAC if iupac else synth.ALPHABET
+    plan = sedcost.build_plan(table, [alpha], [alpha])
     t0 = time.perf_counter()
-    A, B = gen_codes(ids, n, m)
+    if args.workload == "c5":
+        import sedshard
+        lo, hi = sedshard.shard_range(P, world, rank)  # query rows of this rank
+        qa, qb = gen_all_vs_all(P)
+        qa, qb = qa[lo * P:hi * P], qb[lo * P:hi * P]
+        packed = sedgpu.PackedPairs(qa, qb)
+        A = B = None
+        P = len(qa)
+    else:
+        ids = np.arange(rank * P, (rank + 1) * P, dtype=np.uint64)
+        A, B = gen_codes(ids, n, m, iupac)
+        packed = sedgpu.PackedPairs.from_arrays(A, B)
     log("rank %d: generated %d pairs in %.1fs" % (rank, P, time.perf_counter() - t0))
 
     ctx = sedgpu.Context(local)
     if args.rows_per_lane:
         ctx.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, args.rows_per_lane)
     ctx.set_costs(plan)
-    packed = sedgpu.PackedPairs.from_arrays(A, B)
     t0 = time.perf_counter()
     pipeline = want_script and not args.no_pipeline
     batch = sedgpu.Batch(ctx, packed, want_script, pipeline=pipeline)
@@ -220,7 +245,7 @@ def main():
     # ---- verification (untimed) ----
     d_gpu, ii_gpu, ln_gpu, ops = batch.results()
     check = {}
-    if want_script:
+    if want_script and A is not None:
         good = 0
         for s0 in range(0, P, 256):
             sl = slice(s0, min(P, s0 + 256))
@@ -229,7 +254,7 @@ def main():
             good += int((ok & same).sum())
         check["script_valid_rate"] = good / P
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and A is not None:
         try:
             threads = min(16, len(os.sched_getaffinity(0)))
         except AttributeError:

@@ -77,20 +77,12 @@ __device__ __forceinline__ uint64_t load_sc1_u64(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// tb words a lane stores per 4-step group: 4 steps * R rows * 2 bits / 32.
-template <int R> struct TbWords { static constexpr int N = R / 4; };
+// Traceback codes are stored per "group" of G = 64/R steps: G steps x R rows x 2 bits
+// = 16 bytes per lane, one dwordx4 store; the wave writes 1 KiB contiguous.
+template <int R> struct Grp { static constexpr int G = 64 / R; };
 
-template <int NW>
-__device__ __forceinline__ void store_tb(uint32_t *p, const uint32_t (&w)[NW]) {
-    if constexpr (NW == 1) {
-        p[0] = w[0];
-    } else if constexpr (NW == 2) {
-        *reinterpret_cast<uint2 *>(p) = make_uint2(w[0], w[1]);
-    } else {
-#pragma unroll
-        for (int h = 0; h < NW; h += 4)
-            *reinterpret_cast<uint4 *>(p + h) = make_uint4(w[h], w[h + 1], w[h + 2], w[h + 3]);
-    }
+__device__ __forceinline__ void store_tb(uint32_t *p, const uint32_t (&w)[4]) {
+    *reinterpret_cast<uint4 *>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 // ---------------------------------------------------------------------------
@@ -105,7 +97,7 @@ __device__ __forceinline__ void store_tb(uint32_t *p, const uint32_t (&w)[NW]) {
 template <int R, bool TB>
 __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                          uint32_t &bottom, uint32_t &selv, uint32_t &tch, uint32_t &sch,
-                                         uint32_t &outc, uint32_t (&W)[TbWords<R>::N], const int u,
+                                         uint32_t &outc, uint32_t (&W)[4], const int u,
                                          const uint32_t kins, const uint32_t kdel) {
     const uint32_t topv = dpp_shr1(tch, bottom);  // cell above the band, this column (lane 0: chunk)
     selv = dpp_shr1(sch, selv);                   // perm selector of this column's str2 symbol
@@ -151,12 +143,12 @@ __device__ __forceinline__ void i32_reset(uint32_t (&V)[R], uint32_t &top_prev, 
 template <int R, bool TB, bool SLOW>
 __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                           uint32_t &bottom, uint32_t &selv, uint32_t &tch, uint32_t &sch,
-                                          uint32_t &outc, uint32_t (&W)[TbWords<R>::N], const int s0,
+                                          uint32_t &outc, uint32_t (&W)[4], const int s0,
                                           const int lane, const int row0, const uint32_t kins, const uint32_t kdel,
                                           const uint32_t del, const int cap_step, const int cap_lane,
                                           const int cap_row, uint32_t &cap) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < Grp<R>::G; ++u) {
         i32_step<R, TB>(V, cv, top_prev, bottom, selv, tch, sch, outc, W, u, kins, kdel);
         if constexpr (SLOW) {
             const int s = s0 + u;
@@ -179,17 +171,22 @@ __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)
     }
 }
 
-#ifndef SED_I32_WAVES_PER_EU
-#define SED_I32_WAVES_PER_EU 6  // 80 VGPRs at R=16: measured fastest (tools/sweep.sh)
+// Minimum waves per SIMD the register allocator must leave room for, per R
+// (R=16: 80 VGPRs / 6 waves measured fastest by tools/sweep.sh; R=32: 128 VGPRs / 4 waves).
+template <int R> struct I32Waves { static constexpr int value = R >= 32 ? 4 : (R == 16 ? 6 : 8); };
+#ifdef SED_I32_WAVES_PER_EU
+#define SED_I32_WAVES(R) SED_I32_WAVES_PER_EU
+#else
+#define SED_I32_WAVES(R) I32Waves<R>::value
 #endif
 template <int R, bool TB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SED_I32_WAVES_PER_EU))) void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SED_I32_WAVES(R)))) void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
                                                          const uint32_t *__restrict__ seqa,
                                                          const uint32_t *__restrict__ seqb,
                                                          uint32_t *__restrict__ tb, uint32_t *__restrict__ bnd,
                                                          sed_result *__restrict__ res, sed_i32_params prm) {
     constexpr int ROWS = 64 * R;
-    constexpr int NW = TbWords<R>::N;
+    constexpr int G = Grp<R>::G;
     const int lane = threadIdx.x & 63;
     const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (pair >= npairs) return;
@@ -205,8 +202,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SED_I32_WAV
         return;
     }
     const int nstripes = (n + ROWS - 1) / ROWS;
-    const int S4 = (m + 63 + 3) & ~3;
-    const int nchunks = (S4 + 63) >> 6;
+    const int SG = (m + 63 + G - 1) / G * G;  // steps per stripe, rounded to whole groups
+    const int nchunks = (SG + 63) >> 6;
     uint32_t *bndp = bnd + d.bnd_off;
     const uint32_t *pa = seqa + d.a_off;
     const uint32_t *pb = seqb + d.b_off;
@@ -227,9 +224,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SED_I32_WAV
         uint32_t top_prev;
         i32_reset<R>(V, top_prev, row0, prm.del);
         uint32_t bottom = 0, selv = 0, outc = 0;
-        uint32_t W[NW];
-#pragma unroll
-        for (int h = 0; h < NW; ++h) W[h] = 0;
+        uint32_t W[4] = {0, 0, 0, 0};
 
         auto load_top = [&](int c) -> uint32_t {
             const int j = 64 * c + lane + 1;
@@ -242,21 +237,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SED_I32_WAV
             return 0x0C000100u | ((4u + b) << 16);  // perm: byte2 <- cost byte b, bytes1:0 <- 6
         };
         uint32_t tch = load_top(0), sch = load_sel(0);
-        uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(S4 >> 2) * 64u * NW;
+        uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * 256u;
         const bool last = (k == nstripes - 1);
         const int cap_step = last ? m - 1 + cap_lane : -1;
         int s = 0;
         for (int c = 0; c < nchunks; ++c) {
             uint32_t tnx = 0, snx = 0;
             if (c + 1 < nchunks) { tnx = load_top(c + 1); snx = load_sel(c + 1); }
-            for (int g = 0; g < 16 && s < S4; ++g, s += 4) {
-                if (s < 63 || (cap_step >= s && cap_step < s + 4))
+            for (int g = 0; g < 64 / G && s < SG; ++g, s += G) {
+                if (s < 63 || (cap_step >= s && cap_step < s + G))
                     i32_group<R, TB, true>(V, cv, top_prev, bottom, selv, tch, sch, outc, W, s, lane, row0, prm.kins,
                                            prm.kdel, prm.del, cap_step, cap_lane, cap_row, cap);
                 else
                     i32_group<R, TB, false>(V, cv, top_prev, bottom, selv, tch, sch, outc, W, s, lane, row0,
                                             prm.kins, prm.kdel, prm.del, cap_step, cap_lane, cap_row, cap);
-                if constexpr (TB) store_tb<NW>(tbk + ((uint64_t)(s >> 2) * 64u + lane) * NW, W);
+                if constexpr (TB) store_tb(tbk + ((uint64_t)(s / G) * 64u + lane) * 4u, W);
             }
             // lane i holds lane 63's bottom cell of step s-64+i, i.e. column s-126+i at bnd index col+64
             if (!last) bndp[s - 62 + lane] = outc;
@@ -290,7 +285,7 @@ __device__ __forceinline__ void f64_step(double (&D)[R], uint32_t (&LK)[R], uint
                                          double &dtop_prev, uint32_t &ltop_prev, uint32_t &ttop_prev,
                                          double &dbot, uint32_t &lbot, uint32_t &tbot, uint32_t &bsel,
                                          double &dch, uint32_t &lch, uint32_t &tch, uint32_t &sch, double &doutc,
-                                         uint32_t &loutc, uint32_t &toutc, uint32_t (&W)[TbWords<R>::N], const int u,
+                                         uint32_t &loutc, uint32_t &toutc, uint32_t (&W)[4], const int u,
                                          const double cins, const double cdel, const uint32_t tins,
                                          const uint32_t tdel, const bool active, const sed_full_out &fo,
                                          const int i0, const int j) {
@@ -378,7 +373,7 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
                                                          const double *__restrict__ gtab, sed_f64_params prm,
                                                          sed_full_out fo) {
     constexpr int ROWS = 64 * R;
-    constexpr int NW = TbWords<R>::N;
+    constexpr int G = Grp<R>::G;
     __shared__ double2 tab[SED_MAX_K * SED_MAX_K];
     const int K = prm.K;
     for (int e = threadIdx.x; e < K * K; e += blockDim.x)
@@ -413,8 +408,8 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
         return;
     }
     const int nstripes = (n + ROWS - 1) / ROWS;
-    const int S4 = (m + 63 + 3) & ~3;
-    const int nchunks = (S4 + 63) >> 6;
+    const int SG = (m + 63 + G - 1) / G * G;
+    const int nchunks = (SG + 63) >> 6;
     // bottom-row buffer of a pair: [D as u64 | L as u32 | T as u32] planes
     const uint64_t bwords = (uint64_t)(nchunks + 2) * 64u;
     uint64_t *bndD = reinterpret_cast<uint64_t *>(bnd + d.bnd_off);
@@ -442,9 +437,7 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
         uint32_t ttop_prev = (row0 == 0) ? 1u : tdel;
         double dbot = 0.0, doutc = 0.0;
         uint32_t lbot = 0, tbot = 0, bsel = 0, loutc = 0, toutc = 0;
-        uint32_t W[NW];
-#pragma unroll
-        for (int h = 0; h < NW; ++h) W[h] = 0;
+        uint32_t W[4] = {0, 0, 0, 0};
 
         auto load_d = [&](int c) -> double {
             const int j = 64 * c + lane + 1;
@@ -466,7 +459,7 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
         };
         double dch = load_d(0);
         uint32_t lch = load_l(0), tch = TYPED ? load_t(0) : 0u, sch = load_sel(0);
-        uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(S4 >> 2) * 64u * NW;
+        uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * 256u;
         const bool last = (k == nstripes - 1);
         int s = 0;
         for (int c = 0; c < nchunks; ++c) {
@@ -478,10 +471,10 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
                 if (TYPED) tnx = load_t(c + 1);
                 snx = load_sel(c + 1);
             }
-            for (int g = 0; g < 16 && s < S4; ++g, s += 4) {
-                const bool full = (s >= 63) && (s + 3 < m);
+            for (int g = 0; g < 64 / G && s < SG; ++g, s += G) {
+                const bool full = (s >= 63) && (s + G - 1 < m);
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < G; ++u) {
                     const int j = s + u - lane + 1;
                     const bool active = (j >= 1) && (j <= m);
                     if (full)
@@ -495,7 +488,7 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
                                                            toutc, W, u, prm.ins, prm.del, tins, tdel, active, fo,
                                                            row0 + 1, j);
                 }
-                if constexpr (TB) store_tb<NW>(tbk + ((uint64_t)(s >> 2) * 64u + lane) * NW, W);
+                if constexpr (TB) store_tb(tbk + ((uint64_t)(s / G) * 64u + lane) * 4u, W);
             }
             if (!last) {
                 bndD[s - 62 + lane] = (uint64_t)__double_as_longlong(doutc);
@@ -540,13 +533,13 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
                                                            const uint32_t *__restrict__ tb,
                                                            const sed_result *__restrict__ res,
                                                            uint32_t *__restrict__ ops) {
-    constexpr int NW = R / 4;
+    constexpr int G = Grp<R>::G;
     const int pair = blockIdx.x * blockDim.x + threadIdx.x;
     if (pair >= npairs) return;
     const sed_pair_desc d = pd[pair];
     const int n = d.n, m = d.m;
-    const int S4 = (m + 63 + 3) & ~3;
-    const uint64_t stripe_words = (uint64_t)(S4 >> 2) * 64u * NW;
+    const int SG = (m + 63 + G - 1) / G * G;
+    const uint64_t stripe_words = (uint64_t)(SG / G) * 256u;
     uint32_t *out = ops + d.ops_off;
     int q = res[pair].len;  // ops in the script; written from position q-1 down to 0
     int i = n, j = m;
@@ -569,13 +562,14 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
         uint4 cw = make_uint4(0, 0, 0, 0);
         while (true) {
             const int s = j - 1 + t;
-            const int c = (s & 3) * R + r;
-            const uint64_t widx = ((uint64_t)(s >> 2) * 64u + t) * NW + (c >> 4);
-            if ((widx & ~3ull) != cached) {
-                cached = widx & ~3ull;
-                cw = *reinterpret_cast<const uint4 *>(base + cached);
+            const int c = (s % G) * R + r;  // code index inside the lane's 16-byte group block
+            const uint64_t blk = ((uint64_t)(s / G) * 64u + t) * 4u;
+            if (blk != cached) {
+                cached = blk;
+                cw = *reinterpret_cast<const uint4 *>(base + blk);
             }
-            const uint32_t wv = (widx & 2) ? ((widx & 1) ? cw.w : cw.z) : ((widx & 1) ? cw.y : cw.x);
+            const int wsel = c >> 4;
+            const uint32_t wv = (wsel & 2) ? ((wsel & 1) ? cw.w : cw.z) : ((wsel & 1) ? cw.y : cw.x);
             const uint32_t op = (wv >> (2 * (c & 15))) & 3u;
             emit(op);
             if (op != 1) --j;

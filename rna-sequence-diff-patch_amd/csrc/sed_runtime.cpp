@@ -243,10 +243,11 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         d.bnd_off = bndw;
         d.ops_off = opw;
         if (nn > 0 && mm > 0) {
+            const uint64_t G = 64 / R;  // steps per 16-byte traceback group (sed_kernels.hip: Grp)
             const uint64_t nstripes = (nn + ROWS - 1) / ROWS;
-            const uint64_t S4 = (mm + 63 + 3) & ~3ull;
-            const uint64_t nchunks = (S4 + 63) / 64;
-            if (want_tb) tbw += nstripes * (S4 / 4) * 64 * (R / 4);
+            const uint64_t SG = (mm + 63 + G - 1) / G * G;
+            const uint64_t nchunks = (SG + 63) / 64;
+            if (want_tb) tbw += nstripes * (SG / G) * 64 * 4;
             if (nstripes > 1) bndw += (nchunks + 2) * 64 * (packed ? 1 : 4);
         }
         opw += (uint64_t)(nn + mm + 15) / 16;

@@ -46,6 +46,30 @@ def pair_codes(pair_ids, length, stream, base=BASE_SEED):
     return sym.reshape(len(pair_ids), nwords * 32)[:, :length].astype(np.uint8)
 
 
+IUPAC = "AGCUYRWSKMDVHBN"
+
+
+def iupac_codes(pair_ids, length, stream, base=BASE_SEED):
+    """uint8 codes 0..14 (indices into IUPAC): 4-bit fields of the same stream, mod 15."""
+    pair_ids = np.asarray(pair_ids, dtype=np.uint64)
+    seed64 = ((np.uint64(base) + pair_ids) << np.uint64(1)) | np.uint64(stream)
+    seed64 = seed64 ^ np.uint64(0x1F2E3D4C5B6A7988)
+    nwords = (length + 15) // 16
+    w = stream_words(seed64, nwords)
+    shifts = (np.arange(16, dtype=np.uint64) * np.uint64(4)).reshape(1, 1, 16)
+    sym = ((w[:, :, None] >> shifts) & np.uint64(15)) % np.uint64(15)
+    return sym.reshape(len(pair_ids), nwords * 16)[:, :length].astype(np.uint8)
+
+
+def lengths(pair_ids, lo, hi, stream=2, base=BASE_SEED):
+    """Per-id lengths uniform in [lo, hi] (for ragged workloads such as all-vs-all)."""
+    pair_ids = np.asarray(pair_ids, dtype=np.uint64)
+    seed64 = ((np.uint64(base) + pair_ids) << np.uint64(1)) | np.uint64(stream & 1)
+    seed64 = seed64 ^ np.uint64(0xA5A5A5A5DEADBEEF + stream)
+    w = stream_words(seed64, 1)[:, 0]
+    return (lo + (w % np.uint64(hi - lo + 1))).astype(np.int32)
+
+
 def pair_strings(pair_id, n, m, base=BASE_SEED):
     """(str1, str2) for one synthetic pair, as ACGU text."""
     lut = np.frombuffer(ALPHABET.encode(), dtype=np.uint8)
