@@ -53,7 +53,9 @@ enum {
 
 /* sed_set_option keys */
 #define SED_OPT_MODE 1          /* 0 auto, 1 packed-integer kernel, 2 fp64 kernel, 3 fp64 + int-typing */
-#define SED_OPT_ROWS_PER_LANE 2 /* 0 auto, else 1,2,4,8,16,32 (integer) / 1,2,4,8 (fp64) */
+#define SED_OPT_ROWS_PER_LANE 2 /* 0 auto, else 4,8,16,32 (integer) / 4,8 (fp64) */
+#define SED_OPT_SPLIT 3         /* integer kernel, one wave per stripe: 0 auto (small batches of long
+                                   pairs), 1 always, 2 never */
 
 /* modes reported by sed_batch_mode */
 #define SED_MODE_I32 1

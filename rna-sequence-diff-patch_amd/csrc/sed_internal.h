@@ -13,7 +13,8 @@ struct sed_pair_desc {
     uint64_t bnd_off;  // stripe bottom-row buffer: uint32 word offset
     uint64_t ops_off;  // packed script: uint32 word offset
     int32_t n, m;
-    int32_t pad[4];
+    int32_t prog_off;  // SPLIT mode: index of stripe 0's progress word
+    int32_t pad[3];
 };
 
 // Per-pair result (16 bytes).
@@ -21,7 +22,8 @@ struct sed_result {
     double dist;     // dp[n][m].value
     int32_t len;     // ops in the canonical script (L at the sink)
     uint8_t is_int;  // 1 when the reference's value is a Python int
-    uint8_t pad[3];
+    uint8_t err;     // 1 when a SPLIT-mode wait timed out (results invalid)
+    uint8_t pad[2];
 };
 
 // Integer kernel constants: costrow[a] byte b = cost(a -> b); kins = (insert << 16) + 4,
@@ -55,6 +57,9 @@ struct sed_launch {
     sed_result *res;
     int R;
     hipStream_t stream;
+    const int2 *tasks;  // SPLIT mode: (pair, stripe) per workgroup, else nullptr
+    uint32_t *prog;     // SPLIT mode: per-stripe published-column counters (zeroed before each run)
+    int ntasks;         // 0 -> one wave per pair
 };
 
 hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm);

@@ -179,17 +179,50 @@ template <int R> struct I32Waves { static constexpr int value = R >= 32 ? 4 : (R
 #else
 #define SED_I32_WAVES(R) I32Waves<R>::value
 #endif
-template <int R, bool TB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SED_I32_WAVES(R)))) void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
-                                                         const uint32_t *__restrict__ seqa,
-                                                         const uint32_t *__restrict__ seqb,
-                                                         uint32_t *__restrict__ tb, uint32_t *__restrict__ bnd,
-                                                         sed_result *__restrict__ res, sed_i32_params prm) {
+// Inter-workgroup hand-off of stripe bottom rows (SPLIT mode; cdna_hip_programming.md §6 G16):
+// producer = every lane's plain stores -> s_waitcnt vmcnt(0) -> lane 0 agent release fence ->
+// s_waitcnt -> relaxed agent store of the published column count; consumer = relaxed agent
+// poll (bounded, s_sleep) -> agent acquire fence -> L1-bypassing sc1 loads.
+__device__ __forceinline__ void publish_progress(uint32_t *prog, uint32_t cols, int lane) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(prog, cols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+__device__ __forceinline__ bool wait_progress(const uint32_t *prog, uint32_t need) {
+    uint32_t spins = 0;
+    while (__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 24)) return false;  // producer never came: give up, flag the pair
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return true;
+}
+
+// SPLIT = false: one wave per pair walks all of its stripes (batches).
+// SPLIT = true : one wave (one 64-thread workgroup) per stripe, all stripes of
+//                a pair run concurrently, each one 3 chunks (192 steps) behind the
+//                stripe above it (single long pairs: config 2, the GUI).
+template <int R, bool TB, bool SPLIT>
+__global__ __launch_bounds__(SPLIT ? 64 : 256) __attribute__((amdgpu_waves_per_eu(SED_I32_WAVES(R)))) void
+sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *__restrict__ tasks,
+                  uint32_t *__restrict__ prog, const uint32_t *__restrict__ seqa, const uint32_t *__restrict__ seqb,
+                  uint32_t *__restrict__ tb, uint32_t *__restrict__ bnd, sed_result *__restrict__ res,
+                  sed_i32_params prm) {
     constexpr int ROWS = 64 * R;
     constexpr int G = Grp<R>::G;
     const int lane = threadIdx.x & 63;
-    const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (pair >= npairs) return;
+    int pair, kfirst = 0;
+    if constexpr (SPLIT) {
+        const int2 t = tasks[blockIdx.x];
+        pair = __builtin_amdgcn_readfirstlane(t.x);
+        kfirst = __builtin_amdgcn_readfirstlane(t.y);
+    } else {
+        pair = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+        if (pair >= npairs) return;
+    }
     const sed_pair_desc d = pd[pair];
     const int n = d.n, m = d.m;
     if (n == 0 || m == 0) {
@@ -202,17 +235,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SED_I32_WAV
         return;
     }
     const int nstripes = (n + ROWS - 1) / ROWS;
+    const int klast = SPLIT ? kfirst : nstripes - 1;
     const int SG = (m + 63 + G - 1) / G * G;  // steps per stripe, rounded to whole groups
     const int nchunks = (SG + 63) >> 6;
-    uint32_t *bndp = bnd + d.bnd_off;
+    const uint32_t bstride = (uint32_t)(nchunks + 2) * 64u;  // bottom-row buffer of one stripe (SPLIT)
     const uint32_t *pa = seqa + d.a_off;
     const uint32_t *pb = seqb + d.b_off;
     // the sink cell (n, m): last stripe, lane (n-1)%ROWS / R, row (n-1)%R, computed at step m-1+lane
     const int wsink = (n - 1) % ROWS;
     const int cap_lane = wsink / R, cap_row = wsink % R;
     uint32_t cap = 0;
+    bool ok = true;
 
-    for (int k = 0; k < nstripes; ++k) {
+    for (int k = kfirst; k <= klast; ++k) {
+        // in-place single buffer per pair when one wave does all stripes; one buffer per stripe otherwise
+        const uint32_t *bnd_in = bnd + d.bnd_off + (SPLIT ? (uint32_t)(k - 1) * bstride : 0u);
+        uint32_t *bnd_out = bnd + d.bnd_off + (SPLIT ? (uint32_t)k * bstride : 0u);
         const int row0 = k * ROWS + lane * R;  // 0-based str1 index of this lane's first row
         uint32_t cv[R], V[R];
 #pragma unroll
@@ -229,7 +267,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SED_I32_WAV
         auto load_top = [&](int c) -> uint32_t {
             const int j = 64 * c + lane + 1;
             if (k == 0) return i32_border((uint32_t)j, prm.ins);  // row 0: D = j*insert, L = j
-            return load_sc1(bndp + j + 64);
+            if constexpr (SPLIT) {  // after one timeout stop waiting: the kernel must still drain quickly
+                if (ok) ok = wait_progress(prog + d.prog_off + k - 1, (uint32_t)min(m, 64 * c + 64));
+            }
+            return load_sc1(bnd_in + j + 64);
         };
         auto load_sel = [&](int c) -> uint32_t {
             const int ci = 64 * c + lane;
@@ -254,18 +295,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SED_I32_WAV
                 if constexpr (TB) store_tb(tbk + ((uint64_t)(s / G) * 64u + lane) * 4u, W);
             }
             // lane i holds lane 63's bottom cell of step s-64+i, i.e. column s-126+i at bnd index col+64
-            if (!last) bndp[s - 62 + lane] = outc;
+            if (!last) {
+                bnd_out[s - 62 + lane] = outc;
+                if constexpr (SPLIT) publish_progress(prog + d.prog_off + k, (uint32_t)min(m, max(0, s - 63)), lane);
+            }
             tch = tnx;
             sch = snx;
         }
         if (!last) __builtin_amdgcn_s_waitcnt(0);  // own bottom-row stores done before the next stripe reads them
     }
-    if (lane == cap_lane) {
+    if (klast == nstripes - 1 && lane == cap_lane) {
         const uint32_t D = cap >> 16;
         res[pair].dist = (double)D;
         res[pair].len = (int32_t)((cap >> 2) & 0x3FFFu);
         res[pair].is_int = (D == 0);
     }
+    if (SPLIT && !ok && lane == 0) res[pair].err = 1;  // a timed-out wait poisons the pair (err zeroed per run)
 }
 
 // ---------------------------------------------------------------------------
@@ -618,9 +663,16 @@ __global__ void sed_selftest_kernel(uint32_t *out) {
 // ---------------------------------------------------------------------------
 template <int R, bool TB>
 static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
-    const int grid = (L.npairs + 3) / 4;
-    hipLaunchKernelGGL((sed_wf_i32_kernel<R, TB>), dim3(grid), dim3(256), 0, L.stream, L.pd, L.npairs,
-                       (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res, prm);
+    if (L.ntasks > 0) {  // SPLIT: one 64-thread workgroup per (pair, stripe)
+        hipLaunchKernelGGL((sed_wf_i32_kernel<R, TB, true>), dim3(L.ntasks), dim3(64), 0, L.stream, L.pd, L.npairs,
+                           L.tasks, L.prog, (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res,
+                           prm);
+    } else {
+        const int grid = (L.npairs + 3) / 4;
+        hipLaunchKernelGGL((sed_wf_i32_kernel<R, TB, false>), dim3(grid), dim3(256), 0, L.stream, L.pd, L.npairs,
+                           L.tasks, L.prog, (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res,
+                           prm);
+    }
     return hipGetLastError();
 }
 

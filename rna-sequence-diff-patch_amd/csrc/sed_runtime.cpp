@@ -57,7 +57,7 @@ struct sed_ctx {
     int ins_int = 0, del_int = 0;
     DevBuf gtab;  // fp64 kernel table: per entry {value bits, is-int flag}
     // options
-    int opt_mode = 0, opt_R = 0;
+    int opt_mode = 0, opt_R = 0, opt_split = 0;
     DevBuf selftest;
     sed_batch *scratch = nullptr;
 
@@ -84,7 +84,10 @@ struct sed_batch {
     std::vector<int32_t> n, m;
     uint64_t tb_words = 0, bnd_words = 0, ops_words = 0;
     double cells = 0, algo_bytes = 0;
-    DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops;
+    DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops, d_tasks, d_prog;
+    bool split = false;
+    int ntasks = 0;
+    uint64_t prog_words = 0;
     // SED_PIPELINE: run k uses traceback/result buffer k&1, so the traceback of
     // run k (second stream) overlaps the DP of run k+1.
     int nbuf = 1;
@@ -104,6 +107,7 @@ struct sed_batch {
     int cur() const { return (int)((runs - 1) & (nbuf - 1)); }
     ~sed_batch() {
         d_pd.release(); d_seqa.release(); d_seqb.release(); d_bnd.release(); d_ops.release();
+        d_tasks.release(); d_prog.release();
         for (int i = 0; i < 2; ++i) {
             d_tb[i].release();
             d_res[i].release();
@@ -215,6 +219,15 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     }
     if (mode == SED_MODE_I32 ? !(R == 4 || R == 8 || R == 16 || R == 32) : !(R == 4 || R == 8))
         return c->fail(SED_E_ARG, "unsupported rows-per-lane %d for mode %d", R, mode);
+    // SPLIT (integer kernel): one wave per stripe with inter-workgroup hand-offs, for
+    // batches too small to fill the GPU with one wave per pair (config 2, GUI calls).
+    bool split = false;
+    if (mode == SED_MODE_I32 && c->opt_split != 2) {
+        split = c->opt_split == 1 || (npairs <= 256 && max_n > 256);
+        if (split && !c->opt_R) R = 4;
+        if (split && R != 4 && R != 8 && R != 16 && R != 32) split = false;
+    }
+    b->split = split;
     b->mode = mode;
     b->R = R;
     const int ROWS = 64 * R;
@@ -222,7 +235,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
 
     // ---- layout ----
     b->pd.assign(npairs, sed_pair_desc{});
-    uint64_t aw = 0, bw = 0, tbw = 0, bndw = 0, opw = 0;
+    std::vector<int2> tasks;
+    uint64_t aw = 0, bw = 0, tbw = 0, bndw = 0, opw = 0, progw = 0;
     const bool packed = (mode == SED_MODE_I32);
     double cells = 0, in_bytes = 0, tb_bytes = 0;
     for (int p = 0; p < npairs; ++p) {
@@ -242,13 +256,20 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         d.tb_off = tbw;
         d.bnd_off = bndw;
         d.ops_off = opw;
+        d.prog_off = (int32_t)progw;
         if (nn > 0 && mm > 0) {
             const uint64_t G = 64 / R;  // steps per 16-byte traceback group (sed_kernels.hip: Grp)
             const uint64_t nstripes = (nn + ROWS - 1) / ROWS;
             const uint64_t SG = (mm + 63 + G - 1) / G * G;
             const uint64_t nchunks = (SG + 63) / 64;
             if (want_tb) tbw += nstripes * (SG / G) * 64 * 4;
-            if (nstripes > 1) bndw += (nchunks + 2) * 64 * (packed ? 1 : 4);
+            if (nstripes > 1) bndw += (nchunks + 2) * 64 * (packed ? 1 : 4) * (split ? nstripes : 1);
+            if (split) {
+                for (uint64_t k = 0; k < nstripes; ++k) tasks.push_back(make_int2(p, (int)k));
+                progw += nstripes;
+            }
+        } else if (split) {
+            tasks.push_back(make_int2(p, 0));
         }
         opw += (uint64_t)(nn + mm + 15) / 16;
         cells += (double)nn * mm;
@@ -257,6 +278,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     tb_bytes = cells * 0.25;
     b->tb_words = tbw;
     b->bnd_words = bndw;
+    b->ntasks = (int)tasks.size();
+    b->prog_words = progw;
     b->ops_words = opw;
     b->cells = cells;
     b->algo_bytes = in_bytes + (want_tb ? tb_bytes : 0) + 16.0 * npairs;
@@ -285,7 +308,9 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     const size_t sa = packed ? ha.size() * 4 : ha8.size(), sb = packed ? hb.size() * 4 : hb8.size();
     bool okalloc = b->d_pd.reserve(sizeof(sed_pair_desc) * std::max(1, npairs)) && b->d_seqa.reserve(sa) &&
                    b->d_seqb.reserve(sb) && b->d_ops.reserve(4 * std::max<uint64_t>(1, opw)) &&
-                   b->d_bnd.reserve(4 * std::max<uint64_t>(1, bndw));
+                   b->d_bnd.reserve(4 * std::max<uint64_t>(1, bndw)) &&
+                   b->d_tasks.reserve(sizeof(int2) * std::max<size_t>(1, tasks.size())) &&
+                   b->d_prog.reserve(4 * std::max<uint64_t>(1, progw));
     for (int i = 0; i < b->nbuf && okalloc; ++i)
         okalloc = b->d_res[i].reserve(sizeof(sed_result) * std::max(1, npairs)) &&
                   (!want_tb || b->d_tb[i].reserve(4 * std::max<uint64_t>(1, tbw)));
@@ -301,6 +326,9 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     if ((e = hipMemcpyAsync(b->d_seqb.p, packed ? (void *)hb.data() : (void *)hb8.data(), sb, hipMemcpyHostToDevice,
                             c->stream)) != hipSuccess)
         return c->hipfail(e, "upload str2");
+    if (!tasks.empty() && (e = hipMemcpyAsync(b->d_tasks.p, tasks.data(), sizeof(int2) * tasks.size(),
+                                              hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+        return c->hipfail(e, "upload tasks");
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hipfail(e, "upload sync");
 
     // ---- kernel parameters ----
@@ -365,11 +393,20 @@ int run_batch(sed_batch *b) {
     L.res = (sed_result *)b->d_res[k].p;
     L.R = b->R;
     L.stream = c->stream;
+    L.tasks = b->split ? (const int2 *)b->d_tasks.p : nullptr;
+    L.prog = (uint32_t *)b->d_prog.p;
+    L.ntasks = b->split ? b->ntasks : 0;
     // buffer k was last read by the traceback of run runs-2
     if (b->nbuf == 2 && b->runs >= 2 && (e = hipStreamWaitEvent(c->stream, b->ev_tb1[k], 0)) != hipSuccess)
         return c->hipfail(e, "stream wait");
     if ((e = hipEventRecord(b->ev_dp0[k], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
     (void)hipEventRecord(lg[0], c->stream);
+    // per-run state: result error flags, and the SPLIT hand-off counters
+    if ((e = hipMemsetAsync(L.res, 0, sizeof(sed_result) * b->npairs, c->stream)) != hipSuccess)
+        return c->hipfail(e, "memset results");
+    if (b->split && b->prog_words &&
+        (e = hipMemsetAsync(b->d_prog.p, 0, 4 * b->prog_words, c->stream)) != hipSuccess)
+        return c->hipfail(e, "memset progress");
     if (b->mode == SED_MODE_I32)
         e = sed_launch_i32(L, b->ip);
     else
@@ -413,6 +450,8 @@ int fetch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32_t *
                              hipMemcpyDeviceToHost)) !=
                   hipSuccess)
         return c->hipfail(e, "download results");
+    for (int p = 0; p < np; ++p)
+        if (b->h_res[p].err) return c->fail(SED_E_DEVICE, "pair %d: inter-workgroup hand-off timed out", p);
     for (int p = 0; p < np; ++p) {
         if (out_dist) out_dist[p] = b->h_res[p].dist;
         if (out_is_int) out_is_int[p] = b->h_res[p].is_int;
@@ -467,6 +506,10 @@ int sed_set_option(sed_ctx *c, int key, int value) {
     if (!c) return SED_E_ARG;
     if (key == SED_OPT_MODE && value >= 0 && value <= 3) {
         c->opt_mode = value;
+        return SED_OK;
+    }
+    if (key == SED_OPT_SPLIT && value >= 0 && value <= 2) {
+        c->opt_split = value;
         return SED_OK;
     }
     if (key == SED_OPT_ROWS_PER_LANE && (value == 0 || value == 1 || value == 2 || value == 4 || value == 8 ||
@@ -671,6 +714,9 @@ int sed_full_matrix(sed_ctx *c, const uint8_t *codes_a, int32_t n, const uint8_t
     L.bnd = (uint32_t *)tmp.d_bnd.p;
     L.res = (sed_result *)tmp.d_res[0].p;
     L.R = 4;
+    L.tasks = nullptr;
+    L.prog = nullptr;
+    L.ntasks = 0;
     L.stream = c->stream;
     sed_full_out fo{(double *)fD.p, (uint8_t *)fM.p, n, m};
     hipError_t e = sed_launch_f64_full(L, (const double *)c->gtab.p, tmp.fp, tmp.mode == SED_MODE_F64_TYPED, fo);

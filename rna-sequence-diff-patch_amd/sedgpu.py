@@ -15,6 +15,7 @@ SED_WANT_SCRIPT = 1
 SED_PIPELINE = 2
 SED_OPT_MODE = 1
 SED_OPT_ROWS_PER_LANE = 2
+SED_OPT_SPLIT = 3
 MODE_NAMES = {1: "i32", 2: "f64", 3: "f64-typed"}
 
 _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")

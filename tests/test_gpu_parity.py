@@ -20,11 +20,12 @@ OPCH = "idu"
 IUPAC = "AGCUYRWSKMDVHBN"
 
 
-def gpu_run(ctx, table, pairs, mode=0, R=0, script=True):
+def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0):
     """Run (s1, s2) pairs through the engine; returns [(dist, is_int, len, opstr)]."""
     plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
     ctx.set_mode(mode)
     ctx.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, R)
+    ctx.set_option(sedgpu.SED_OPT_SPLIT, split)
     ctx.set_costs(plan)
     packed = sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs], [plan.encode(b) for _, b in pairs])
     dist, is_int, ln, ops = ctx.run(packed, script)
@@ -36,6 +37,7 @@ def gpu_run(ctx, table, pairs, mode=0, R=0, script=True):
         out.append((float(dist[p]), bool(is_int[p]), int(ln[p]), s))
     ctx.set_mode(0)
     ctx.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
+    ctx.set_option(sedgpu.SED_OPT_SPLIT, 0)
     return out
 
 
@@ -69,10 +71,17 @@ def test_g3_config2_pair(gpu, tables):
     g3 = load_golden("g3_config2.json")
     s1, s2 = synth.pair_strings(g3["pair_id"], g3["n"], g3["m"], g3["base_seed"])
     assert hashlib.sha256(s1.encode()).hexdigest() == g3["s1_sha256"]
-    for R in (0, 4, 8, 32):
-        (d, ii, ln, s), = gpu_run(gpu, tables[True], [(s1, s2)], R=R)
+    for R, split in ((0, 0), (4, 2), (8, 2), (16, 2), (32, 2), (4, 1), (8, 1), (16, 1)):
+        (d, ii, ln, s), = gpu_run(gpu, tables[True], [(s1, s2)], R=R, split=split)
         assert d == float.fromhex(g3["dist"][0]) and not ii
-        assert ln == g3["len"] and s == g3["canon"], R
+        assert ln == g3["len"] and s == g3["canon"], (R, split)
+
+
+@pytest.mark.parametrize("R", [4, 8, 16])
+def test_split_mode_vs_oracle(gpu, tables, R):
+    """One wave per stripe with inter-workgroup hand-offs (forced on), ragged pairs."""
+    pairs = _random_pairs(100 + R, 24, "ACGU", 0, 1500, related=True)
+    _oracle_check(tables[True], pairs, gpu_run(gpu, tables[True], pairs, R=R, split=1))
 
 
 def _random_pairs(seed, count, alphabet, lo, hi, related=False):
