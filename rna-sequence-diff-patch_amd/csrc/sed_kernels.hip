@@ -94,15 +94,27 @@ __device__ __forceinline__ void store_tb(uint32_t *p, const uint32_t (&w)[4]) {
 // reset to its column-0 state right before its first step, and a lane past
 // column m computes columns that nothing reads.
 // ---------------------------------------------------------------------------
+#ifndef SED_I32_LDS_CHUNK
+#define SED_I32_LDS_CHUNK 1  // lane 0's per-step inputs from an LDS broadcast read instead of DPP rotations
+#endif
+
+// One column step of a lane's R rows.  tv = {top, sel} of this step's column
+// for lane 0 (the stripe's top row and str2 symbol): every lane reads the same
+// LDS word, only lane 0 keeps it (the DPP move's `old` operand).
 template <int R, bool TB>
 __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                          uint32_t &bottom, uint32_t &selv, uint32_t &tch, uint32_t &sch,
-                                         uint32_t &outc, uint32_t (&W)[4], const int u,
+                                         const uint2 tv, uint32_t &outc, uint32_t (&W)[4], const int u,
                                          const uint32_t kins, const uint32_t kdel) {
-    const uint32_t topv = dpp_shr1(tch, bottom);  // cell above the band, this column (lane 0: chunk)
-    selv = dpp_shr1(sch, selv);                   // perm selector of this column's str2 symbol
+#if SED_I32_LDS_CHUNK
+    const uint32_t topv = dpp_shr1(tv.x, bottom);  // cell above the band, this column
+    selv = dpp_shr1(tv.y, selv);                   // perm selector of this column's str2 symbol
+#else
+    const uint32_t topv = dpp_shr1(tch, bottom);
+    selv = dpp_shr1(sch, selv);
     tch = dpp_rol1(tch);
     sch = dpp_rol1(sch);
+#endif
     uint32_t up = topv, diag = top_prev;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -143,13 +155,18 @@ __device__ __forceinline__ void i32_reset(uint32_t (&V)[R], uint32_t &top_prev, 
 template <int R, bool TB, bool SLOW>
 __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                           uint32_t &bottom, uint32_t &selv, uint32_t &tch, uint32_t &sch,
-                                          uint32_t &outc, uint32_t (&W)[4], const int s0,
-                                          const int lane, const int row0, const uint32_t kins, const uint32_t kdel,
-                                          const uint32_t del, const int cap_step, const int cap_lane,
-                                          const int cap_row, uint32_t &cap) {
+                                          const uint2 *__restrict__ lch, uint32_t &outc, uint32_t (&W)[4],
+                                          const int s0, const int lane, const int row0, const uint32_t kins,
+                                          const uint32_t kdel, const uint32_t del, const int cap_step,
+                                          const int cap_lane, const int cap_row, uint32_t &cap) {
+    constexpr int G = Grp<R>::G;
+    uint2 tv[G];
+    const uint2 *lp = lch + (s0 & 63);  // G divides 64: a group never wraps the chunk
 #pragma unroll
-    for (int u = 0; u < Grp<R>::G; ++u) {
-        i32_step<R, TB>(V, cv, top_prev, bottom, selv, tch, sch, outc, W, u, kins, kdel);
+    for (int u = 0; u < G; ++u) tv[u] = SED_I32_LDS_CHUNK ? lp[u] : make_uint2(0, 0);
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+        i32_step<R, TB>(V, cv, top_prev, bottom, selv, tch, sch, tv[u], outc, W, u, kins, kdel);
         if constexpr (SLOW) {
             const int s = s0 + u;
             const bool hit = (s == cap_step) && (lane == cap_lane);
@@ -246,6 +263,9 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
     const int cap_lane = wsink / R, cap_row = wsink % R;
     uint32_t cap = 0;
     bool ok = true;
+    // lane 0's inputs of the current 64-step chunk ({top, sel} per step), one slot per wave
+    __shared__ uint2 lds_chunk[SPLIT ? 1 : 4][64];
+    uint2 *lch = lds_chunk[SPLIT ? 0 : (threadIdx.x >> 6)];
 
     for (int k = kfirst; k <= klast; ++k) {
         // in-place single buffer per pair when one wave does all stripes; one buffer per stripe otherwise
@@ -278,6 +298,7 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             return 0x0C000100u | ((4u + b) << 16);  // perm: byte2 <- cost byte b, bytes1:0 <- 6
         };
         uint32_t tch = load_top(0), sch = load_sel(0);
+        if (SED_I32_LDS_CHUNK) lch[lane] = make_uint2(tch, sch);
         uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * 256u;
         const bool last = (k == nstripes - 1);
         const int cap_step = last ? m - 1 + cap_lane : -1;
@@ -287,12 +308,15 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             if (c + 1 < nchunks) { tnx = load_top(c + 1); snx = load_sel(c + 1); }
             for (int g = 0; g < 64 / G && s < SG; ++g, s += G) {
                 if (s < 63 || (cap_step >= s && cap_step < s + G))
-                    i32_group<R, TB, true>(V, cv, top_prev, bottom, selv, tch, sch, outc, W, s, lane, row0, prm.kins,
-                                           prm.kdel, prm.del, cap_step, cap_lane, cap_row, cap);
+                    i32_group<R, TB, true>(V, cv, top_prev, bottom, selv, tch, sch, lch, outc, W, s, lane, row0,
+                                           prm.kins, prm.kdel, prm.del, cap_step, cap_lane, cap_row, cap);
                 else
-                    i32_group<R, TB, false>(V, cv, top_prev, bottom, selv, tch, sch, outc, W, s, lane, row0,
+                    i32_group<R, TB, false>(V, cv, top_prev, bottom, selv, tch, sch, lch, outc, W, s, lane, row0,
                                             prm.kins, prm.kdel, prm.del, cap_step, cap_lane, cap_row, cap);
-                if constexpr (TB) store_tb(tbk + ((uint64_t)(s / G) * 64u + lane) * 4u, W);
+                if constexpr (TB) {
+                    uint32_t *gp = tbk + (uint64_t)(s / G) * 256u;  // wave-uniform base, per-lane 16-byte offset
+                    store_tb(gp + lane * 4, W);
+                }
             }
             // lane i holds lane 63's bottom cell of step s-64+i, i.e. column s-126+i at bnd index col+64
             if (!last) {
@@ -301,6 +325,7 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             }
             tch = tnx;
             sch = snx;
+            if (SED_I32_LDS_CHUNK) lch[lane] = make_uint2(tch, sch);  // after the chunk's last LDS read (in order)
         }
         if (!last) __builtin_amdgcn_s_waitcnt(0);  // own bottom-row stores done before the next stripe reads them
     }
