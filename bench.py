@@ -38,7 +38,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
 # wave64 v_add/v_and issue every ~2.5 cycles per SIMD, VOP3-only ops (v_min3, v_perm,
 # v_alignbit) every ~4.4.  A script-mode cell is 4 of the former + 3 of the latter.
 SIMDS, CLOCK = 1024, 2.4e9
-CELL_CYCLES = {("i32", True): 4 * 2.5 + 3 * 4.4, ("i32", False): 4 * 2.5 + 2 * 4.4}  # per 64 cells
+# VALU ceiling of the integer kernels: every op of the dependent DP cell issues at ~4 cycles per wave64
+# instruction on gfx950 whatever the op mix (tools/ubench/valu_mix.hip, valu_row.hip: 4.0-4.2 cycles/op,
+# the nominal 2-cycle ops do not pair when interleaved with the 4-cycle v_perm/v_min3/v_alignbit).
+# Ops per cell: perm + 3 add + min3 (+ and for the op-count field) (+ alignbit for the traceback).
+VALU_CYCLES_PER_OP = 4.0
+CELL_OPS = {"script": 7, "len": 6, "nolen": 5}
 
 WORKLOADS = {
     # name: (pairs per GPU, n, m, cost table, description)
@@ -105,27 +110,25 @@ def script_costs(plan, A, B, ln, ops, ops_off):
     return ok, cost
 
 
-def cpu_baseline(plan, A, B, seconds, threads):
-    """Oracle (C restatement, test infrastructure) on a bounded sample."""
+def cpu_baseline(plan, packed, seconds, threads, want_ops):
+    """Oracle (C restatement, test infrastructure) on a bounded prefix of the same pairs."""
     import oracle
     cs = oracle.Costs.from_plan(plan)
-    n, m = A.shape[1], B.shape[1]
+    P = packed.npairs
+    la, lb = packed.len_a[:P], packed.len_b[:P]
+    cum = np.cumsum(la.astype(np.float64) * lb)
+    probe = int(min(P, np.searchsorted(cum, 2e6) + 1))  # ~2M cells, single thread
     t0 = time.perf_counter()
-    oracle.pair(cs, A[0], B[0], want_ops=True)
-    t1 = time.perf_counter() - t0
-    per_thread = max(1, int(seconds / max(t1, 1e-6)))
-    count = min(len(A), per_thread * threads)
-    la = np.full(count, n, np.int32)
-    lb = np.full(count, m, np.int32)
-    offa = np.arange(count, dtype=np.int64) * n
-    offb = np.arange(count, dtype=np.int64) * m
+    oracle.batch(cs, packed.codes_a, packed.off_a, la, packed.codes_b, packed.off_b, lb, probe, want_ops=want_ops)
+    per_cell = (time.perf_counter() - t0) / max(1.0, float(cum[probe - 1]))
+    budget = seconds * threads / max(per_cell, 1e-12)  # cells the sample may hold
+    count = int(min(P, max(threads, np.searchsorted(cum, budget))))
     t0 = time.perf_counter()
-    dist, is_int, ln, ops, ops_off = oracle.batch(cs, np.ascontiguousarray(A[:count]), offa, la,
-                                                  np.ascontiguousarray(B[:count]), offb, lb, count,
-                                                  want_ops=True, nthreads=threads)
+    dist, is_int, ln, ops, ops_off = oracle.batch(cs, packed.codes_a, packed.off_a, la, packed.codes_b,
+                                                  packed.off_b, lb, count, want_ops=want_ops, nthreads=threads)
     dt = time.perf_counter() - t0
-    return {"value": count * n * m / dt, "seconds": dt, "count": count, "dist": dist, "len": ln, "ops": ops,
-            "ops_off": ops_off}
+    return {"value": float(cum[count - 1]) / dt, "seconds": dt, "count": count, "dist": dist, "len": ln,
+            "ops": ops, "ops_off": ops_off}
 
 
 def main():
@@ -198,7 +201,7 @@ def main():
     ctx.set_costs(plan)
     t0 = time.perf_counter()
     pipeline = want_script and not args.no_pipeline
-    batch = sedgpu.Batch(ctx, packed, want_script, pipeline=pipeline)
+    batch = sedgpu.Batch(ctx, packed, want_script, pipeline=pipeline, no_len=not want_script)
     log("rank %d: batch resident in %.1fs (mode %s, R=%d)" % (rank, time.perf_counter() - t0, batch.mode,
                                                              batch.rows_per_lane))
     cells, algo_bytes = batch.work()
@@ -254,25 +257,27 @@ def main():
             good += int((ok & same).sum())
         check["script_valid_rate"] = good / P
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and A is not None:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             threads = min(16, len(os.sched_getaffinity(0)))
         except AttributeError:
             threads = min(16, os.cpu_count() or 1)
-        cpu = cpu_baseline(plan, A, B, args.cpu_seconds, threads)
+        cpu = cpu_baseline(plan, packed, args.cpu_seconds, threads, want_script)
         c = cpu["count"]
-        exact = (cpu["dist"] == d_gpu[:c]) & (cpu["len"] == ln_gpu[:c])
+        exact = (cpu["dist"] == d_gpu[:c]) & ((cpu["len"] == ln_gpu[:c]) | (ln_gpu[:c] == -1))
         if want_script:
             for p in range(c):
                 if exact[p]:
                     g = sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln_gpu[p]))
                     o = cpu["ops"][cpu["ops_off"][p]: cpu["ops_off"][p] + cpu["len"][p]]
                     exact[p] = np.array_equal(g, o)
-        check["script_exact_rate"] = float(exact.mean())
-        check["script_exact_sample"] = int(c)
+        check["script_exact_rate" if want_script else "dist_exact_rate"] = float(exact.mean())
+        check["exact_sample"] = int(c)
+        shape = "%dx%d" % (n, m) if n else "ragged"
         cpu_obj = {"value": cpu["value"], "unit": "cells/s", "cores": threads, "kind": "port",
-                   "sample": "%d of the %d pairs (%dx%d, %s), C oracle sed_oracle.c, %.1f s"
-                             % (c, P, n, m, costs_file, cpu["seconds"])}
+                   "sample": "first %d of the %d pairs (%s, %s, %s), C oracle sed_oracle.c, %.1f s"
+                             % (c, P, shape, costs_file, "distance + script" if want_script else "distance",
+                                cpu["seconds"])}
 
     if rank != 0:
         if dist is not None:
@@ -286,24 +291,31 @@ def main():
             pm = json.load(f)
         if pm.get("workload") == desc and batch.mode == "i32" and want_script and P == WORKLOADS[args.workload][0]:
             traffic = pm.get("hbm_bytes_per_launch")
-    cyc = CELL_CYCLES.get((batch.mode, want_script))
+    ops_cell = CELL_OPS["script" if want_script else "nolen"] if batch.mode == "i32" else None
+    valu_peak = SIMDS * CLOCK * 64 / (VALU_CYCLES_PER_OP * ops_cell) if ops_cell else None
     rate = cells / (dp_avg * 1e-3)
+    nl = batch.lane_pairs
+    if batch.mode != "i32":
+        kname = "sed_wf_f64_kernel"
+    else:
+        kname = "sed_lane_i32_kernel" if nl == P else ("sed_wf_i32_kernel" if nl == 0 else
+                                                       "sed_wf_i32_kernel+sed_lane_i32_kernel")
     line = {
         "metric": METRIC, "value": value, "unit": "cells/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u32" if batch.mode == "i32" else "f64", "data": "synthetic",
         "config": {"workload": desc, "pairs_per_gpu": P, "n": n, "m": m, "costs": costs_file,
                    "script": want_script, "pipeline": pipeline, "mode": batch.mode,
-                   "rows_per_lane": batch.rows_per_lane,
+                   "rows_per_lane": batch.rows_per_lane, "lane_pairs": nl,
                    "parallelism": "dp%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "sed_wf_i32_kernel" if batch.mode == "i32" else "sed_wf_f64_kernel",
+                     "kernel": kname,
                      "kernel_ms": dp_avg, "algo_bytes_per_launch": algo_bytes},
-        "valu": None if cyc is None else {
-            "model": "per 64 cells: 4 full-rate + %d half-rate VALU (tools/ubench/valu_rate.hip)" % (3 if want_script else 2),
-            "achieved": rate, "peak": SIMDS * CLOCK * 64 / cyc, "unit": "cells/s",
-            "frac": rate / (SIMDS * CLOCK * 64 / cyc)},
+        "valu": None if valu_peak is None else {
+            "model": "%d VALU ops/cell x %.1f cycles/op per wave64 (tools/ubench/valu_row.hip), 1024 SIMDs, %.1f GHz"
+                     % (ops_cell, VALU_CYCLES_PER_OP, CLOCK / 1e9),
+            "achieved": rate, "peak": valu_peak, "unit": "cells/s", "frac": rate / valu_peak},
         "traceback_ms": float(np.mean(tb_ms)) if want_script else None,
         "gather_ms": gather_ms,
         "cpu_baseline": cpu_obj if cpu is not None else None,

@@ -50,12 +50,17 @@ enum {
 /* sed_batch only: two traceback/result buffers and a second stream, so the traceback of
  * run k overlaps the DP kernel of run k+1 (device memory for the traceback doubles). */
 #define SED_PIPELINE 2u
+/* distance only (no SED_WANT_SCRIPT): out_len is not computed (-1), which lets the integer
+ * kernels drop the op-count field of their keys (5 instead of 6 VALU ops per cell). */
+#define SED_NO_LEN 4u
 
 /* sed_set_option keys */
 #define SED_OPT_MODE 1          /* 0 auto, 1 packed-integer kernel, 2 fp64 kernel, 3 fp64 + int-typing */
 #define SED_OPT_ROWS_PER_LANE 2 /* 0 auto, else 4,8,16,32 (integer) / 4,8 (fp64) */
 #define SED_OPT_SPLIT 3         /* integer kernel, one wave per stripe: 0 auto (small batches of long
                                    pairs), 1 always, 2 never */
+#define SED_OPT_LANE 4          /* integer kernel, one lane per pair for short str2 (m <= 32, n <= 512):
+                                   0 auto (on), 2 never */
 
 /* modes reported by sed_batch_mode */
 #define SED_MODE_I32 1
@@ -99,6 +104,7 @@ sed_batch *sed_batch_create(sed_ctx *ctx,
 void sed_batch_destroy(sed_batch *b);
 int sed_batch_mode(const sed_batch *b);               /* SED_MODE_* chosen for this batch */
 int sed_batch_rows_per_lane(const sed_batch *b);
+int sed_batch_lane_pairs(const sed_batch *b);         /* pairs on the lane-per-pair kernel (short str2) */
 int sed_batch_run(sed_batch *b);                      /* enqueue on the context stream, returns at once */
 int sed_batch_sync(sed_batch *b);                     /* wait for the last run */
 /* device time of the last run, from HIP events on the launching stream (ms) */

@@ -215,7 +215,7 @@ class DPMatrix:
         ctx = sedgpu.context()
         ctx.set_costs(self._plan)
         packed = sedgpu.PackedPairs([self._codes[0]], [self._codes[1]])
-        dist, is_int, ln, ops = ctx.run(packed, want_script)
+        dist, is_int, ln, ops = ctx.run(packed, want_script, no_len=not want_script)
         d = float(dist[0])
         self._final = int(d) if is_int[0] else d
         if want_script:
@@ -532,7 +532,7 @@ def distance_batch(strs1, strs2, userCosts=False):
     ctx = sedgpu.context()
     ctx.set_costs(plan)
     packed = sedgpu.PackedPairs([plan.encode(a) for a in strs1], [plan.encode(b) for b in strs2])
-    dist, is_int, _, _ = ctx.run(packed, False)
+    dist, is_int, _, _ = ctx.run(packed, False, no_len=True)
     return [int(d) if t else float(d) for d, t in zip(dist.tolist(), is_int.tolist())]
 
 

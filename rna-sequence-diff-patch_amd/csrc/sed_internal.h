@@ -14,7 +14,8 @@ struct sed_pair_desc {
     uint64_t ops_off;  // packed script: uint32 word offset
     int32_t n, m;
     int32_t prog_off;  // SPLIT mode: index of stripe 0's progress word
-    int32_t pad[3];
+    int32_t lane;      // 1: computed by the lane-per-pair kernel (short str2), the wave kernels skip it
+    int32_t pad[2];
 };
 
 // Per-pair result (16 bytes).
@@ -53,6 +54,7 @@ struct sed_launch {
     int npairs;
     const void *seqa, *seqb;
     uint32_t *tb;   // nullptr -> distance only
+    uint32_t *ops;  // packed scripts (lane kernel writes them itself)
     uint32_t *bnd;
     sed_result *res;
     int R;
@@ -62,9 +64,15 @@ struct sed_launch {
     int ntasks;         // 0 -> one wave per pair
 };
 
-hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm);
+// len = false (distance only, SED_NO_LEN): keys without the op-count field, out len = -1.
+hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm, bool len);
 hipError_t sed_launch_f64(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed);
 hipError_t sed_launch_f64_full(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed,
                                const sed_full_out &fo);
+// Lane-per-pair integer kernel (sed_lane.hip): pairs idx[0..nidx) with 1 <= m <= SED_LANE_MAXM.
+// len = false: distance only, no op-count field (5 VALU per cell).
+#define SED_LANE_MAXM 32
+#define SED_LANE_MAXN 512
+hipError_t sed_launch_lane_i32(const sed_launch &L, const int32_t *idx, int nidx, const sed_i32_params &prm, bool len);
 hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops);
 hipError_t sed_launch_selftest(uint32_t *d_out, hipStream_t stream);

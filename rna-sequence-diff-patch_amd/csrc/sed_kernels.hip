@@ -101,7 +101,7 @@ __device__ __forceinline__ void store_tb(uint32_t *p, const uint32_t (&w)[4]) {
 // One column step of a lane's R rows.  tv = {top, sel} of this step's column
 // for lane 0 (the stripe's top row and str2 symbol): every lane reads the same
 // LDS word, only lane 0 keeps it (the DPP move's `old` operand).
-template <int R, bool TB>
+template <int R, bool TB, bool LEN>
 __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                          uint32_t &bottom, uint32_t &selv, uint32_t &tch, uint32_t &sch,
                                          const uint2 tv, uint32_t &outc, uint32_t (&W)[4], const int u,
@@ -121,13 +121,13 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
         const uint32_t left = V[r];
         const uint32_t mm = umin3(left + kins,                                     // insert (op 0)
                                   up + kdel,                                       // delete (op 1)
-                                  diag + __builtin_amdgcn_perm(cv[r], 6u, selv));  // update (op 2)
+                                  diag + __builtin_amdgcn_perm(cv[r], LEN ? 6u : 0u, selv));  // update (op 2)
         if constexpr (TB) {
             const int c = u * R + r;  // compile-time after unrolling
             W[c >> 4] = __builtin_amdgcn_alignbit(mm, W[c >> 4], 2);
         }
         diag = left;
-        up = mm & ~3u;
+        up = LEN ? (mm & ~3u) : mm;  // !LEN: distance only, keys carry no L/op field
         V[r] = up;
     }
     top_prev = topv;
@@ -152,7 +152,7 @@ __device__ __forceinline__ void i32_reset(uint32_t (&V)[R], uint32_t &top_prev, 
 // SLOW groups: ramp-up (the lane that starts next step is reset to column 0)
 // and the group that produces the sink cell (captured).  Branch-free selects,
 // so no value lives across a basic-block boundary.
-template <int R, bool TB, bool SLOW>
+template <int R, bool TB, bool LEN, bool SLOW>
 __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                           uint32_t &bottom, uint32_t &selv, uint32_t &tch, uint32_t &sch,
                                           const uint2 *__restrict__ lch, uint32_t &outc, uint32_t (&W)[4],
@@ -166,7 +166,7 @@ __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)
     for (int u = 0; u < G; ++u) tv[u] = SED_I32_LDS_CHUNK ? lp[u] : make_uint2(0, 0);
 #pragma unroll
     for (int u = 0; u < G; ++u) {
-        i32_step<R, TB>(V, cv, top_prev, bottom, selv, tch, sch, tv[u], outc, W, u, kins, kdel);
+        i32_step<R, TB, LEN>(V, cv, top_prev, bottom, selv, tch, sch, tv[u], outc, W, u, kins, kdel);
         if constexpr (SLOW) {
             const int s = s0 + u;
             const bool hit = (s == cap_step) && (lane == cap_lane);
@@ -222,7 +222,7 @@ __device__ __forceinline__ bool wait_progress(const uint32_t *prog, uint32_t nee
 // SPLIT = true : one wave (one 64-thread workgroup) per stripe, all stripes of
 //                a pair run concurrently, each one 3 chunks (192 steps) behind the
 //                stripe above it (single long pairs: config 2, the GUI).
-template <int R, bool TB, bool SPLIT>
+template <int R, bool TB, bool SPLIT, bool LEN = true>
 __global__ __launch_bounds__(SPLIT ? 64 : 256) __attribute__((amdgpu_waves_per_eu(SED_I32_WAVES(R)))) void
 sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *__restrict__ tasks,
                   uint32_t *__restrict__ prog, const uint32_t *__restrict__ seqa, const uint32_t *__restrict__ seqb,
@@ -241,6 +241,7 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
         if (pair >= npairs) return;
     }
     const sed_pair_desc d = pd[pair];
+    if (d.lane) return;  // short str2: sed_lane.hip
     const int n = d.n, m = d.m;
     if (n == 0 || m == 0) {
         if (lane == 0) {
@@ -251,6 +252,7 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
         }
         return;
     }
+    const uint32_t kins = LEN ? prm.kins : (prm.ins << 16), kdel = LEN ? prm.kdel : (prm.del << 16);
     const int nstripes = (n + ROWS - 1) / ROWS;
     const int klast = SPLIT ? kfirst : nstripes - 1;
     const int SG = (m + 63 + G - 1) / G * G;  // steps per stripe, rounded to whole groups
@@ -308,11 +310,11 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             if (c + 1 < nchunks) { tnx = load_top(c + 1); snx = load_sel(c + 1); }
             for (int g = 0; g < 64 / G && s < SG; ++g, s += G) {
                 if (s < 63 || (cap_step >= s && cap_step < s + G))
-                    i32_group<R, TB, true>(V, cv, top_prev, bottom, selv, tch, sch, lch, outc, W, s, lane, row0,
-                                           prm.kins, prm.kdel, prm.del, cap_step, cap_lane, cap_row, cap);
+                    i32_group<R, TB, LEN, true>(V, cv, top_prev, bottom, selv, tch, sch, lch, outc, W, s, lane, row0,
+                                           kins, kdel, prm.del, cap_step, cap_lane, cap_row, cap);
                 else
-                    i32_group<R, TB, false>(V, cv, top_prev, bottom, selv, tch, sch, lch, outc, W, s, lane, row0,
-                                            prm.kins, prm.kdel, prm.del, cap_step, cap_lane, cap_row, cap);
+                    i32_group<R, TB, LEN, false>(V, cv, top_prev, bottom, selv, tch, sch, lch, outc, W, s, lane, row0,
+                                            kins, kdel, prm.del, cap_step, cap_lane, cap_row, cap);
                 if constexpr (TB) {
                     uint32_t *gp = tbk + (uint64_t)(s / G) * 256u;  // wave-uniform base, per-lane 16-byte offset
                     store_tb(gp + lane * 4, W);
@@ -332,7 +334,7 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
     if (klast == nstripes - 1 && lane == cap_lane) {
         const uint32_t D = cap >> 16;
         res[pair].dist = (double)D;
-        res[pair].len = (int32_t)((cap >> 2) & 0x3FFFu);
+        res[pair].len = LEN ? (int32_t)((cap >> 2) & 0x3FFFu) : -1;
         res[pair].is_int = (D == 0);
     }
     if (SPLIT && !ok && lane == 0) res[pair].err = 1;  // a timed-out wait poisons the pair (err zeroed per run)
@@ -607,6 +609,7 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
     const int pair = blockIdx.x * blockDim.x + threadIdx.x;
     if (pair >= npairs) return;
     const sed_pair_desc d = pd[pair];
+    if (d.lane) return;  // scripted by sed_lane.hip
     const int n = d.n, m = d.m;
     const int SG = (m + 63 + G - 1) / G * G;
     const uint64_t stripe_words = (uint64_t)(SG / G) * 256u;
@@ -686,27 +689,28 @@ __global__ void sed_selftest_kernel(uint32_t *out) {
 // ---------------------------------------------------------------------------
 // Launchers (host side, called from sed_runtime.cpp)
 // ---------------------------------------------------------------------------
-template <int R, bool TB>
+template <int R, bool TB, bool LEN = true>
 static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
     if (L.ntasks > 0) {  // SPLIT: one 64-thread workgroup per (pair, stripe)
-        hipLaunchKernelGGL((sed_wf_i32_kernel<R, TB, true>), dim3(L.ntasks), dim3(64), 0, L.stream, L.pd, L.npairs,
+        hipLaunchKernelGGL((sed_wf_i32_kernel<R, TB, true, LEN>), dim3(L.ntasks), dim3(64), 0, L.stream, L.pd, L.npairs,
                            L.tasks, L.prog, (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res,
                            prm);
     } else {
         const int grid = (L.npairs + 3) / 4;
-        hipLaunchKernelGGL((sed_wf_i32_kernel<R, TB, false>), dim3(grid), dim3(256), 0, L.stream, L.pd, L.npairs,
+        hipLaunchKernelGGL((sed_wf_i32_kernel<R, TB, false, LEN>), dim3(grid), dim3(256), 0, L.stream, L.pd, L.npairs,
                            L.tasks, L.prog, (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res,
                            prm);
     }
     return hipGetLastError();
 }
 
-hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm) {
+hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm, bool len) {
     const bool tb = L.tb != nullptr;
     switch (L.R) {
-#define CASE(RR)                                                          \
-    case RR:                                                              \
-        return tb ? launch_i32_R<RR, true>(L, prm) : launch_i32_R<RR, false>(L, prm);
+#define CASE(RR)                                                                                     \
+    case RR:                                                                                         \
+        return tb ? launch_i32_R<RR, true>(L, prm)                                                   \
+                  : (len ? launch_i32_R<RR, false>(L, prm) : launch_i32_R<RR, false, false>(L, prm));
         CASE(4) CASE(8) CASE(16) CASE(32)
 #undef CASE
     default: return hipErrorInvalidValue;

@@ -1,0 +1,151 @@
+// sed_lane.hip — lane-per-pair integer kernel for short str2 (m <= SED_LANE_MAXM).
+//
+// Config 5 (all-vs-all over ~24-32 nt piRNAs, IRMethods.py:435-440 / 443-477) and the GUI's
+// short pairs: a 64-lane wave per pair (sed_kernels.hip) would leave most lanes idle and spend
+// ~m+63 systolic steps on a 32-column matrix.  Here one lane owns one pair and walks its matrix
+// row by row (StringEditDistance.py:185-222 order) with the whole DP row in VGPRs: no DPP, no
+// LDS, no inter-lane traffic; 64 pairs per wave, >= 4 waves per SIMD for 250k pairs.
+//
+// Cell keys are the packed-integer keys of sed_kernels.hip (D << 16 | L << 2 | op), so results
+// (distance, L = script length, canonical op) are identical to the wave kernel's:
+//   LEN:  candidates left+kins, up+kdel, diag+perm(costrow, 6, sel) -> v_min3 -> & ~3   (6 VALU)
+//   !LEN: distance only, no L/op field: +ins<<16, +del<<16, +cost<<16 -> v_min3         (5 VALU)
+// TB (implies LEN): the op of every cell (2 bits, 32 per row = one uint2) is stored per pair,
+// row-major, and the same lane walks it back from (n, m) to write the canonical script.
+#include "sed_internal.h"
+
+namespace {
+
+__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) {
+    return min(min(a, b), c);  // folds to v_min3_u32
+}
+__device__ __forceinline__ uint32_t lane_border(uint32_t i, uint32_t cost) { return ((i * cost) << 16) | (i << 2); }
+
+template <bool LEN, bool TB>
+__global__ __launch_bounds__(256) void sed_lane_i32_kernel(const sed_pair_desc *__restrict__ pd,
+                                                           const int32_t *__restrict__ idx, int nidx,
+                                                           const uint32_t *__restrict__ seqa,
+                                                           const uint32_t *__restrict__ seqb,
+                                                           uint32_t *__restrict__ tb, uint32_t *__restrict__ ops,
+                                                           sed_result *__restrict__ res, sed_i32_params prm) {
+    static_assert(LEN || !TB, "the traceback needs the op-count field");
+    constexpr int MM = SED_LANE_MAXM;
+    static_assert(MM == 32, "str2 codes are read as two 16-symbol words");
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nidx) return;
+    const int pair = idx[t];
+    const sed_pair_desc d = pd[pair];
+    const int n = d.n, m = d.m;  // host guarantees 1 <= n <= SED_LANE_MAXN, 1 <= m <= MM
+    const uint32_t kins = LEN ? prm.kins : (prm.ins << 16);
+    const uint32_t kdel = LEN ? prm.kdel : (prm.del << 16);
+    const uint32_t s1 = LEN ? 6u : 0u;  // perm bytes 1:0 of the update candidate (L+1, op 2)
+    // Transposed lookup: the lane keeps, per column j, the 4 costs cost(a -> b_j) as bytes of colw[j];
+    // a row's symbol a_i becomes the perm selector, so a row costs 2 ops of setup instead of a
+    // per-lane select of its cost row.  (Columns beyond m read the next pair's codes or padding:
+    // don't-care, nothing flows from column j > m into columns <= m.)
+    uint32_t colrow[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) w |= ((prm.costrow[a] >> (8 * b)) & 0xFFu) << (8 * a);
+        colrow[b] = w;
+    }
+    const uint32_t *pb = seqb + d.b_off;
+    const uint32_t wb0 = pb[0], wb1 = pb[1];
+    uint32_t colw[MM], V[MM + 1];
+#pragma unroll
+    for (int j = 0; j < MM; ++j) {
+        const uint32_t b = ((j < 16 ? wb0 : wb1) >> (2 * (j & 15))) & 3u;
+        const uint32_t lo = (b & 1u) ? colrow[1] : colrow[0], hi = (b & 1u) ? colrow[3] : colrow[2];
+        colw[j] = (b & 2u) ? hi : lo;
+    }
+#pragma unroll
+    for (int j = 0; j <= MM; ++j) V[j] = lane_border((uint32_t)j, prm.ins);  // row 0: j inserts
+    const uint32_t *pa = seqa + d.a_off;
+    const uint32_t cstep = (prm.del << 16) | 4u;  // column 0: i deletes
+    uint32_t wa = 0, colv = 0;
+    uint2 *tbp = reinterpret_cast<uint2 *>(tb) + (TB ? d.tb_off / 2 : 0);
+    for (int i = 0; i < n; ++i) {
+        if ((i & 15) == 0) wa = pa[i >> 4];
+        const uint32_t a = (wa >> (2 * (i & 15))) & 3u;
+        const uint32_t sel = 0x0C000100u | ((4u + a) << 16);  // perm: byte2 <- cost byte a, bytes1:0 <- s1
+        // update candidate of column j+1 is formed from the old V[j] before V[j] is overwritten,
+        // so every V[j] is updated in place (no register rotation across the row loop)
+        uint32_t dg = V[0] + __builtin_amdgcn_perm(colw[0], s1, sel);
+        colv += cstep;
+        V[0] = colv;
+        uint32_t left = colv;
+        uint32_t W0 = 0, W1 = 0;
+#pragma unroll
+        for (int j = 1; j <= MM; ++j) {
+            const uint32_t up = V[j];
+            const uint32_t cdel = up + kdel;                                              // delete (op 1)
+            const uint32_t dnext = j < MM ? up + __builtin_amdgcn_perm(colw[j], s1, sel) : 0u;
+            const uint32_t mm = umin3(left + kins, cdel, dg);  // insert (op 0), update (op 2)
+            dg = dnext;
+            if constexpr (TB) {
+                if (j <= 16) W0 = __builtin_amdgcn_alignbit(mm, W0, 2);
+                else W1 = __builtin_amdgcn_alignbit(mm, W1, 2);
+            }
+            const uint32_t v = LEN ? (mm & ~3u) : mm;
+            V[j] = v;
+            left = v;
+        }
+        if constexpr (TB) tbp[i] = make_uint2(W0, W1);  // column j's op at bits 2(j-1) of the row's 64 bits
+    }
+    uint32_t cap = V[1];
+#pragma unroll
+    for (int j = 2; j <= MM; ++j) cap = (j == m) ? V[j] : cap;
+    const uint32_t D = cap >> 16;
+    const int32_t L = LEN ? (int32_t)((cap >> 2) & 0x3FFFu) : -1;
+    sed_result r;
+    r.dist = (double)D;
+    r.len = L;
+    r.is_int = (D == 0);
+    r.err = 0;
+    r.pad[0] = r.pad[1] = 0;
+    res[pair] = r;
+    if constexpr (TB) {
+        // canonical path, sink -> origin; op k of the script (origin -> sink) at bits 2(k&15) of word k>>4
+        uint32_t *po = ops + d.ops_off;
+        int i = n, j = m, k = L - 1;
+        uint32_t w = 0;
+        while (k >= 0) {
+            uint32_t op;
+            if (i == 0) op = 0;
+            else if (j == 0) op = 1;
+            else {
+                const uint2 rw = tbp[i - 1];
+                op = ((j <= 16 ? rw.x : rw.y) >> (2 * ((j - 1) & 15))) & 3u;
+            }
+            w |= op << (2 * (k & 15));
+            if ((k & 15) == 0) {
+                po[k >> 4] = w;
+                w = 0;
+            }
+            i -= (op != 0);
+            j -= (op != 1);
+            --k;
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t sed_launch_lane_i32(const sed_launch &L, const int32_t *idx, int nidx, const sed_i32_params &prm,
+                               bool len) {
+    if (nidx <= 0) return hipSuccess;
+    const dim3 grid((nidx + 255) / 256), block(256);
+    const uint32_t *a = (const uint32_t *)L.seqa, *b = (const uint32_t *)L.seqb;
+    if (L.tb)
+        hipLaunchKernelGGL((sed_lane_i32_kernel<true, true>), grid, block, 0, L.stream, L.pd, idx, nidx, a, b, L.tb,
+                           L.ops, L.res, prm);
+    else if (len)
+        hipLaunchKernelGGL((sed_lane_i32_kernel<true, false>), grid, block, 0, L.stream, L.pd, idx, nidx, a, b,
+                           nullptr, nullptr, L.res, prm);
+    else
+        hipLaunchKernelGGL((sed_lane_i32_kernel<false, false>), grid, block, 0, L.stream, L.pd, idx, nidx, a, b,
+                           nullptr, nullptr, L.res, prm);
+    return hipGetLastError();
+}

@@ -57,7 +57,7 @@ struct sed_ctx {
     int ins_int = 0, del_int = 0;
     DevBuf gtab;  // fp64 kernel table: per entry {value bits, is-int flag}
     // options
-    int opt_mode = 0, opt_R = 0, opt_split = 0;
+    int opt_mode = 0, opt_R = 0, opt_split = 0, opt_lane = 0;
     DevBuf selftest;
     sed_batch *scratch = nullptr;
 
@@ -84,8 +84,9 @@ struct sed_batch {
     std::vector<int32_t> n, m;
     uint64_t tb_words = 0, bnd_words = 0, ops_words = 0;
     double cells = 0, algo_bytes = 0;
-    DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops, d_tasks, d_prog;
+    DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops, d_tasks, d_prog, d_lane;
     bool split = false;
+    int nlane = 0, nwave = 0;  // pairs on the lane-per-pair kernel / on the wave kernels
     int ntasks = 0;
     uint64_t prog_words = 0;
     // SED_PIPELINE: run k uses traceback/result buffer k&1, so the traceback of
@@ -107,7 +108,7 @@ struct sed_batch {
     int cur() const { return (int)((runs - 1) & (nbuf - 1)); }
     ~sed_batch() {
         d_pd.release(); d_seqa.release(); d_seqb.release(); d_bnd.release(); d_ops.release();
-        d_tasks.release(); d_prog.release();
+        d_tasks.release(); d_prog.release(); d_lane.release();
         for (int i = 0; i < 2; ++i) {
             d_tb[i].release();
             d_res[i].release();
@@ -236,6 +237,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // ---- layout ----
     b->pd.assign(npairs, sed_pair_desc{});
     std::vector<int2> tasks;
+    std::vector<int32_t> lane_idx;
+    const bool use_lane = mode == SED_MODE_I32 && !split && c->opt_lane != 2;
     uint64_t aw = 0, bw = 0, tbw = 0, bndw = 0, opw = 0, progw = 0;
     const bool packed = (mode == SED_MODE_I32);
     double cells = 0, in_bytes = 0, tb_bytes = 0;
@@ -257,7 +260,11 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         d.bnd_off = bndw;
         d.ops_off = opw;
         d.prog_off = (int32_t)progw;
-        if (nn > 0 && mm > 0) {
+        if (use_lane && nn >= 1 && nn <= SED_LANE_MAXN && mm >= 1 && mm <= SED_LANE_MAXM) {
+            d.lane = 1;
+            lane_idx.push_back(p);
+            if (want_tb) tbw += 2 * (uint64_t)nn;  // one uint2 of 2-bit ops per row
+        } else if (nn > 0 && mm > 0) {
             const uint64_t G = 64 / R;  // steps per 16-byte traceback group (sed_kernels.hip: Grp)
             const uint64_t nstripes = (nn + ROWS - 1) / ROWS;
             const uint64_t SG = (mm + 63 + G - 1) / G * G;
@@ -278,6 +285,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     tb_bytes = cells * 0.25;
     b->tb_words = tbw;
     b->bnd_words = bndw;
+    b->nlane = (int)lane_idx.size();
+    b->nwave = npairs - b->nlane;
     b->ntasks = (int)tasks.size();
     b->prog_words = progw;
     b->ops_words = opw;
@@ -310,7 +319,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
                    b->d_seqb.reserve(sb) && b->d_ops.reserve(4 * std::max<uint64_t>(1, opw)) &&
                    b->d_bnd.reserve(4 * std::max<uint64_t>(1, bndw)) &&
                    b->d_tasks.reserve(sizeof(int2) * std::max<size_t>(1, tasks.size())) &&
-                   b->d_prog.reserve(4 * std::max<uint64_t>(1, progw));
+                   b->d_prog.reserve(4 * std::max<uint64_t>(1, progw)) &&
+                   b->d_lane.reserve(4 * std::max<size_t>(1, lane_idx.size()));
     for (int i = 0; i < b->nbuf && okalloc; ++i)
         okalloc = b->d_res[i].reserve(sizeof(sed_result) * std::max(1, npairs)) &&
                   (!want_tb || b->d_tb[i].reserve(4 * std::max<uint64_t>(1, tbw)));
@@ -329,6 +339,12 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     if (!tasks.empty() && (e = hipMemcpyAsync(b->d_tasks.p, tasks.data(), sizeof(int2) * tasks.size(),
                                               hipMemcpyHostToDevice, c->stream)) != hipSuccess)
         return c->hipfail(e, "upload tasks");
+    if (!lane_idx.empty() && (e = hipMemcpyAsync(b->d_lane.p, lane_idx.data(), 4 * lane_idx.size(),
+                                                 hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+        return c->hipfail(e, "upload lane list");
+    for (int i = 0; i < b->nbuf; ++i)
+        if ((e = hipMemsetAsync(b->d_res[i].p, 0, sizeof(sed_result) * std::max(1, npairs), c->stream)) != hipSuccess)
+            return c->hipfail(e, "zero results");
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hipfail(e, "upload sync");
 
     // ---- kernel parameters ----
@@ -389,6 +405,7 @@ int run_batch(sed_batch *b) {
     L.seqa = b->d_seqa.p;
     L.seqb = b->d_seqb.p;
     L.tb = want_tb ? (uint32_t *)b->d_tb[k].p : nullptr;
+    L.ops = (uint32_t *)b->d_ops.p;
     L.bnd = (uint32_t *)b->d_bnd.p;
     L.res = (sed_result *)b->d_res[k].p;
     L.R = b->R;
@@ -401,24 +418,30 @@ int run_batch(sed_batch *b) {
         return c->hipfail(e, "stream wait");
     if ((e = hipEventRecord(b->ev_dp0[k], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
     (void)hipEventRecord(lg[0], c->stream);
-    // per-run state: result error flags, and the SPLIT hand-off counters
-    if ((e = hipMemsetAsync(L.res, 0, sizeof(sed_result) * b->npairs, c->stream)) != hipSuccess)
+    // per-run state (SPLIT only): result error flags and the hand-off counters; the other kernels
+    // write every result field and never set err (buffers are zeroed once at creation)
+    if (b->split && (e = hipMemsetAsync(L.res, 0, sizeof(sed_result) * b->npairs, c->stream)) != hipSuccess)
         return c->hipfail(e, "memset results");
     if (b->split && b->prog_words &&
         (e = hipMemsetAsync(b->d_prog.p, 0, 4 * b->prog_words, c->stream)) != hipSuccess)
         return c->hipfail(e, "memset progress");
-    if (b->mode == SED_MODE_I32)
-        e = sed_launch_i32(L, b->ip);
-    else
-        e = sed_launch_f64(L, (const double *)c->gtab.p, b->fp, b->mode == SED_MODE_F64_TYPED);
-    if (e != hipSuccess) return c->hipfail(e, "DP kernel launch");
+    const bool len = want_tb || !(b->flags & SED_NO_LEN);
+    if (b->nwave > 0) {
+        if (b->mode == SED_MODE_I32)
+            e = sed_launch_i32(L, b->ip, len);
+        else
+            e = sed_launch_f64(L, (const double *)c->gtab.p, b->fp, b->mode == SED_MODE_F64_TYPED);
+        if (e != hipSuccess) return c->hipfail(e, "DP kernel launch");
+    }
+    if (b->nlane > 0 && (e = sed_launch_lane_i32(L, (const int32_t *)b->d_lane.p, b->nlane, b->ip, len)) != hipSuccess)
+        return c->hipfail(e, "lane kernel launch");
     if ((e = hipEventRecord(b->ev_dp1[k], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
     (void)hipEventRecord(lg[1], c->stream);
     if (ts != c->stream && (e = hipStreamWaitEvent(ts, b->ev_dp1[k], 0)) != hipSuccess)
         return c->hipfail(e, "stream wait");
     if ((e = hipEventRecord(b->ev_tb0[k], ts)) != hipSuccess) return c->hipfail(e, "event record");
     (void)hipEventRecord(lg[2], ts);
-    if (want_tb) {
+    if (want_tb && b->nwave > 0) {
         L.stream = ts;
         if ((e = sed_launch_traceback(L, (uint32_t *)b->d_ops.p)) != hipSuccess)
             return c->hipfail(e, "traceback kernel launch");
@@ -512,6 +535,10 @@ int sed_set_option(sed_ctx *c, int key, int value) {
         c->opt_split = value;
         return SED_OK;
     }
+    if (key == SED_OPT_LANE && value >= 0 && value <= 2) {
+        c->opt_lane = value;
+        return SED_OK;
+    }
     if (key == SED_OPT_ROWS_PER_LANE && (value == 0 || value == 1 || value == 2 || value == 4 || value == 8 ||
                                          value == 16 || value == 32)) {
         c->opt_R = value;
@@ -571,6 +598,7 @@ void sed_batch_destroy(sed_batch *b) {
 
 int sed_batch_mode(const sed_batch *b) { return b ? b->mode : SED_E_ARG; }
 int sed_batch_rows_per_lane(const sed_batch *b) { return b ? b->R : SED_E_ARG; }
+int sed_batch_lane_pairs(const sed_batch *b) { return b ? b->nlane : SED_E_ARG; }
 
 int sed_batch_run(sed_batch *b) {
     if (!b) return SED_E_ARG;

@@ -13,9 +13,11 @@ LIB_PATH = os.environ.get("SED_LIBRARY", os.path.join(HERE, "libsed.so"))
 
 SED_WANT_SCRIPT = 1
 SED_PIPELINE = 2
+SED_NO_LEN = 4
 SED_OPT_MODE = 1
 SED_OPT_ROWS_PER_LANE = 2
 SED_OPT_SPLIT = 3
+SED_OPT_LANE = 4
 MODE_NAMES = {1: "i32", 2: "f64", 3: "f64-typed"}
 
 _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
@@ -39,6 +41,7 @@ SIGNATURES = [
     ("sed_batch_destroy", None, [C.c_void_p]),
     ("sed_batch_mode", C.c_int, [C.c_void_p]),
     ("sed_batch_rows_per_lane", C.c_int, [C.c_void_p]),
+    ("sed_batch_lane_pairs", C.c_int, [C.c_void_p]),
     ("sed_batch_run", C.c_int, [C.c_void_p]),
     ("sed_batch_sync", C.c_int, [C.c_void_p]),
     ("sed_batch_last_times", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
@@ -125,8 +128,9 @@ class Context:
     def selftest(self):
         return self._lib.sed_selftest(self.ptr)
 
-    def run(self, packed, want_script):
-        """packed: PackedPairs.  Returns (dist f64[], is_int u8[], len i32[], ops u32[] | None)."""
+    def run(self, packed, want_script, no_len=False):
+        """packed: PackedPairs.  Returns (dist f64[], is_int u8[], len i32[], ops u32[] | None).
+        no_len (distance only): lengths are not computed (-1), the integer kernels run 5 ops/cell."""
         np_ = packed.npairs
         dist = np.zeros(max(np_, 1), np.float64)
         is_int = np.zeros(max(np_, 1), np.uint8)
@@ -138,7 +142,8 @@ class Context:
             ops_ptr = ops.ctypes.data_as(C.c_void_p)
             ops_off_ptr = packed.ops_off.ctypes.data_as(C.c_void_p)
         rc = self._lib.sed_run_batch(self.ptr, packed.codes_a, packed.off_a, packed.len_a, packed.codes_b,
-                                     packed.off_b, packed.len_b, np_, SED_WANT_SCRIPT if want_script else 0,
+                                     packed.off_b, packed.len_b, np_,
+                                     SED_WANT_SCRIPT if want_script else (SED_NO_LEN if no_len else 0),
                                      dist, is_int, ln, ops_ptr, ops_off_ptr)
         self._check(rc, "sed_run_batch")
         return dist[:np_], is_int[:np_], ln[:np_], ops
@@ -201,12 +206,13 @@ def unpack_ops(ops_words, ops_off, p, length):
 class Batch:
     """Device-resident batch (sed_batch_*): upload once, run many times."""
 
-    def __init__(self, ctx, packed, want_script, pipeline=False):
+    def __init__(self, ctx, packed, want_script, pipeline=False, no_len=False):
         self.ctx = ctx
         self._lib = ctx._lib
         self.packed = packed
         self.want_script = want_script
-        flags = (SED_WANT_SCRIPT if want_script else 0) | (SED_PIPELINE if pipeline else 0)
+        flags = (SED_WANT_SCRIPT if want_script else (SED_NO_LEN if no_len else 0)) | \
+            (SED_PIPELINE if pipeline else 0)
         self.ptr = self._lib.sed_batch_create(ctx.ptr, packed.codes_a, packed.off_a, packed.len_a, packed.codes_b,
                                               packed.off_b, packed.len_b, packed.npairs, flags)
         if not self.ptr:
@@ -231,6 +237,10 @@ class Batch:
     @property
     def rows_per_lane(self):
         return self._lib.sed_batch_rows_per_lane(self.ptr)
+
+    @property
+    def lane_pairs(self):
+        return self._lib.sed_batch_lane_pairs(self.ptr)
 
     def run(self):
         self.ctx._check(self._lib.sed_batch_run(self.ptr), "sed_batch_run")

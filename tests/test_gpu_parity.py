@@ -20,15 +20,16 @@ OPCH = "idu"
 IUPAC = "AGCUYRWSKMDVHBN"
 
 
-def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0):
+def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len=False):
     """Run (s1, s2) pairs through the engine; returns [(dist, is_int, len, opstr)]."""
     plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
     ctx.set_mode(mode)
     ctx.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, R)
     ctx.set_option(sedgpu.SED_OPT_SPLIT, split)
+    ctx.set_option(sedgpu.SED_OPT_LANE, lane)
     ctx.set_costs(plan)
     packed = sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs], [plan.encode(b) for _, b in pairs])
-    dist, is_int, ln, ops = ctx.run(packed, script)
+    dist, is_int, ln, ops = ctx.run(packed, script, no_len=no_len)
     out = []
     for p in range(len(pairs)):
         s = None
@@ -38,6 +39,7 @@ def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0):
     ctx.set_mode(0)
     ctx.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
     ctx.set_option(sedgpu.SED_OPT_SPLIT, 0)
+    ctx.set_option(sedgpu.SED_OPT_LANE, 0)
     return out
 
 
@@ -98,13 +100,15 @@ def _random_pairs(seed, count, alphabet, lo, hi, related=False):
     return out
 
 
-def _oracle_check(table, pairs, got):
+def _oracle_check(table, pairs, got, no_len=False):
     plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
     cs = oracle.Costs.from_plan(plan)
     for (a, b), (d, ii, ln, s) in zip(pairs, got):
         o = oracle.pair(cs, plan.encode(a), plan.encode(b))
-        assert (d, ii, ln) == (o["dist"], bool(o["is_int"]), o["len"]), (len(a), len(b))
-        assert s == oracle.ops_to_str(o["ops"]), (len(a), len(b))
+        assert (d, ii) == (o["dist"], bool(o["is_int"])), (len(a), len(b))
+        assert ln == (-1 if no_len and len(a) and len(b) else o["len"]), (len(a), len(b))
+        if s is not None:
+            assert s == oracle.ops_to_str(o["ops"]), (len(a), len(b))
 
 
 @pytest.mark.parametrize("user", [False, True])
@@ -138,3 +142,35 @@ def test_full_matrix_g1(gpu, tables):
         want = [[float.fromhex(h), bool(ii), mk] for h, ii, mk in r["cells"]]
         have = [[float(d), bool(mm >> 3), int(mm & 7)] for d, mm in zip(D.ravel(), M.ravel())]
         assert want == have, (r["s1"], r["s2"])
+
+
+@pytest.mark.parametrize("user", [False, True])
+def test_lane_kernel_short_str2_vs_oracle(gpu, tables, user):
+    """Lane-per-pair kernel (m <= 32, n <= 512) mixed in one batch with wave-kernel pairs
+    (m > 32 or n > 512): scripts, distance + length, distance only (SED_NO_LEN)."""
+    rng = np.random.default_rng(31 + user)
+    pairs = []
+    for _ in range(300):
+        n = int(rng.choice([rng.integers(1, 40), rng.integers(1, 513), rng.integers(500, 700)]))
+        m = int(rng.choice([rng.integers(1, 33), 32, 33, rng.integers(20, 80)]))
+        a = "".join(rng.choice(list("ACGU"), size=n))
+        b = "".join(rng.choice(list("ACGU"), size=m)) if rng.random() < 0.5 else \
+            "".join(c if rng.random() > 0.1 else rng.choice(list("ACGU")) for c in a[:m])
+        pairs.append((a, b or "A"))
+    pairs += [("A", "C"), ("ACGU" * 128, "ACGU" * 8), ("G" * 512, "G" * 32), ("G" * 513, "G" * 32)]
+    _oracle_check(tables[user], pairs, gpu_run(gpu, tables[user], pairs))
+    _oracle_check(tables[user], pairs, gpu_run(gpu, tables[user], pairs, script=False))
+    _oracle_check(tables[user], pairs, gpu_run(gpu, tables[user], pairs, script=False, no_len=True), no_len=True)
+    # the same batch with the lane kernel disabled (every pair on the wave kernel)
+    _oracle_check(tables[user], pairs, gpu_run(gpu, tables[user], pairs, lane=2))
+    _oracle_check(tables[user], pairs, gpu_run(gpu, tables[user], pairs, script=False, no_len=True, lane=2),
+                  no_len=True)
+
+
+def test_lane_kernel_all_vs_all_shape(gpu, tables):
+    """Config-5 shape: every pair on the lane kernel (piRNA-like lengths 24..32)."""
+    rng = np.random.default_rng(5)
+    seqs = ["".join(rng.choice(list("ACGU"), size=int(rng.integers(24, 33)))) for _ in range(40)]
+    pairs = [(a, b) for a in seqs for b in seqs]
+    _oracle_check(tables[False], pairs, gpu_run(gpu, tables[False], pairs, script=False, no_len=True), no_len=True)
+    _oracle_check(tables[False], pairs[::7], gpu_run(gpu, tables[False], pairs[::7]))
