@@ -94,8 +94,8 @@ struct sed_batch {
     int nbuf = 1;
     DevBuf d_tb[2], d_res[2];
     hipStream_t tb_stream = nullptr;
-    // events per buffer: DP start/end on the DP stream, traceback start/end on the traceback stream
-    hipEvent_t ev_dp0[2] = {}, ev_dp1[2] = {}, ev_tb0[2] = {}, ev_tb1[2] = {};
+    // per buffer: the event-log entry of the last run that used it (handles copied from `log`)
+    std::array<hipEvent_t, 4> evk[2] = {};
     long runs = 0;
     bool ran = false;
     // per-run event log (sed_batch_times): {dp start, dp end, tb start, tb end}
@@ -112,8 +112,6 @@ struct sed_batch {
         for (int i = 0; i < 2; ++i) {
             d_tb[i].release();
             d_res[i].release();
-            for (hipEvent_t e : {ev_dp0[i], ev_dp1[i], ev_tb0[i], ev_tb1[i]})
-                if (e) (void)hipEventDestroy(e);
         }
         if (tb_stream) (void)hipStreamDestroy(tb_stream);
         for (auto &a : log)
@@ -162,6 +160,20 @@ int choose_R(int mode, int max_n, int forced) {
     const int want = next_pow2(std::max(1, (max_n + 63) / 64));
     if (mode == SED_MODE_I32) return std::min(16, std::max(4, want));
     return std::min(8, std::max(4, want));
+}
+
+// Event-log entries {DP start, DP end, traceback start, traceback end}, created ahead of the runs
+// that use them (outside any timed loop for up to `more` runs).
+hipError_t grow_log(sed_batch *b, size_t more) {
+    for (size_t i = 0; i < more; ++i) {
+        std::array<hipEvent_t, 4> a{};
+        for (auto &x : a) {
+            hipError_t e = hipEventCreate(&x);
+            if (e != hipSuccess) return e;
+        }
+        b->log.push_back(a);
+    }
+    return hipSuccess;
 }
 
 int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const int32_t *len_a,
@@ -372,9 +384,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         fp.K = c->K;
         b->fp = fp;
     }
-    for (int i = 0; i < 2; ++i)
-        for (hipEvent_t *ev : {&b->ev_dp0[i], &b->ev_dp1[i], &b->ev_tb0[i], &b->ev_tb1[i]})
-            if (!*ev && (e = hipEventCreate(ev)) != hipSuccess) return c->hipfail(e, "event create");
+    if ((e = grow_log(b, 64)) != hipSuccess) return c->hipfail(e, "event create");
     if (b->nbuf == 2 && !b->tb_stream &&
         (e = hipStreamCreateWithFlags(&b->tb_stream, hipStreamNonBlocking)) != hipSuccess)
         return c->hipfail(e, "traceback stream");
@@ -391,13 +401,8 @@ int run_batch(sed_batch *b) {
     const int k = (int)(b->runs & (b->nbuf - 1));
     const bool want_tb = (b->flags & SED_WANT_SCRIPT) != 0;
     hipError_t e;
-    if (b->nlog == b->log.size()) {
-        std::array<hipEvent_t, 4> a{};
-        for (auto &x : a)
-            if ((e = hipEventCreate(&x)) != hipSuccess) return c->hipfail(e, "event create");
-        b->log.push_back(a);
-    }
-    const std::array<hipEvent_t, 4> &lg = b->log[b->nlog++];
+    if (b->nlog == b->log.size() && (e = grow_log(b, 64)) != hipSuccess) return c->hipfail(e, "event create");
+    const std::array<hipEvent_t, 4> lg = b->log[b->nlog++];
     hipStream_t ts = b->nbuf == 2 ? b->tb_stream : c->stream;
     sed_launch L{};
     L.pd = (const sed_pair_desc *)b->d_pd.p;
@@ -414,10 +419,11 @@ int run_batch(sed_batch *b) {
     L.prog = (uint32_t *)b->d_prog.p;
     L.ntasks = b->split ? b->ntasks : 0;
     // buffer k was last read by the traceback of run runs-2
-    if (b->nbuf == 2 && b->runs >= 2 && (e = hipStreamWaitEvent(c->stream, b->ev_tb1[k], 0)) != hipSuccess)
+    if (b->nbuf == 2 && want_tb && b->runs >= 2 && (e = hipStreamWaitEvent(c->stream, b->evk[k][3], 0)) != hipSuccess)
         return c->hipfail(e, "stream wait");
-    if ((e = hipEventRecord(b->ev_dp0[k], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
-    (void)hipEventRecord(lg[0], c->stream);
+    // Only the event-log records sit between kernels: each record is a packet on the queue, and for
+    // the ~50 us lane kernel (config 5) every avoided record is measurable.
+    if ((e = hipEventRecord(lg[0], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
     // per-run state (SPLIT only): result error flags and the hand-off counters; the other kernels
     // write every result field and never set err (buffers are zeroed once at creation)
     if (b->split && (e = hipMemsetAsync(L.res, 0, sizeof(sed_result) * b->npairs, c->stream)) != hipSuccess)
@@ -435,19 +441,18 @@ int run_batch(sed_batch *b) {
     }
     if (b->nlane > 0 && (e = sed_launch_lane_i32(L, (const int32_t *)b->d_lane.p, b->nlane, b->ip, len)) != hipSuccess)
         return c->hipfail(e, "lane kernel launch");
-    if ((e = hipEventRecord(b->ev_dp1[k], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
-    (void)hipEventRecord(lg[1], c->stream);
-    if (ts != c->stream && (e = hipStreamWaitEvent(ts, b->ev_dp1[k], 0)) != hipSuccess)
-        return c->hipfail(e, "stream wait");
-    if ((e = hipEventRecord(b->ev_tb0[k], ts)) != hipSuccess) return c->hipfail(e, "event record");
-    (void)hipEventRecord(lg[2], ts);
-    if (want_tb && b->nwave > 0) {
-        L.stream = ts;
-        if ((e = sed_launch_traceback(L, (uint32_t *)b->d_ops.p)) != hipSuccess)
-            return c->hipfail(e, "traceback kernel launch");
+    if ((e = hipEventRecord(lg[1], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
+    if (want_tb) {
+        if (ts != c->stream && (e = hipStreamWaitEvent(ts, lg[1], 0)) != hipSuccess) return c->hipfail(e, "stream wait");
+        if ((e = hipEventRecord(lg[2], ts)) != hipSuccess) return c->hipfail(e, "event record");
+        if (b->nwave > 0) {
+            L.stream = ts;
+            if ((e = sed_launch_traceback(L, (uint32_t *)b->d_ops.p)) != hipSuccess)
+                return c->hipfail(e, "traceback kernel launch");
+        }
+        if ((e = hipEventRecord(lg[3], ts)) != hipSuccess) return c->hipfail(e, "event record");
     }
-    if ((e = hipEventRecord(b->ev_tb1[k], ts)) != hipSuccess) return c->hipfail(e, "event record");
-    (void)hipEventRecord(lg[3], ts);
+    b->evk[k] = lg;
     ++b->runs;
     b->ran = true;
     return SED_OK;
@@ -615,9 +620,9 @@ int sed_batch_last_times(const sed_batch *b, float *dp_ms, float *tb_ms) {
     if (!b || !b->ran) return SED_E_STATE;
     float a = 0, t = 0;
     if (b->npairs) {
-        const int k = b->cur();
-        if (hipEventElapsedTime(&a, b->ev_dp0[k], b->ev_dp1[k]) != hipSuccess) return SED_E_DEVICE;
-        if (hipEventElapsedTime(&t, b->ev_tb0[k], b->ev_tb1[k]) != hipSuccess) return SED_E_DEVICE;
+        const std::array<hipEvent_t, 4> &ev = b->evk[b->cur()];
+        if (hipEventElapsedTime(&a, ev[0], ev[1]) != hipSuccess) return SED_E_DEVICE;
+        if ((b->flags & SED_WANT_SCRIPT) && hipEventElapsedTime(&t, ev[2], ev[3]) != hipSuccess) return SED_E_DEVICE;
     }
     if (dp_ms) *dp_ms = a;
     if (tb_ms) *tb_ms = t;
@@ -632,7 +637,7 @@ int sed_batch_times(sed_batch *b, float *dp_ms, float *tb_ms, int max_runs) {
     for (int i = 0; i < cnt; ++i) {
         float a = 0, t = 0;
         if (hipEventElapsedTime(&a, b->log[i][0], b->log[i][1]) != hipSuccess ||
-            hipEventElapsedTime(&t, b->log[i][2], b->log[i][3]) != hipSuccess)
+            ((b->flags & SED_WANT_SCRIPT) && hipEventElapsedTime(&t, b->log[i][2], b->log[i][3]) != hipSuccess))
             return b->ctx->fail(SED_E_DEVICE, "event timing");
         if (dp_ms) dp_ms[i] = a;
         if (tb_ms) tb_ms[i] = t;
