@@ -22,8 +22,9 @@ len(dp), len(dp[0]) and dp[n][m].value need nothing more, any other cell
 materialises the whole matrix (values, int/float typing and the co-optimal
 edges) with one fp64 kernel.  create_paths(dp)[0] — the path the GUI and
 every edit-script consumer takes first — comes from the device traceback;
-later paths are enumerated on the host in the reference's BFS order over the
-materialised edges.  Deliberate differences: no import-time demo print
+later paths are enumerated on the host in the reference's order (length, then
+sink-lexicographic) over the materialised edges by copaths.iter_paths, and
+count_paths(dp) gives their number without enumerating them.  Deliberate differences: no import-time demo print
 (:463-471), and create_paths never blocks (the reference's bounded Queue
 deadlocks once live paths exceed (n+1)(m+1), :237,265).
 
@@ -35,6 +36,7 @@ from collections import deque
 
 import numpy as np
 
+import copaths
 import sedcost
 import sedgpu
 
@@ -333,25 +335,10 @@ def _cells_of_script(dp, ops):
     return Path(cells, ops)
 
 
-def _bfs_paths(dp):
-    """Every co-optimal path in the reference's order (BFS from the sink over
-    incoming edges stored insert, delete, update), without its queue bound."""
-    M = dp._materialise()[1]
-    q = deque([((dp.n, dp.m),)])
-    while q:
-        p = q.popleft()
-        r, c = p[-1]
-        if r == 0 and c == 0:
-            yield p
-        mask = int(M[r, c]) & 7
-        for bit, (pr, pc) in ((1, (r, c - 1)), (2, (r - 1, c)), (4, (r - 1, c - 1))):
-            if mask & bit:
-                q.append(p + ((pr, pc),))
-
-
 class PathList:
     """Lazy result of create_paths(dp): element 0 is the device's canonical
-    path; the rest are enumerated on demand, in the reference's order."""
+    path; the rest are enumerated on demand, in the reference's order, by
+    copaths.iter_paths over the materialised edge mask (no BFS frontier)."""
 
     def __init__(self, dp):
         self._dp = dp
@@ -366,18 +353,14 @@ class PathList:
         if self._exhausted:
             return False
         if self._gen is None:
-            self._gen = _bfs_paths(self._dp)
-            next(self._gen)  # the first BFS path is the canonical one already returned
+            self._gen = copaths.iter_paths(self._dp._materialise()[1])
+            next(self._gen)  # the first path in reference order is the canonical one already returned
         try:
-            p = next(self._gen)
+            ops = next(self._gen)
         except StopIteration:
             self._exhausted = True
             return False
-        cells = [self._dp.cell(r, c) for r, c in reversed(p)]
-        ops = []
-        for a, b in zip(cells, cells[1:]):
-            ops.append(2 if (b.row > a.row and b.col > a.col) else (1 if b.row > a.row else 0))
-        self._done.append(Path(cells, np.array(ops, np.uint8)))
+        self._done.append(_cells_of_script(self._dp, ops))
         return True
 
     def __getitem__(self, k):
@@ -413,6 +396,21 @@ def create_paths(dp):
         dp[dp.n][dp.m].visited = True
         return PathList(dp)
     return _create_paths_graph(dp)
+
+
+def count_paths(dp):
+    """Number of co-optimal paths, i.e. len(create_paths(dp)), as an exact int without
+    enumerating them (extension)."""
+    if isinstance(dp, DPMatrix):
+        return copaths.count_paths(dp._materialise()[1])
+    n, m = len(dp) - 1, len(dp[0]) - 1
+    M = np.zeros((n + 1, m + 1), np.uint8)
+    bit = {"insert": 1, "delete": 2, "update": 4}
+    for r in range(n + 1):
+        for c in range(m + 1):
+            for e in dp[r][c].incoming_edges:
+                M[r, c] |= bit[e.operation]
+    return copaths.count_paths(M)
 
 
 def _create_paths_graph(dp):

@@ -18,6 +18,11 @@ Fixture sets:
   G4  25x25 wf_score matrix over test_input.xml (IRMethods.wf_score).
   G5  generate_rev_es / generate_sequence_from_es / patching cases.
   G6  error and typing cases (KeyError, IndexError, int-zero typing).
+  G7  ingest + search: import_xml on test_input.xml and on seqxml_cases.xml (T/X
+      normalisation, duplicate ids), and IRMethods.search_collection(query, ..., wf_score)
+      over a list-backed collection of the test_input.xml sequences.
+
+    python -B tests/golden/make_golden.py --g7       # G7 only
 """
 import hashlib
 import io
@@ -269,6 +274,43 @@ def gen_g6(S):
     return out
 
 
+SEQXML_CASES = """<?xml version="1.0"?>
+<seqXML source="synthetic" seqXMLversion="0.4">
+    <entry id="t-and-x"><RNAseq>ACGTTXGA</RNAseq></entry>
+    <entry id="plain"><RNAseq>GGGAAAUUUCCC</RNAseq></entry>
+    <entry id="dup"><RNAseq>AAAA</RNAseq></entry>
+    <entry id="lower"><RNAseq>acgtx</RNAseq></entry>
+    <entry id="dup"><RNAseq>TTTT</RNAseq></entry>
+    <entry id="iupac"><RNAseq>RYKMSWBDHVNX</RNAseq></entry>
+</seqXML>
+"""
+
+
+class _ListCollection:
+    """pymongo-collection stand-in: find({}) over a list of {'sequence': ...} docs."""
+
+    def __init__(self, seqs):
+        self.docs = [{"sequence": s} for s in seqs]
+
+    def find(self, flt):
+        assert flt == {}
+        return iter(self.docs)
+
+
+def gen_g7(IR, IX):
+    cases_path = os.path.join(HERE, "seqxml_cases.xml")
+    with open(cases_path, "w") as f:
+        f.write(SEQXML_CASES)
+    seqs = IX.import_xml(os.path.join(REF, "test_input.xml"))
+    docs = list(seqs.values())
+    coll = _ListCollection(docs)
+    searches = []
+    for q in (docs[0], docs[7], docs[-1], "ACGUACGUNN"):
+        scores = IR.search_collection(q, None, coll, IR.wf_score)
+        searches.append({"query": q, "scores": [[s, float(v).hex()] for s, v in scores]})
+    return {"test_input": seqs, "cases": IX.import_xml(cases_path), "searches": searches}
+
+
 def dump(name, obj):
     path = os.path.join(HERE, name)
     with open(path, "w") as f:
@@ -281,11 +323,15 @@ def main():
     if "--g3" in sys.argv:
         dump("g3_config2.json", gen_g3(S))
         return
+    if "--g7" in sys.argv:
+        dump("g7_ingest_search.json", gen_g7(IR, IX))
+        return
     dump("g1_small.json", gen_g1(S))
     dump("g6_errors.json", gen_g6(S))
     dump("g5_patching.json", gen_g5(S))
     dump("g4_wf_score.json", gen_g4(IR, IX))
     dump("g2_medium.json", gen_g2(S))
+    dump("g7_ingest_search.json", gen_g7(IR, IX))
 
 
 if __name__ == "__main__":

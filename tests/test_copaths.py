@@ -1,0 +1,56 @@
+"""CPU: co-optimal path enumeration in the reference's create_paths order (copaths.py) on the
+G1 golden masks (generated from the reference's own dp graphs and create_paths)."""
+import itertools
+import math
+
+import numpy as np
+
+from conftest import load_golden
+import copaths
+
+
+def _mask(rec):
+    n, m = len(rec["s1"]), len(rec["s2"])
+    return np.array([c[2] for c in rec["cells"]], np.uint8).reshape(n + 1, m + 1)
+
+
+def test_g1_paths_in_reference_order():
+    for r in load_golden("g1_small.json"):
+        M = _mask(r)
+        got = ["".join("idu"[o] for o in p) for p in copaths.iter_paths(M)]
+        assert got[0] == r["canon"], (r["s1"], r["s2"])
+        if r["paths"] == "deadlock":
+            # the reference blocks forever here (bounded queue); the count stands in for it
+            assert len(got) == copaths.count_paths(M) > (len(r["s1"]) + 1) * (len(r["s2"]) + 1)
+            continue
+        assert got == r["paths"], (r["s1"], r["s2"], r["user"])
+        assert copaths.count_paths(M) == r["npaths"] == len(got)
+
+
+def test_lazy_prefix_and_big_count():
+    # every edge optimal: the count is the Delannoy number D(n, m) (a 100-bit integer here)
+    n = m = 40
+    M = np.full((n + 1, m + 1), 7, np.uint8)
+    M[0, :] = 1
+    M[:, 0] = 2
+    M[0, 0] = 0
+    dela = sum(math.comb(n, k) * math.comb(m, k) * 2 ** k for k in range(min(n, m) + 1))
+    assert copaths.count_paths(M) == dela
+    first = list(itertools.islice(copaths.iter_paths(M), 5))
+    assert [len(p) for p in first] == [40, 41, 41, 41, 41]  # the all-update path, then one i+d pair
+    assert "".join("idu"[o] for o in first[0]) == "u" * 40
+    assert "".join("idu"[o] for o in first[1]) == "u" * 39 + "di"  # from the sink: i first
+    # shortest paths have exactly n updates; the next lengths come only after all of them
+    lengths = [len(p) for p in itertools.islice(copaths.iter_paths(M), 200)]
+    assert lengths == sorted(lengths)
+
+
+def test_lex_order_from_sink():
+    M = np.full((4, 4), 7, np.uint8)
+    M[0, :] = 1
+    M[:, 0] = 2
+    M[0, 0] = 0
+    paths = ["".join("idu"[o] for o in p) for p in copaths.iter_paths(M)]
+    assert len(paths) == copaths.count_paths(M) == 63  # Delannoy D(3,3)
+    key = [(len(p), p[::-1].translate(str.maketrans("idu", "012"))) for p in paths]
+    assert key == sorted(key)

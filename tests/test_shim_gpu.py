@@ -134,3 +134,42 @@ def test_reload_user_costs(SED, tmp_path, monkeypatch):
         assert SED.wagnerFisher("", "AC", True)[-1][-1].value == 2.0
     finally:
         SED.user_costs = old
+
+
+def test_count_paths_and_enumeration(SED):
+    import itertools
+    import copaths
+    for r in load_golden("g1_small.json")[::5]:
+        dp = SED.wagnerFisher(r["s1"], r["s2"], r["user"])
+        if r["paths"] != "deadlock":
+            assert SED.count_paths(dp) == r["npaths"]
+    # medium pairs: the device's canonical script is the first path of the ordered enumeration,
+    # and the next paths come quickly (the reference's BFS frontier would be exponential here)
+    for r in load_golden("g2_medium.json")[:6]:
+        dp = SED.wagnerFisher(r["s1"], r["s2"], r["user"])
+        paths = SED.create_paths(dp)
+        first = next(copaths.iter_paths(dp._materialise()[1]))
+        assert np.array_equal(first, paths[0].ops)
+        more = [p.ops for p in itertools.islice(iter(paths), 20)]
+        keys = [(len(o), tuple(o[::-1])) for o in more]
+        assert keys == sorted(keys) and len(set(keys)) == len(keys)
+        assert SED.count_paths(dp) >= len(more)
+
+
+def test_search_collection_matches_reference(SED):
+    import seqio
+    import wfsearch
+    g7 = load_golden("g7_ingest_search.json")
+    coll = seqio.ListCollection.from_sequences(list(g7["test_input"].values()))
+    wfsearch.clear_cache()
+    for s in g7["searches"]:
+        want = [[seq, float.fromhex(h)] for seq, h in s["scores"]]
+        got = wfsearch.search_collection(s["query"], None, coll, wfsearch.wf_score)
+        assert [[a, b] for a, b in got] == want
+        rd = {}
+        wfsearch.search_collection(s["query"], "tf", coll, wfsearch.wf_score, return_dict=rd)  # cached
+        assert [[a, b] for a, b in rd["wf_score"]] == want
+        seen = []
+        wfsearch.search_collection(s["query"], None, coll, wfsearch.wf_score, callback=seen.append)
+        assert [[a, b] for a, b in seen[0]] == want
+        assert wfsearch.wf_score(s["query"], want[3][0]) == want[3][1]
