@@ -149,41 +149,45 @@ __device__ __forceinline__ void i32_reset(uint32_t (&V)[R], uint32_t &top_prev, 
     }
 }
 
-// SLOW groups: ramp-up (the lane that starts next step is reset to column 0)
-// and the group that produces the sink cell (captured).  Branch-free selects,
-// so no value lives across a basic-block boundary.
-template <int R, bool TB, bool LEN, bool SLOW>
+// Ramp without resets.  Every lane starts a stripe at its column-0 state (i32_reset) and lane
+// t begins real work at step t.  Before that it runs "virtual" negative columns that must leave
+// its state unchanged, which costs one per-lane select per step instead of per-row resets:
+//   * its str2 selector is the sentinel SED_SEL_SENT (perm byte 0x0D -> cost 0xFF), so the update
+//     candidate is far above the others;
+//   * its insert constant is 0, so the insert candidate is exactly the old value (op 0, L kept),
+//     one below the delete candidate border(row-1) + kdel = border(row) + 1.
+// The state (V, bottom, top_prev) therefore stays at the column-0 borders until the lane's
+// first real column, whose neighbours are then exactly D[row][0], D[row-1][0] and the cell above.
+#define SED_SEL_SENT 0x0C0D0100u
+
+// RAMP groups: steps < 63 of a stripe (per-lane insert constant).  CAP: the group that produces
+// the sink cell (captured on its lane).  Branch-free selects, so no value lives across a
+// basic-block boundary.
+template <int R, bool TB, bool LEN, bool RAMP, bool CAP>
 __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                           uint32_t &bottom, uint32_t &selv, uint32_t &tch, uint32_t &sch,
                                           const uint2 *__restrict__ lch, uint32_t &outc, uint32_t (&W)[4],
-                                          const int s0, const int lane, const int row0, const uint32_t kins,
-                                          const uint32_t kdel, const uint32_t del, const int cap_step,
-                                          const int cap_lane, const int cap_row, uint32_t &cap) {
+                                          const int s0, const int lane, const uint32_t kins, const uint32_t kdel,
+                                          const int cap_step, const int cap_lane, const int cap_row, uint32_t &cap) {
     constexpr int G = Grp<R>::G;
+    // opaque copies: the four group variants sit in sibling branches, and without this the
+    // compiler hoists the first step's V[r] + kins out of them (16 more live VGPRs -> spills)
+    uint32_t kin = kins, kde = kdel;
+    asm volatile("" : "+s"(kin), "+s"(kde));
     uint2 tv[G];
     const uint2 *lp = lch + (s0 & 63);  // G divides 64: a group never wraps the chunk
 #pragma unroll
     for (int u = 0; u < G; ++u) tv[u] = SED_I32_LDS_CHUNK ? lp[u] : make_uint2(0, 0);
 #pragma unroll
     for (int u = 0; u < G; ++u) {
-        i32_step<R, TB, LEN>(V, cv, top_prev, bottom, selv, tch, sch, tv[u], outc, W, u, kins, kdel);
-        if constexpr (SLOW) {
-            const int s = s0 + u;
+        const int s = s0 + u;
+        uint32_t ki = kin;
+        if constexpr (RAMP) ki = kin & ~(uint32_t)((s - lane) >> 31);  // virtual column: insert adds nothing
+        i32_step<R, TB, LEN>(V, cv, top_prev, bottom, selv, tch, sch, tv[u], outc, W, u, ki, kde);
+        if constexpr (CAP) {
             const bool hit = (s == cap_step) && (lane == cap_lane);
 #pragma unroll
             for (int r = 0; r < R; ++r) cap = (hit && r == cap_row) ? V[r] : cap;
-            const bool start = (lane == s + 1);
-            int rr = row0;
-            uint32_t dd = del;
-            asm volatile("" : "+v"(rr), "+s"(dd));  // keep the column-0 values from being hoisted (VGPRs)
-            uint32_t v = i32_border((uint32_t)rr, dd);
-            const uint32_t st = (dd << 16) | 4u;
-            top_prev = start ? v : top_prev;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                v += st;
-                V[r] = start ? v : V[r];
-            }
         }
     }
 }
@@ -283,7 +287,8 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
         }
         uint32_t top_prev;
         i32_reset<R>(V, top_prev, row0, prm.del);
-        uint32_t bottom = 0, selv = 0, outc = 0;
+        // column-0 state for every lane; virtual columns until the lane's first real one (see above)
+        uint32_t bottom = V[R - 1], selv = SED_SEL_SENT, outc = 0;
         uint32_t W[4] = {0, 0, 0, 0};
 
         auto load_top = [&](int c) -> uint32_t {
@@ -309,12 +314,19 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             uint32_t tnx = 0, snx = 0;
             if (c + 1 < nchunks) { tnx = load_top(c + 1); snx = load_sel(c + 1); }
             for (int g = 0; g < 64 / G && s < SG; ++g, s += G) {
-                if (s < 63 || (cap_step >= s && cap_step < s + G))
-                    i32_group<R, TB, LEN, true>(V, cv, top_prev, bottom, selv, tch, sch, lch, outc, W, s, lane, row0,
-                                           kins, kdel, prm.del, cap_step, cap_lane, cap_row, cap);
-                else
-                    i32_group<R, TB, LEN, false>(V, cv, top_prev, bottom, selv, tch, sch, lch, outc, W, s, lane, row0,
-                                            kins, kdel, prm.del, cap_step, cap_lane, cap_row, cap);
+                const bool capg = cap_step >= s && cap_step < s + G;
+#define SED_GROUP(RAMP, CAP)                                                                            \
+    i32_group<R, TB, LEN, RAMP, CAP>(V, cv, top_prev, bottom, selv, tch, sch, lch, outc, W, s, lane, kins, kdel, \
+                                     cap_step, cap_lane, cap_row, cap)
+                if (s < 63) {
+                    if (capg) SED_GROUP(true, true);
+                    else SED_GROUP(true, false);
+                } else if (capg) {
+                    SED_GROUP(false, true);
+                } else {
+                    SED_GROUP(false, false);
+                }
+#undef SED_GROUP
                 if constexpr (TB) {
                     uint32_t *gp = tbk + (uint64_t)(s / G) * 256u;  // wave-uniform base, per-lane 16-byte offset
                     store_tb(gp + lane * 4, W);

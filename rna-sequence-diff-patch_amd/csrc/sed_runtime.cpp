@@ -220,7 +220,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         for (int p = 0; p < npairs && fits; ++p) {
             const double npad = (double)((len_a[p] + ROWS - 1) / ROWS) * ROWS;
             const double dmax = npad * c->del + (double)len_b[p] * c->ins;
-            if (dmax >= 65536.0 || npad + len_b[p] >= 16384.0) fits = false;
+            // 256 of headroom: the ramp's sentinel update cost (0xFF << 16) is added to border values
+            if (dmax >= 65536.0 - 256.0 || npad + len_b[p] >= 16384.0) fits = false;
         }
         if (!fits) {
             if (c->opt_mode == 1) return c->fail(SED_E_RANGE, "integer key would overflow (D < 2^16, L < 2^14)");
