@@ -36,6 +36,7 @@ from collections import deque
 
 import numpy as np
 
+import _sedhost  # host C: edit-script dicts, reversal, patching, JSON (csrc/sedhost.c)
 import copaths
 import sedcost
 import sedgpu
@@ -316,23 +317,75 @@ def wagnerFisher(str1, str2, userCosts=False):
 # paths
 # ---------------------------------------------------------------------------
 class Path(list):
-    """A co-optimal path (list of Cell, origin -> sink) with its op codes."""
+    """A co-optimal path (list of Cell, origin -> sink) with its op codes.
 
-    def __init__(self, cells, ops=None):
-        super().__init__(cells)
+    The cells are built on first use: generate_es and the batch helpers only need
+    the op codes, and building 8k cell views of a 4096 x 4096 path costs ~4 ms."""
+
+    def __init__(self, dp, ops):
+        super().__init__()
         self.ops = ops
+        self._dp = dp
+        self._filled = False
+
+    def _fill(self):
+        if not self._filled:
+            self._filled = True
+            r = c = 0
+            cells = [self._dp.cell(0, 0)]
+            for op in self.ops:
+                if op != 1:
+                    c += 1
+                if op != 0:
+                    r += 1
+                cells.append(self._dp.cell(r, c))
+            list.extend(self, cells)
+        return self
+
+    def __len__(self):
+        return len(self.ops) + 1
+
+    def __bool__(self):
+        return True
+
+    def __getitem__(self, k):
+        return list.__getitem__(self._fill(), k)
+
+    def __iter__(self):
+        return list.__iter__(self._fill())
+
+    def __reversed__(self):
+        return list.__reversed__(self._fill())
+
+    def __contains__(self, x):
+        return list.__contains__(self._fill(), x)
+
+    def __eq__(self, other):
+        return list.__eq__(self._fill(), other)
+
+    __hash__ = None
+
+    def __repr__(self):
+        return list.__repr__(self._fill())
+
+    def index(self, *a):
+        return list.index(self._fill(), *a)
+
+    def count(self, x):
+        return list.count(self._fill(), x)
+
+    def copy(self):
+        return list(self._fill())
+
+    def __add__(self, other):
+        return list(self._fill()) + list(other)
+
+    def __reduce__(self):
+        return (list, (list(self._fill()),))
 
 
 def _cells_of_script(dp, ops):
-    r = c = 0
-    cells = [dp.cell(0, 0)]
-    for op in ops:
-        if op != 1:
-            c += 1
-        if op != 0:
-            r += 1
-        cells.append(dp.cell(r, c))
-    return Path(cells, ops)
+    return Path(dp, ops)
 
 
 class PathList:
@@ -448,6 +501,8 @@ def generate_es(path, str1, str2):
     ops = getattr(path, 'ops', None)
     es = []
     if ops is not None and len(ops) == len(path) - 1:
+        if type(str1) is str and type(str2) is str:
+            return _sedhost.es_from_ops(np.asarray(ops, np.uint8).tobytes(), str1, str2)
         for op, nxt in zip(ops, path[1:]):
             es.append(_op_record(_OPNAME[op], str1, str2, nxt.i, nxt.j))
         return es
@@ -461,6 +516,9 @@ def generate_es(path, str1, str2):
 
 def generate_rev_es(es):
     """The script that turns str2 back into str1 (reference :338-369)."""
+    fast = _sedhost.rev_es(es)
+    if fast is not NotImplemented:
+        return fast
     out = []
     for e in es:
         op = e['operation']
@@ -483,6 +541,9 @@ def generate_rev_es(es):
 
 def generate_sequence_from_es(es):
     """The source string a script was generated from (reference :371-377)."""
+    fast = _sedhost.seq_from_es(es)
+    if fast is not NotImplemented:
+        return fast
     return ''.join(op['source']['character'] for op in es if op['operation'] != 'insert')
 
 
@@ -490,6 +551,9 @@ def patching(es, str1):
     """Apply an edit script to str1 -> (error_code, patched) (reference :380-457).
     error_code: 0 str1 is the script's source, 1 str1 is at least as long (warn),
     -1 str1 is shorter (returns (-1, ''))."""
+    fast = _sedhost.patching(es, str1)
+    if fast is not NotImplemented:
+        return fast
     original = generate_sequence_from_es(es)
     if str1 == original:
         error_code = 0
@@ -501,10 +565,11 @@ def patching(es, str1):
     removed = inserted = 0
     for rec in es:
         op = rec['operation']
+        at, dst_at = rec['source']['index'], rec['destination']['index']  # both read, as the reference does
         if op != 'insert':
-            at = rec['source']['index'] + removed + inserted
+            at = at + removed + inserted
         else:
-            at = rec['destination']['index']
+            at = dst_at
         if op == 'update':
             out = out[:at] + rec['destination']['character'] + out[at + 1:]
         elif op == 'delete':
@@ -514,6 +579,26 @@ def patching(es, str1):
             out = out[:at] + rec['destination']['character'] + out[at:]
             inserted += 1
     return (error_code, out)
+
+
+def es_to_json(es, indent=4):
+    """json.dumps({'edit_script': es}, indent=indent) — the GUI's export format (gui.py:629-638)."""
+    fast = _sedhost.es_json(es, indent)
+    if fast is not NotImplemented:
+        return fast
+    return json.dumps({'edit_script': es}, indent=indent)
+
+
+def save_es(path, es, indent=4):
+    """Write an edit script the way the GUI's export does (gui.py:629-638)."""
+    with open(path, 'w') as f:
+        f.write(es_to_json(es, indent))
+
+
+def load_es(path):
+    """Read an edit script the way the GUI's patch-tab import does (gui.py:650-657)."""
+    with open(path, 'r') as f:
+        return json.load(f)['edit_script']
 
 
 # ---------------------------------------------------------------------------
@@ -549,14 +634,7 @@ def edit_script_batch(strs1, strs2, userCosts=False):
     out = []
     for p, (a, b) in enumerate(zip(strs1, strs2)):
         codes = sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln[p]))
-        r = c = 0
-        es = []
-        for op in codes:
-            if op != 1:
-                c += 1
-            if op != 0:
-                r += 1
-            es.append(_op_record(_OPNAME[op], a, b, r - 1, c - 1))
+        es = _sedhost.es_from_ops(codes.tobytes(), a, b)
         v = float(dist[p])
         out.append((int(v) if is_int[p] else v, es))
     return out

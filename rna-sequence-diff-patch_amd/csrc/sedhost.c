@@ -1,0 +1,525 @@
+/* sedhost.c — host-side C for the edit-script half of the path, as a
+ * CPython extension module `_sedhost`.
+ *
+ * Once the DP and the traceback run on the GPU, a 4096 x 4096 pair spends more time in
+ * Python building the edit-script dicts, patching and writing JSON than on the device.
+ * These functions reproduce the reference's results exactly:
+ *
+ *   es_from_ops(ops, str1, str2)  generate_es over the canonical path given as op codes
+ *                                 (StringEditDistance.py:274-334, index -1 quirk included)
+ *   rev_es(es)                    generate_rev_es (:338-369), sharing the same dict objects
+ *   seq_from_es(es)               generate_sequence_from_es (:371-377)
+ *   patching(es, str1)            patching (:380-457), Python slicing semantics
+ *   es_json(es, indent)           json.dumps({'edit_script': es}, indent=indent) (gui.py:629-638)
+ *
+ * Each function returns NotImplemented for inputs outside its fast path (non-dict records,
+ * multi-character 'character' values, indices that do not fit a C long, non-ASCII text in
+ * JSON ...); the Python wrappers then run the Python restatement, so results never differ.
+ */
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#include <string.h>
+
+static PyObject *K_OPERATION, *K_SOURCE, *K_DESTINATION, *K_CHARACTER, *K_INDEX;
+static PyObject *S_INSERT, *S_DELETE, *S_UPDATE;
+
+/* ------------------------------------------------------------------ es_from_ops */
+static PyObject *char_at(PyObject *s, Py_ssize_t len, Py_ssize_t i) {
+    if (i < 0) i += len;
+    if (i < 0 || i >= len) {
+        PyErr_SetString(PyExc_IndexError, "string index out of range");
+        return NULL;
+    }
+    return PyUnicode_Substring(s, i, i + 1);
+}
+
+static PyObject *side(PyObject *s, Py_ssize_t len, Py_ssize_t i) {
+    PyObject *ch = char_at(s, len, i);
+    if (!ch) return NULL;
+    PyObject *idx = PyLong_FromSsize_t(i);
+    PyObject *d = PyDict_New();
+    if (!idx || !d || PyDict_SetItem(d, K_CHARACTER, ch) || PyDict_SetItem(d, K_INDEX, idx)) {
+        Py_XDECREF(d);
+        d = NULL;
+    }
+    Py_DECREF(ch);
+    Py_XDECREF(idx);
+    return d;
+}
+
+static PyObject *es_from_ops(PyObject *self, PyObject *args) {
+    Py_buffer ops;
+    PyObject *s1, *s2;
+    if (!PyArg_ParseTuple(args, "y*UU", &ops, &s1, &s2)) return NULL;
+    const unsigned char *op = (const unsigned char *)ops.buf;
+    const Py_ssize_t n = ops.len, l1 = PyUnicode_GET_LENGTH(s1), l2 = PyUnicode_GET_LENGTH(s2);
+    PyObject *out = PyList_New(n);
+    if (!out) goto fail;
+    Py_ssize_t r = 0, c = 0;
+    for (Py_ssize_t k = 0; k < n; ++k) {
+        if (op[k] > 2) {
+            PyErr_SetString(PyExc_ValueError, "op code > 2");
+            goto fail;
+        }
+        if (op[k] != 1) ++c;
+        if (op[k] != 0) ++r;
+        PyObject *src = side(s1, l1, r - 1);
+        if (!src) goto fail;
+        PyObject *dst = side(s2, l2, c - 1);
+        if (!dst) {
+            Py_DECREF(src);
+            goto fail;
+        }
+        PyObject *rec = PyDict_New();
+        PyObject *name = op[k] == 0 ? S_INSERT : (op[k] == 1 ? S_DELETE : S_UPDATE);
+        if (!rec || PyDict_SetItem(rec, K_OPERATION, name) || PyDict_SetItem(rec, K_SOURCE, src) ||
+            PyDict_SetItem(rec, K_DESTINATION, dst)) {
+            Py_XDECREF(rec);
+            Py_DECREF(src);
+            Py_DECREF(dst);
+            goto fail;
+        }
+        Py_DECREF(src);
+        Py_DECREF(dst);
+        PyList_SET_ITEM(out, k, rec);
+    }
+    PyBuffer_Release(&ops);
+    return out;
+fail:
+    Py_XDECREF(out);
+    PyBuffer_Release(&ops);
+    return NULL;
+}
+
+/* ------------------------------------------------------------------ helpers on records */
+/* str equality with the interned-pointer shortcut (generated records share the interned names) */
+static int eq(PyObject *a, PyObject *b) {
+    if (a == b) return 1;
+    if (!PyUnicode_Check(a)) return 0;
+    return PyUnicode_GET_LENGTH(a) == PyUnicode_GET_LENGTH(b) && PyUnicode_Compare(a, b) == 0;
+}
+
+/* borrowed rec[key] when rec is a dict holding it, else NULL without an exception set */
+static PyObject *get(PyObject *rec, PyObject *key) {
+    if (!PyDict_CheckExact(rec)) return NULL;
+    return PyDict_GetItemWithError(rec, key);
+}
+
+#define NOT_IMPL() \
+    do {           \
+        Py_RETURN_NOTIMPLEMENTED; \
+    } while (0)
+
+/* ------------------------------------------------------------------ rev_es */
+static PyObject *rev_es(PyObject *self, PyObject *es) {
+    if (!PyList_CheckExact(es)) NOT_IMPL();
+    const Py_ssize_t n = PyList_GET_SIZE(es);
+    /* validate first: any record outside the fast path -> Python restatement */
+    for (Py_ssize_t k = 0; k < n; ++k) {
+        PyObject *rec = PyList_GET_ITEM(es, k), *op, *src, *dst;
+        if (!(op = get(rec, K_OPERATION)) || !(src = get(rec, K_SOURCE)) || !(dst = get(rec, K_DESTINATION))) {
+            if (PyErr_Occurred()) return NULL;
+            NOT_IMPL();
+        }
+        if (!PyUnicode_CheckExact(op)) NOT_IMPL();
+        const int isd = eq(op, S_DELETE);
+        if (!isd && !eq(op, S_INSERT) && !eq(op, S_UPDATE)) NOT_IMPL();
+        if (isd) {
+            PyObject *i = get(dst, K_INDEX), *ch = get(dst, K_CHARACTER);
+            if (!i || !ch || !PyLong_CheckExact(i)) {
+                if (PyErr_Occurred()) return NULL;
+                NOT_IMPL();
+            }
+        }
+    }
+    PyObject *out = PyList_New(n);
+    if (!out) return NULL;
+    for (Py_ssize_t k = 0; k < n; ++k) {
+        PyObject *rec = PyList_GET_ITEM(es, k);
+        PyObject *op = get(rec, K_OPERATION), *src = get(rec, K_SOURCE), *dst = get(rec, K_DESTINATION);
+        PyObject *nop, *nsrc, *ndst = src;
+        if (eq(op, S_INSERT)) {
+            nop = S_DELETE;
+            nsrc = dst;
+            Py_INCREF(nsrc);
+        } else if (eq(op, S_DELETE)) {
+            nop = S_INSERT;
+            PyObject *one = PyLong_FromLong(1);
+            PyObject *i = one ? PyNumber_Subtract(get(dst, K_INDEX), one) : NULL;
+            Py_XDECREF(one);
+            nsrc = PyDict_New();
+            if (!i || !nsrc || PyDict_SetItem(nsrc, K_INDEX, i) ||
+                PyDict_SetItem(nsrc, K_CHARACTER, get(dst, K_CHARACTER))) {
+                Py_XDECREF(i);
+                Py_XDECREF(nsrc);
+                Py_DECREF(out);
+                return NULL;
+            }
+            Py_DECREF(i);
+        } else {
+            nop = S_UPDATE;
+            nsrc = dst;
+            Py_INCREF(nsrc);
+        }
+        PyObject *r = PyDict_New();
+        if (!r || PyDict_SetItem(r, K_OPERATION, nop) || PyDict_SetItem(r, K_SOURCE, nsrc) ||
+            PyDict_SetItem(r, K_DESTINATION, ndst)) {
+            Py_XDECREF(r);
+            Py_DECREF(nsrc);
+            Py_DECREF(out);
+            return NULL;
+        }
+        Py_DECREF(nsrc);
+        PyList_SET_ITEM(out, k, r);
+    }
+    return out;
+}
+
+/* ------------------------------------------------------------------ seq_from_es */
+/* fast path: every record a dict with a str operation; non-inserts have a 1-char str source char */
+static int source_chars(PyObject *es, Py_UCS4 **buf, Py_ssize_t *len) {
+    const Py_ssize_t n = PyList_GET_SIZE(es);
+    Py_UCS4 *b = PyMem_Malloc(sizeof(Py_UCS4) * (n ? n : 1));
+    if (!b) {
+        PyErr_NoMemory();
+        return -1;
+    }
+    Py_ssize_t m = 0;
+    for (Py_ssize_t k = 0; k < n; ++k) {
+        PyObject *rec = PyList_GET_ITEM(es, k), *op = get(rec, K_OPERATION), *src, *ch;
+        if (!op || !PyUnicode_CheckExact(op)) goto bail;
+        if (eq(op, S_INSERT)) continue;
+        if (!(src = get(rec, K_SOURCE)) || !(ch = get(src, K_CHARACTER))) goto bail;
+        if (!PyUnicode_CheckExact(ch) || PyUnicode_GET_LENGTH(ch) != 1) goto bail;
+        b[m++] = PyUnicode_READ_CHAR(ch, 0);
+    }
+    *buf = b;
+    *len = m;
+    return 0;
+bail:
+    PyMem_Free(b);
+    return PyErr_Occurred() ? -1 : 1;
+}
+
+static PyObject *seq_from_es(PyObject *self, PyObject *es) {
+    if (!PyList_CheckExact(es)) NOT_IMPL();
+    Py_UCS4 *b;
+    Py_ssize_t m;
+    const int rc = source_chars(es, &b, &m);
+    if (rc < 0) return NULL;
+    if (rc > 0) NOT_IMPL();
+    PyObject *s = PyUnicode_FromKindAndData(PyUnicode_4BYTE_KIND, b, m);
+    PyMem_Free(b);
+    return s;
+}
+
+/* ------------------------------------------------------------------ patching */
+typedef struct {
+    Py_UCS4 *p;
+    Py_ssize_t len, cap;
+} ubuf;
+
+static int ub_reserve(ubuf *u, Py_ssize_t want) {
+    if (want <= u->cap) return 0;
+    Py_ssize_t cap = u->cap ? u->cap : 64;
+    while (cap < want) cap *= 2;
+    Py_UCS4 *q = PyMem_Realloc(u->p, sizeof(Py_UCS4) * cap);
+    if (!q) {
+        PyErr_NoMemory();
+        return -1;
+    }
+    u->p = q;
+    u->cap = cap;
+    return 0;
+}
+
+/* Python slice bound: s[:k] / s[k:] with k possibly negative or past the end */
+static Py_ssize_t norm(long long k, Py_ssize_t len) {
+    if (k < 0) k += len;
+    if (k < 0) k = 0;
+    if (k > len) k = len;
+    return (Py_ssize_t)k;
+}
+
+/* out = s[:a] + (ch or nothing) + s[b:], with a = norm(k), b = norm(k2) (b may be < a) */
+static int splice(ubuf *u, long long k, long long k2, int have_ch, Py_UCS4 ch) {
+    const Py_ssize_t a = norm(k, u->len), b = norm(k2, u->len);
+    const Py_ssize_t tail = u->len - b, nlen = a + (have_ch ? 1 : 0) + tail;
+    if (b >= a) {  /* in place: shift the tail */
+        if (ub_reserve(u, nlen)) return -1;
+        memmove(u->p + a + (have_ch ? 1 : 0), u->p + b, sizeof(Py_UCS4) * tail);
+        if (have_ch) u->p[a] = ch;
+        u->len = nlen;
+        return 0;
+    }
+    /* overlapping slices (negative index quirks): build a fresh buffer */
+    Py_UCS4 *q = PyMem_Malloc(sizeof(Py_UCS4) * (nlen ? nlen : 1));
+    if (!q) {
+        PyErr_NoMemory();
+        return -1;
+    }
+    memcpy(q, u->p, sizeof(Py_UCS4) * a);
+    if (have_ch) q[a] = ch;
+    memcpy(q + a + (have_ch ? 1 : 0), u->p + b, sizeof(Py_UCS4) * tail);
+    PyMem_Free(u->p);
+    u->p = q;
+    u->len = u->cap = nlen;
+    if (!nlen) u->cap = 1;
+    return 0;
+}
+
+static int long_of(PyObject *o, long long *v) {
+    if (!o || !PyLong_CheckExact(o)) return 1;
+    int ovf = 0;
+    *v = PyLong_AsLongLongAndOverflow(o, &ovf);
+    if (ovf || *v > (1LL << 40) || *v < -(1LL << 40)) return 1;
+    return 0;
+}
+
+typedef struct {
+    long long si, di;
+    Py_UCS4 sch, dch;  /* source char (non-inserts), destination char (updates / inserts) */
+    signed char op;    /* 0 insert, 1 delete, 2 update, -1 other (reads indices, applies nothing) */
+} prec;
+
+static PyObject *patching(PyObject *self, PyObject *args) {
+    PyObject *es, *s1;
+    if (!PyArg_ParseTuple(args, "OO", &es, &s1)) return NULL;
+    if (!PyList_CheckExact(es) || !PyUnicode_CheckExact(s1)) NOT_IMPL();
+    const Py_ssize_t n = PyList_GET_SIZE(es);
+    prec *pr = PyMem_Malloc(sizeof(prec) * (n ? n : 1));
+    if (!pr) return PyErr_NoMemory();
+    /* one pass: validate every record (the reference reads both indices of every record, the
+     * source character of every non-insert and the destination character of updates/inserts) */
+    Py_ssize_t olen = 0;
+    for (Py_ssize_t k = 0; k < n; ++k) {
+        PyObject *rec = PyList_GET_ITEM(es, k), *op = get(rec, K_OPERATION), *src, *dst, *ch;
+        if (!op || !PyUnicode_CheckExact(op) || !(src = get(rec, K_SOURCE)) || !(dst = get(rec, K_DESTINATION)) ||
+            long_of(get(src, K_INDEX), &pr[k].si) || long_of(get(dst, K_INDEX), &pr[k].di))
+            goto notimpl;
+        pr[k].op = eq(op, S_INSERT) ? 0 : eq(op, S_DELETE) ? 1 : eq(op, S_UPDATE) ? 2 : -1;
+        if (pr[k].op != 0) {
+            ch = get(src, K_CHARACTER);
+            if (!ch || !PyUnicode_CheckExact(ch) || PyUnicode_GET_LENGTH(ch) != 1) goto notimpl;
+            pr[k].sch = PyUnicode_READ_CHAR(ch, 0);
+            ++olen;
+        }
+        if (pr[k].op == 0 || pr[k].op == 2) {
+            ch = get(dst, K_CHARACTER);
+            if (!ch || !PyUnicode_CheckExact(ch) || PyUnicode_GET_LENGTH(ch) != 1) goto notimpl;
+            pr[k].dch = PyUnicode_READ_CHAR(ch, 0);
+        }
+    }
+    /* error code: str1 == generate_sequence_from_es(es) ? 0 : (len(str1) >= its length ? 1 : -1) */
+    const Py_ssize_t l1 = PyUnicode_GET_LENGTH(s1);
+    int err = 0;
+    if (l1 == olen) {
+        const int kind = PyUnicode_KIND(s1);
+        const void *data = PyUnicode_DATA(s1);
+        Py_ssize_t i = 0;
+        for (Py_ssize_t k = 0; k < n && !err; ++k)
+            if (pr[k].op != 0 && PyUnicode_READ(kind, data, i++) != pr[k].sch) err = 1;
+    } else {
+        err = l1 >= olen ? 1 : -1;
+    }
+    if (err == -1) {
+        PyMem_Free(pr);
+        return Py_BuildValue("(is)", -1, "");
+    }
+    ubuf u = {0, 0, 0};
+    if (ub_reserve(&u, l1 + n + 1) || !PyUnicode_AsUCS4(s1, u.p, u.cap, 0)) {
+        PyMem_Free(u.p);
+        PyMem_Free(pr);
+        return NULL;
+    }
+    u.len = l1;
+    long long removed = 0, inserted = 0;
+    for (Py_ssize_t k = 0; k < n; ++k) {
+        const long long at = pr[k].op == 0 ? pr[k].di : pr[k].si + removed + inserted;
+        int e = 0;
+        if (pr[k].op == 2) {
+            if (at >= 0 && at < u.len) u.p[at] = pr[k].dch; /* s[:at] + ch + s[at+1:] */
+            else e = splice(&u, at, at + 1, 1, pr[k].dch);
+        } else if (pr[k].op == 1) {
+            e = splice(&u, at, at + 1, 0, 0);
+            removed -= 1;
+        } else if (pr[k].op == 0) {
+            e = splice(&u, at, at, 1, pr[k].dch);
+            inserted += 1;
+        }
+        if (e) {
+            PyMem_Free(u.p);
+            PyMem_Free(pr);
+            return NULL;
+        }
+    }
+    PyMem_Free(pr);
+    PyObject *res = PyUnicode_FromKindAndData(PyUnicode_4BYTE_KIND, u.p, u.len);
+    PyMem_Free(u.p);
+    if (!res) return NULL;
+    return Py_BuildValue("(iN)", err, res);
+notimpl:
+    PyMem_Free(pr);
+    if (PyErr_Occurred()) return NULL;
+    Py_RETURN_NOTIMPLEMENTED;
+}
+
+/* ------------------------------------------------------------------ es_json */
+typedef struct {
+    char *p;
+    size_t len, cap;
+} cbuf;
+
+static int cb_put(cbuf *b, const char *s, size_t n) {
+    if (b->len + n > b->cap) {
+        size_t cap = b->cap ? b->cap : 4096;
+        while (cap < b->len + n) cap *= 2;
+        char *q = PyMem_Realloc(b->p, cap);
+        if (!q) {
+            PyErr_NoMemory();
+            return -1;
+        }
+        b->p = q;
+        b->cap = cap;
+    }
+    memcpy(b->p + b->len, s, n);
+    b->len += n;
+    return 0;
+}
+static int cb_str(cbuf *b, const char *s) { return cb_put(b, s, strlen(s)); }
+static int cb_nl(cbuf *b, int depth, int indent) {
+    static const char nl[] = "\n                                                                ";  /* 64 spaces */
+    const int n = depth * indent;  /* depth <= 4, indent <= 16 */
+    return cb_put(b, nl, (size_t)(1 + n));
+}
+
+/* a JSON string for a 1-char printable-ASCII str (json.dumps escapes '"' and '\\') */
+static int json_char(cbuf *b, PyObject *ch) {
+    if (!ch || !PyUnicode_CheckExact(ch) || PyUnicode_GET_LENGTH(ch) != 1) return 1;
+    const Py_UCS4 c = PyUnicode_READ_CHAR(ch, 0);
+    if (c < 0x20 || c > 0x7e) return 1;
+    char tmp[5] = {'"', 0, 0, 0, 0};
+    int k = 1;
+    if (c == '"' || c == '\\') tmp[k++] = '\\';
+    tmp[k++] = (char)c;
+    tmp[k++] = '"';
+    return cb_put(b, tmp, k) ? -1 : 0;
+}
+
+static int json_side(cbuf *b, PyObject *d, int depth, int indent) {
+    if (!d || !PyDict_CheckExact(d) || PyDict_GET_SIZE(d) != 2) return 1;
+    /* key order as stored: {'character', 'index'} (generate_es) or {'index', 'character'} (rev of a delete) */
+    PyObject *key, *val;
+    Py_ssize_t pos = 0;
+    if (cb_put(b, "{", 1)) return -1;
+    int first = 1;
+    while (PyDict_Next(d, &pos, &key, &val)) {
+        if (!first && cb_put(b, ",", 1)) return -1;
+        first = 0;
+        if (cb_nl(b, depth + 1, indent)) return -1;
+        if (eq(key, K_CHARACTER)) {
+            if (cb_str(b, "\"character\": ")) return -1;
+            const int r = json_char(b, val);
+            if (r) return r;
+        } else if (eq(key, K_INDEX)) {
+            long long v;
+            if (long_of(val, &v)) return 1;
+            char num[32];
+            snprintf(num, sizeof num, "\"index\": %lld", v);
+            if (cb_str(b, num)) return -1;
+        } else {
+            return 1;
+        }
+    }
+    if (cb_nl(b, depth, indent) || cb_put(b, "}", 1)) return -1;
+    return 0;
+}
+
+static PyObject *es_json(PyObject *self, PyObject *args) {
+    PyObject *es;
+    int indent = 4;
+    if (!PyArg_ParseTuple(args, "O|i", &es, &indent)) return NULL;
+    if (!PyList_CheckExact(es) || indent < 0 || indent > 16) NOT_IMPL();
+    cbuf b = {0, 0, 0};
+    int r = 0;
+    const Py_ssize_t n = PyList_GET_SIZE(es);
+    if ((r = cb_put(&b, "{", 1)) || (r = cb_nl(&b, 1, indent)) || (r = cb_str(&b, "\"edit_script\": ["))) goto done;
+    if (n == 0) {
+        if ((r = cb_str(&b, "]"))) goto done;
+    }
+    for (Py_ssize_t k = 0; k < n && !r; ++k) {
+        PyObject *rec = PyList_GET_ITEM(es, k);
+        if (!PyDict_CheckExact(rec) || PyDict_GET_SIZE(rec) != 3) {
+            r = 1;
+            break;
+        }
+        PyObject *op = get(rec, K_OPERATION), *src = get(rec, K_SOURCE), *dst = get(rec, K_DESTINATION);
+        if (!op || !src || !dst || !PyUnicode_CheckExact(op)) {
+            r = 1;
+            break;
+        }
+        const char *name = eq(op, S_INSERT)   ? "insert"
+                           : eq(op, S_DELETE) ? "delete"
+                           : eq(op, S_UPDATE) ? "update"
+                                                                  : NULL;
+        if (!name) {
+            r = 1;
+            break;
+        }
+        /* keys must be stored in the order operation, source, destination */
+        PyObject *key, *val;
+        Py_ssize_t pos = 0, i = 0;
+        PyObject *order[3] = {K_OPERATION, K_SOURCE, K_DESTINATION};
+        while (PyDict_Next(rec, &pos, &key, &val))
+            if (!eq(key, order[i++])) r = 1;
+        if (r) break;
+        if (k && (r = cb_put(&b, ",", 1))) break;
+        if ((r = cb_nl(&b, 2, indent)) || (r = cb_put(&b, "{", 1)) || (r = cb_nl(&b, 3, indent)) ||
+            (r = cb_str(&b, "\"operation\": \"")) || (r = cb_str(&b, name)) || (r = cb_str(&b, "\",")) ||
+            (r = cb_nl(&b, 3, indent)) || (r = cb_str(&b, "\"source\": ")) || (r = json_side(&b, src, 3, indent)) ||
+            (r = cb_put(&b, ",", 1)) || (r = cb_nl(&b, 3, indent)) || (r = cb_str(&b, "\"destination\": ")) ||
+            (r = json_side(&b, dst, 3, indent)) || (r = cb_nl(&b, 2, indent)) || (r = cb_put(&b, "}", 1)))
+            break;
+    }
+    if (!r && n && ((r = cb_nl(&b, 1, indent)) || (r = cb_put(&b, "]", 1)))) goto done;
+    if (!r) {
+        if ((r = cb_nl(&b, 0, indent)) || (r = cb_put(&b, "}", 1))) goto done;
+    }
+done:;
+    PyObject *res = NULL;
+    if (r == 0) res = PyUnicode_DecodeASCII(b.p, (Py_ssize_t)b.len, NULL);
+    PyMem_Free(b.p);
+    if (r < 0 || (r == 0 && !res)) return NULL;
+    if (r > 0) {
+        if (PyErr_Occurred()) return NULL;
+        Py_RETURN_NOTIMPLEMENTED;
+    }
+    return res;
+}
+
+/* ------------------------------------------------------------------ module */
+static PyMethodDef methods[] = {
+    {"es_from_ops", es_from_ops, METH_VARARGS, "generate_es over a canonical op sequence"},
+    {"rev_es", rev_es, METH_O, "generate_rev_es"},
+    {"seq_from_es", seq_from_es, METH_O, "generate_sequence_from_es"},
+    {"patching", patching, METH_VARARGS, "patching(es, str1) -> (error_code, str)"},
+    {"es_json", es_json, METH_VARARGS, "json.dumps({'edit_script': es}, indent=indent)"},
+    {NULL, NULL, 0, NULL},
+};
+
+static struct PyModuleDef moddef = {PyModuleDef_HEAD_INIT, "_sedhost", NULL, -1, methods};
+
+PyMODINIT_FUNC PyInit__sedhost(void) {
+    K_OPERATION = PyUnicode_InternFromString("operation");
+    K_SOURCE = PyUnicode_InternFromString("source");
+    K_DESTINATION = PyUnicode_InternFromString("destination");
+    K_CHARACTER = PyUnicode_InternFromString("character");
+    K_INDEX = PyUnicode_InternFromString("index");
+    S_INSERT = PyUnicode_InternFromString("insert");
+    S_DELETE = PyUnicode_InternFromString("delete");
+    S_UPDATE = PyUnicode_InternFromString("update");
+    if (!K_OPERATION || !K_SOURCE || !K_DESTINATION || !K_CHARACTER || !K_INDEX || !S_INSERT || !S_DELETE ||
+        !S_UPDATE)
+        return NULL;
+    return PyModule_Create(&moddef);
+}
