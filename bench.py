@@ -58,6 +58,9 @@ WORKLOADS = {
     "c5": (500, 0, 0, "costs.json",
            "config 5 (synthetic): all-vs-all wf_score over 500 ACGU sequences of length U[24,32], costs.json, "
            "250000 ordered pairs, distance only"),
+    "c5n": (500, 0, 0, "costs.json",
+            "config 5 with N (synthetic): all-vs-all wf_score over 500 sequences of length U[24,32], ~1% N "
+            "(fp64 path), costs.json, 250000 ordered pairs, distance only"),
 }
 
 
@@ -76,11 +79,15 @@ def gen_codes(pair_ids, n, m, iupac=False):
     return A, B
 
 
-def gen_all_vs_all(nseq, lo=24, hi=32):
-    """Config 5 stand-in: nseq synthetic ACGU sequences, every ordered pair (query = str1)."""
+def gen_all_vs_all(nseq, lo=24, hi=32, n_rate=0.0):
+    """Config 5 stand-in: nseq synthetic ACGU sequences, every ordered pair (query = str1).
+    n_rate > 0: that fraction of positions becomes N (code 4), which forces the fp64 path."""
     ids = np.arange(nseq, dtype=np.uint64)
     ln = synth.lengths(ids, lo, hi)
     seqs = [synth.pair_codes([i], int(l), 0)[0] for i, l in zip(ids, ln)]
+    if n_rate > 0:
+        rng = np.random.default_rng(20261015)
+        seqs = [np.where(rng.random(len(q)) < n_rate, 4, q).astype(np.uint8) for q in seqs]
     return [seqs[a] for a in range(nseq) for _ in range(nseq)], [seqs[b] for _ in range(nseq) for b in range(nseq)]
 
 
@@ -142,6 +149,7 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run DP and traceback back to back on one stream (no overlap across steps)")
     ap.add_argument("--rows-per-lane", type=int, default=0)
+    ap.add_argument("--no-lane", action="store_true", help="route short pairs to the wave kernels too (A/B)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_dp_i32_c4.json"),
@@ -174,17 +182,17 @@ def main():
     P, n, m, costs_file, desc = WORKLOADS[args.workload]
     if args.pairs:
         P = args.pairs
-    want_script = not args.no_script and args.workload != "c5"
+    want_script = not args.no_script and args.workload not in ("c5", "c5n")
     iupac = args.workload == "iupac"
     with open(os.path.join(REPO, "tests", "golden", costs_file)) as f:
         table = json.load(f)
-    alpha = synth.IUPAC if iupac else synth.ALPHABET
+    alpha = synth.IUPAC if iupac else (synth.ALPHABET + "N" if args.workload == "c5n" else synth.ALPHABET)
     plan = sedcost.build_plan(table, [alpha], [alpha])
     t0 = time.perf_counter()
-    if args.workload == "c5":
+    if args.workload in ("c5", "c5n"):
         import sedshard
         lo, hi = sedshard.shard_range(P, world, rank)  # query rows of this rank
-        qa, qb = gen_all_vs_all(P)
+        qa, qb = gen_all_vs_all(P, n_rate=0.01 if args.workload == "c5n" else 0.0)
         qa, qb = qa[lo * P:hi * P], qb[lo * P:hi * P]
         packed = sedgpu.PackedPairs(qa, qb)
         A = B = None
@@ -198,6 +206,8 @@ def main():
     ctx = sedgpu.Context(local)
     if args.rows_per_lane:
         ctx.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, args.rows_per_lane)
+    if args.no_lane:
+        ctx.set_option(sedgpu.SED_OPT_LANE, 2)
     ctx.set_costs(plan)
     t0 = time.perf_counter()
     pipeline = want_script and not args.no_pipeline
@@ -296,7 +306,8 @@ def main():
     rate = cells / (dp_avg * 1e-3)
     nl = batch.lane_pairs
     if batch.mode != "i32":
-        kname = "sed_wf_f64_kernel"
+        kname = "sed_lane_f64_kernel" if nl == P else ("sed_wf_f64_kernel" if nl == 0 else
+                                                       "sed_wf_f64_kernel+sed_lane_f64_kernel")
     else:
         kname = "sed_lane_i32_kernel" if nl == P else ("sed_wf_i32_kernel" if nl == 0 else
                                                        "sed_wf_i32_kernel+sed_lane_i32_kernel")

@@ -468,6 +468,7 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
     const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (pair >= npairs) return;
     const sed_pair_desc d = pd[pair];
+    if (d.lane) return;  // short str2, distance only: sed_lane.hip
     const int n = d.n, m = d.m;
     if constexpr (FULL) {  // border cells: row 0 (insert edges) and column 0 (delete edges)
         for (int j = lane; j <= m; j += 64) {

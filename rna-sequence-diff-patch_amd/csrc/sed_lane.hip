@@ -1,4 +1,5 @@
-// sed_lane.hip — lane-per-pair integer kernel for short str2 (m <= SED_LANE_MAXM).
+// sed_lane.hip — lane-per-pair kernels for short str2 (m <= SED_LANE_MAXM): integer keys
+// (distance, length, canonical script) and fp64 distance-only.
 //
 // Config 5 (all-vs-all over ~24-32 nt piRNAs, IRMethods.py:435-440 / 443-477) and the GUI's
 // short pairs: a 64-lane wave per pair (sed_kernels.hip) would leave most lanes idle and spend
@@ -131,7 +132,75 @@ __global__ __launch_bounds__(256) void sed_lane_i32_kernel(const sed_pair_desc *
     }
 }
 
+// fp64 distance-only variant (SED_MODE_F64 = "simple typing", SED_NO_LEN): short pairs whose
+// alphabet or costs rule out the integer keys (IUPAC codes, N in piRNA data; config 5 with N).
+// Cells follow the reference exactly: borders j*insert and i*delete are products
+// (StringEditDistance.py:146-182), each candidate is one fp64 add, the value is the minimum
+// (ties have equal values; in this mode a value is a Python int exactly when it is 0).
+// The K x K cost table sits in LDS; a lane keeps per-column byte offsets into it.
+template <int MM>
+__global__ __launch_bounds__(256) void sed_lane_f64_kernel(const sed_pair_desc *__restrict__ pd,
+                                                           const int32_t *__restrict__ idx, int nidx,
+                                                           const uint8_t *__restrict__ seqa,
+                                                           const uint8_t *__restrict__ seqb,
+                                                           sed_result *__restrict__ res,
+                                                           const double *__restrict__ gtab, double ins, double del,
+                                                           int K) {
+    __shared__ double tab[SED_MAX_K * SED_MAX_K];
+    for (int e = threadIdx.x; e < K * K; e += blockDim.x) tab[e] = gtab[2 * e];
+    __syncthreads();
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nidx) return;
+    const int pair = idx[t];
+    const sed_pair_desc d = pd[pair];
+    const int n = d.n, m = d.m;  // host guarantees 1 <= n <= SED_LANE_MAXN, 1 <= m <= MM
+    const uint8_t *pa = seqa + d.a_off, *pb = seqb + d.b_off;
+    uint32_t col[MM];  // byte offset of cost(., b_j) within a table row
+    double V[MM + 1];
+#pragma unroll
+    for (int j = 0; j < MM; ++j) col[j] = (j < m ? (uint32_t)pb[j] : 0u) * 8u;
+#pragma unroll
+    for (int j = 0; j <= MM; ++j) V[j] = (double)j * ins;
+    const char *tb8 = reinterpret_cast<const char *>(tab);
+    uint32_t a_next = pa[0];
+    for (int i = 0; i < n; ++i) {
+        const char *row = tb8 + a_next * (uint32_t)K * 8u;
+        if (i + 1 < n) a_next = pa[i + 1];  // in flight during this row
+        double dg = V[0] + *reinterpret_cast<const double *>(row + col[0]);
+        V[0] = (double)(i + 1) * del;
+        double left = V[0];
+#pragma unroll
+        for (int j = 1; j <= MM; ++j) {
+            const double up = V[j];
+            const double cdel = up + del;
+            const double dnext = j < MM ? up + *reinterpret_cast<const double *>(row + col[j]) : 0.0;
+            const double v = fmin(fmin(left + ins, cdel), dg);
+            dg = dnext;
+            V[j] = v;
+            left = v;
+        }
+    }
+    double D = V[1];
+#pragma unroll
+    for (int j = 2; j <= MM; ++j) D = (j == m) ? V[j] : D;
+    sed_result r;
+    r.dist = D;
+    r.len = -1;
+    r.is_int = (D == 0.0);
+    r.err = 0;
+    r.pad[0] = r.pad[1] = 0;
+    res[pair] = r;
+}
+
 }  // namespace
+
+hipError_t sed_launch_lane_f64(const sed_launch &L, const int32_t *idx, int nidx, const double *gtab, double ins,
+                               double del, int K) {
+    if (nidx <= 0) return hipSuccess;
+    hipLaunchKernelGGL((sed_lane_f64_kernel<SED_LANE_MAXM>), dim3((nidx + 255) / 256), dim3(256), 0, L.stream, L.pd,
+                       idx, nidx, (const uint8_t *)L.seqa, (const uint8_t *)L.seqb, L.res, gtab, ins, del, K);
+    return hipGetLastError();
+}
 
 hipError_t sed_launch_lane_i32(const sed_launch &L, const int32_t *idx, int nidx, const sed_i32_params &prm,
                                bool len) {

@@ -251,7 +251,9 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     b->pd.assign(npairs, sed_pair_desc{});
     std::vector<int2> tasks;
     std::vector<int32_t> lane_idx;
-    const bool use_lane = mode == SED_MODE_I32 && !split && c->opt_lane != 2;
+    // lane-per-pair kernels: integer keys (any flags), or fp64 distance-only in "simple typing" mode
+    const bool use_lane = !split && c->opt_lane != 2 &&
+                          (mode == SED_MODE_I32 || (mode == SED_MODE_F64 && !want_tb && (flags & SED_NO_LEN)));
     uint64_t aw = 0, bw = 0, tbw = 0, bndw = 0, opw = 0, progw = 0;
     const bool packed = (mode == SED_MODE_I32);
     double cells = 0, in_bytes = 0, tb_bytes = 0;
@@ -440,8 +442,14 @@ int run_batch(sed_batch *b) {
             e = sed_launch_f64(L, (const double *)c->gtab.p, b->fp, b->mode == SED_MODE_F64_TYPED);
         if (e != hipSuccess) return c->hipfail(e, "DP kernel launch");
     }
-    if (b->nlane > 0 && (e = sed_launch_lane_i32(L, (const int32_t *)b->d_lane.p, b->nlane, b->ip, len)) != hipSuccess)
-        return c->hipfail(e, "lane kernel launch");
+    if (b->nlane > 0) {
+        if (b->mode == SED_MODE_I32)
+            e = sed_launch_lane_i32(L, (const int32_t *)b->d_lane.p, b->nlane, b->ip, len);
+        else
+            e = sed_launch_lane_f64(L, (const int32_t *)b->d_lane.p, b->nlane, (const double *)c->gtab.p, c->ins,
+                                    c->del, c->K);
+        if (e != hipSuccess) return c->hipfail(e, "lane kernel launch");
+    }
     if ((e = hipEventRecord(lg[1], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
     if (want_tb) {
         if (ts != c->stream && (e = hipStreamWaitEvent(ts, lg[1], 0)) != hipSuccess) return c->hipfail(e, "stream wait");
