@@ -150,6 +150,8 @@ def main():
                     help="run DP and traceback back to back on one stream (no overlap across steps)")
     ap.add_argument("--rows-per-lane", type=int, default=0)
     ap.add_argument("--no-lane", action="store_true", help="route short pairs to the wave kernels too (A/B)")
+    ap.add_argument("--chain", type=int, default=0,
+                    help="SED_OPT_CHAIN: 0 auto, 1 force, 2 off, L>=3 force with chains of L pairs (A/B)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_dp_i32_c4.json"),
@@ -208,6 +210,8 @@ def main():
         ctx.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, args.rows_per_lane)
     if args.no_lane:
         ctx.set_option(sedgpu.SED_OPT_LANE, 2)
+    if args.chain:
+        ctx.set_option(sedgpu.SED_OPT_CHAIN, args.chain)
     ctx.set_costs(plan)
     t0 = time.perf_counter()
     pipeline = want_script and not args.no_pipeline
@@ -317,7 +321,7 @@ def main():
         "vs_baseline": None, "dtype": "u32" if batch.mode == "i32" else "f64", "data": "synthetic",
         "config": {"workload": desc, "pairs_per_gpu": P, "n": n, "m": m, "costs": costs_file,
                    "script": want_script, "pipeline": pipeline, "mode": batch.mode,
-                   "rows_per_lane": batch.rows_per_lane, "lane_pairs": nl,
+                   "rows_per_lane": batch.rows_per_lane, "lane_pairs": nl, "chains": batch.chains,
                    "parallelism": "dp%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -62,10 +62,18 @@ struct sed_launch {
     const int2 *tasks;  // SPLIT mode: (pair, stripe) per workgroup, else nullptr
     uint32_t *prog;     // SPLIT mode: per-stripe published-column counters (zeroed before each run)
     int ntasks;         // 0 -> one wave per pair
+    // CHAIN mode: chain c runs pairs chain_pairs[chain_off[c] .. chain_off[c+1]) back to back;
+    // with chain_counter set, nchains persistent waves take list entries [0, chain_list) from it
+    const int32_t *chain_pairs, *chain_off;
+    int nchains;
+    uint32_t *chain_counter;
+    int chain_list;
 };
 
 // len = false (distance only, SED_NO_LEN): keys without the op-count field, out len = -1.
 hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm, bool len);
+// CHAIN mode (single-stripe pairs, R in {4, 8, 16}): one wave per chain of pairs.
+hipError_t sed_launch_i32_chain(const sed_launch &L, const sed_i32_params &prm, bool len);
 hipError_t sed_launch_f64(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed);
 hipError_t sed_launch_f64_full(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed,
                                const sed_full_out &fo);

@@ -353,6 +353,251 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
 }
 
 // ---------------------------------------------------------------------------
+// CHAIN mode (integer keys, single-stripe pairs: n <= 64R).  One wave runs a chain of pairs
+// back to back so that a pair's 63-step wavefront ramp overlaps the previous pair's drain.
+// Pair q of the chain owns global steps [T_q, T_q + S_q) for lane 0, S_q = m_q rounded up to
+// 64 (whole LDS chunks); lane t runs it at [T_q + t, T_q + S_q + t).  Lane t therefore
+// switches pairs right after global step T_q + t - 1: its V / cost rows / diagonal are set
+// to the new pair's column-0 state with per-lane selects (rows are the same for every pair
+// of the chain: row0 = 64R * 0 + t*R, so the column-0 borders are per-lane constants).
+// The cell above a lane's band keeps arriving by DPP from lane t-1, which switched one step
+// earlier, and the str2 selectors flow from lane 0 as in the stripe kernel.  The first pair
+// starts with the virtual-column ramp.  Per-pair traceback layout, results and captures are
+// exactly the stripe kernel's (one stripe), so the traceback kernel is shared.
+// ---------------------------------------------------------------------------
+struct chain_pair_state {
+    int pair, m, T, S, end;            // end: first global step after its last real column (T + m + 63)
+    int cap_step, cap_lane, cap_row;   // the sink cell (n, m)
+    uint64_t tb_off;
+    int sg;                            // traceback groups allocated per stripe
+    const uint32_t *pb;                // str2 codes
+};
+
+template <int R>
+__device__ __forceinline__ chain_pair_state chain_load(const sed_pair_desc *__restrict__ pd,
+                                                       const uint32_t *__restrict__ seqb, int pair, int T) {
+    constexpr int G = Grp<R>::G;
+    const sed_pair_desc d = pd[pair];
+    chain_pair_state c;
+    c.pair = pair;
+    c.m = d.m;
+    c.T = T;
+    c.S = (d.m + 63) & ~63;
+    c.end = T + d.m + 63;
+    const int wsink = d.n - 1;
+    c.cap_lane = wsink / R;
+    c.cap_row = wsink % R;
+    c.cap_step = T + d.m - 1 + c.cap_lane;
+    c.tb_off = d.tb_off;
+    c.sg = (d.m + 63 + G - 1) / G;
+    c.pb = seqb + d.b_off;
+    return c;
+}
+
+// One group of G steps.  SW: lanes switch from the previous pair to the pair starting at
+// `Tcur` after the step at which lane == s + 1 - Tcur.  GEN (rare groups: the first pair's
+// virtual-column ramp, sink captures of the previous (A) and current (B) pair, and any switch
+// in those groups) additionally masks the insert constant (ramp != 0) and captures.
+template <int R, bool TB, bool LEN, bool SW, bool GEN>
+__device__ __forceinline__ void i32_chain_group(uint32_t (&V)[R], uint32_t (&cv)[R], const uint32_t (&cvn)[R],
+                                                const uint32_t (&Vb)[R], const uint32_t tpb, uint32_t &top_prev,
+                                                uint32_t &bottom, uint32_t &selv, const uint2 *__restrict__ lch,
+                                                uint32_t &outc, uint32_t (&W)[4], const int s0, const int lane,
+                                                const uint32_t kins, const uint32_t kdel, const int Tcur,
+                                                const bool ramp, const int csA, const int clA, const int crA,
+                                                uint32_t &capA, const int csB, const int clB, const int crB,
+                                                uint32_t &capB) {
+    constexpr int G = Grp<R>::G;
+    uint32_t kin = kins, kde = kdel;
+    asm volatile("" : "+s"(kin), "+s"(kde));  // see i32_group: keep sibling variants from hoisting V+kins
+    uint2 tv[G];
+    const uint2 *lp = lch + (s0 & 63);
+#pragma unroll
+    for (int u = 0; u < G; ++u) tv[u] = lp[u];
+    uint32_t tch = 0, sch = 0;
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+        const int s = s0 + u;
+        uint32_t ki = kin;
+        if constexpr (GEN) ki = ramp ? (kin & ~(uint32_t)((s - lane) >> 31)) : kin;
+        i32_step<R, TB, LEN>(V, cv, top_prev, bottom, selv, tch, sch, tv[u], outc, W, u, ki, kde);
+        if constexpr (GEN) {
+            const bool hA = (s == csA) && (lane == clA), hB = (s == csB) && (lane == clB);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                capA = (hA && r == crA) ? V[r] : capA;
+                capB = (hB && r == crB) ? V[r] : capB;
+            }
+        }
+        if constexpr (SW || GEN) {
+            const bool sw = (lane == s + 1 - Tcur);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                V[r] = sw ? Vb[r] : V[r];
+                cv[r] = sw ? cvn[r] : cv[r];
+            }
+            top_prev = sw ? tpb : top_prev;
+        }
+    }
+}
+
+template <int R, bool TB, bool LEN>
+__device__ __forceinline__ void chain_store_result(sed_result *__restrict__ res, int pair, uint32_t cap) {
+    const uint32_t D = cap >> 16;
+    res[pair].dist = (double)D;
+    res[pair].len = LEN ? (int32_t)((cap >> 2) & 0x3FFFu) : -1;
+    res[pair].is_int = (D == 0);
+}
+
+// the chain kernel also holds the next pair's cost rows and the column-0 constants
+template <int R> struct ChainWaves { static constexpr int value = R >= 16 ? 4 : 5; };
+
+template <int R, bool TB, bool LEN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainWaves<R>::value))) void
+sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restrict__ chain_pairs,
+                        const int32_t *__restrict__ chain_off, int nchains, uint32_t *__restrict__ counter,
+                        int nlist, const uint32_t *__restrict__ seqa, const uint32_t *__restrict__ seqb,
+                        uint32_t *__restrict__ tb, sed_result *__restrict__ res, sed_i32_params prm) {
+    constexpr int G = Grp<R>::G;
+    const int lane = threadIdx.x & 63;
+    const int chain = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (chain >= nchains) return;
+    // Static chains: list entries [chain_off[c], chain_off[c+1]).  Dynamic (counter != null):
+    // persistent waves take the next list entry from a device counter whenever lane 0 reaches
+    // the end of a pair, so every wave stays busy until the list is exhausted.
+    auto grab = [&]() -> int {
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(counter, 1u);
+        return (int)__builtin_amdgcn_readfirstlane(v);
+    };
+    int c0, c1;
+    if (counter) {
+        c0 = grab();
+        c1 = nlist;
+        if (c0 >= nlist) return;
+    } else {
+        c0 = chain_off[chain];
+        c1 = chain_off[chain + 1];
+    }
+    const uint32_t kins = LEN ? prm.kins : (prm.ins << 16), kdel = LEN ? prm.kdel : (prm.del << 16);
+    __shared__ uint2 lds_chunk[4][64];
+    uint2 *lch = lds_chunk[threadIdx.x >> 6];
+    const int row0 = lane * R;
+
+    // per-lane constants: column-0 state of this lane's rows (the same for every pair)
+    uint32_t Vb[R], tpb;
+    i32_reset<R>(Vb, tpb, row0, prm.del);
+    auto rows_of = [&](int pair, uint32_t (&out)[R]) {
+        const uint32_t *pa = seqa + pd[pair].a_off;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int ri = row0 + r;
+            const uint32_t a = (pa[ri >> 4] >> ((ri & 15) * 2)) & 3u;
+            out[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
+        }
+    };
+    auto chunk_of = [&](const chain_pair_state &c, int cl) -> uint2 {  // lane 0's inputs, local chunk cl
+        const int j = 64 * cl + lane;
+        const uint32_t b = (c.pb[j >> 4] >> ((j & 15) * 2)) & 3u;
+        return make_uint2(i32_border((uint32_t)(j + 1), prm.ins), 0x0C000100u | ((4u + b) << 16));
+    };
+
+    chain_pair_state cur = chain_load<R>(pd, seqb, chain_pairs[c0], 0), prv = cur;
+    bool have_cur = true, have_prv = false;
+    int q = c0;
+    uint32_t cv[R], cvn[R], V[R];
+    rows_of(cur.pair, cv);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        V[r] = Vb[r];
+        cvn[r] = cv[r];
+    }
+    uint32_t top_prev = tpb, bottom = V[R - 1], selv = SED_SEL_SENT, outc = 0, capA = 0, capB = 0;
+    uint32_t W[4] = {0, 0, 0, 0};
+    lch[lane] = chunk_of(cur, 0);
+
+    for (int s0 = 0;; s0 += 64) {
+        // prefetch the next chunk's lane-0 inputs (this pair's next chunk, or the next pair's first)
+        uint2 nx = make_uint2(0, 0);
+        chain_pair_state nxt = cur;
+        bool have_nxt = false;
+        if (have_cur && s0 + 64 < cur.T + cur.S) {
+            nx = chunk_of(cur, (s0 + 64 - cur.T) >> 6);
+        } else if (have_cur) {
+            const int qn = counter ? grab() : q + 1;
+            if (qn < c1) {
+                nxt = chain_load<R>(pd, seqb, chain_pairs[qn], cur.T + cur.S);
+                have_nxt = true;
+                nx = chunk_of(nxt, 0);
+                q = qn - 1;  // advanced below when nxt becomes cur
+            }
+        }
+        for (int g = 0; g < 64 / G; ++g) {
+            const int s = s0 + g * G;
+            const bool win = have_cur && have_prv && s < cur.T + 64;  // lanes switch from prv to cur
+            const bool ramp = have_cur && !have_prv && s < 63;       // first pair: virtual columns
+            const bool capg = (have_prv && prv.cap_step >= s && prv.cap_step < s + G) ||
+                              (have_cur && cur.cap_step >= s && cur.cap_step < s + G);
+            // wave-uniform: which body; Tsw never matches a lane outside a switch window
+            const int Tsw = win ? cur.T : -(1 << 30);
+#define SED_CGROUP(SW, GEN)                                                                               \
+    i32_chain_group<R, TB, LEN, SW, GEN>(V, cv, cvn, Vb, tpb, top_prev, bottom, selv, lch, outc, W, s, lane, kins, \
+                                         kdel, Tsw, ramp, prv.cap_step, prv.cap_lane, prv.cap_row, capA,          \
+                                         cur.cap_step, cur.cap_lane, cur.cap_row, capB)
+            if (capg || ramp) SED_CGROUP(false, true);
+            else if (win) SED_CGROUP(true, false);
+            else SED_CGROUP(false, false);
+#undef SED_CGROUP
+            if constexpr (TB) {
+                // a lane's 16 bytes go to the pair it worked on; in the switch window a group holds
+                // steps of both pairs, so it is stored to both (each slot's unused part is never read).
+                // Uniform base + 32-bit lane offset: saddr stores, no per-lane 64-bit address kept live.
+                uint32_t lo = (uint32_t)lane * 16u;
+                asm volatile("" : "+v"(lo));
+                if (have_cur && s >= cur.T) {
+                    char *gp = reinterpret_cast<char *>(tb + cur.tb_off + (uint64_t)((s - cur.T) / G) * 256u);
+                    *reinterpret_cast<uint4 *>(gp + lo) = make_uint4(W[0], W[1], W[2], W[3]);
+                }
+                // lanes still on prv: the switch window, or the final drain after the chain's last pair
+                if (have_prv && s < (have_cur ? cur.T + 64 : prv.end) && (s - prv.T) / G < prv.sg) {
+                    char *gp = reinterpret_cast<char *>(tb + prv.tb_off + (uint64_t)((s - prv.T) / G) * 256u);
+                    *reinterpret_cast<uint4 *>(gp + lo) = make_uint4(W[0], W[1], W[2], W[3]);
+                }
+            }
+            if (capg) {
+                if (have_prv && prv.cap_step >= s && prv.cap_step < s + G && lane == prv.cap_lane)
+                    chain_store_result<R, TB, LEN>(res, prv.pair, capA);
+                if (have_cur && cur.cap_step >= s && cur.cap_step < s + G && lane == cur.cap_lane)
+                    chain_store_result<R, TB, LEN>(res, cur.pair, capB);
+            }
+        }
+        lch[lane] = nx;  // after the chunk's last LDS read (in order)
+        const int s1 = s0 + 64;
+        if (have_cur && s1 == cur.T + cur.S) {  // lane 0 is done with cur: it becomes the draining pair
+            prv = cur;
+            have_prv = true;
+            capA = capB;
+            if (have_nxt) {
+                cur = nxt;
+                ++q;
+                rows_of(cur.pair, cvn);
+                // lane 0 switches before the next pair's first step
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    V[r] = lane == 0 ? Vb[r] : V[r];
+                    cv[r] = lane == 0 ? cvn[r] : cv[r];
+                }
+                top_prev = lane == 0 ? tpb : top_prev;
+            } else {
+                have_cur = false;
+            }
+        }
+        if (have_prv && s1 >= prv.end && (!have_cur || s1 >= cur.T + 64)) have_prv = false;  // drained
+        if (!have_cur && !have_prv) break;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // fp64 kernel (general costs).  State per row: D (fp64), Lk = L << 2,
 // optional int-typing bit T (TYPED).  Cost table in LDS:
 //   tab[a*K + b] = {cost value, is-int flag}
@@ -715,6 +960,27 @@ static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
                            prm);
     }
     return hipGetLastError();
+}
+
+template <int R, bool TB, bool LEN>
+static hipError_t launch_chain_R(const sed_launch &L, const sed_i32_params &prm) {
+    hipLaunchKernelGGL((sed_wf_i32_chain_kernel<R, TB, LEN>), dim3((L.nchains + 3) / 4), dim3(256), 0, L.stream, L.pd,
+                       L.chain_pairs, L.chain_off, L.nchains, L.chain_counter, L.chain_list,
+                       (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.res, prm);
+    return hipGetLastError();
+}
+
+hipError_t sed_launch_i32_chain(const sed_launch &L, const sed_i32_params &prm, bool len) {
+    const bool tb = L.tb != nullptr;
+    switch (L.R) {
+#define CASE(RR)                                                                                   \
+    case RR:                                                                                       \
+        return tb ? launch_chain_R<RR, true, true>(L, prm)                                         \
+                  : (len ? launch_chain_R<RR, false, true>(L, prm) : launch_chain_R<RR, false, false>(L, prm));
+        CASE(4) CASE(8) CASE(16)
+#undef CASE
+    default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm, bool len) {

@@ -57,7 +57,7 @@ struct sed_ctx {
     int ins_int = 0, del_int = 0;
     DevBuf gtab;  // fp64 kernel table: per entry {value bits, is-int flag}
     // options
-    int opt_mode = 0, opt_R = 0, opt_split = 0, opt_lane = 0;
+    int opt_mode = 0, opt_R = 0, opt_split = 0, opt_lane = 0, opt_chain = 0;
     DevBuf selftest;
     sed_batch *scratch = nullptr;
 
@@ -84,9 +84,12 @@ struct sed_batch {
     std::vector<int32_t> n, m;
     uint64_t tb_words = 0, bnd_words = 0, ops_words = 0;
     double cells = 0, algo_bytes = 0;
-    DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops, d_tasks, d_prog, d_lane;
+    DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops, d_tasks, d_prog, d_lane, d_chain;
     bool split = false;
     int nlane = 0, nwave = 0;  // pairs on the lane-per-pair kernel / on the wave kernels
+    int nchains = 0;           // CHAIN mode: wave pairs run as nchains back-to-back chains (0 = off)
+    size_t chain_npairs = 0;   // d_chain = [chain_pairs (chain_npairs) | chain_off (nchains + 1) | counter]
+    bool chain_dyn = false;    // persistent waves + device counter instead of static chains
     int ntasks = 0;
     uint64_t prog_words = 0;
     // SED_PIPELINE: run k uses traceback/result buffer k&1, so the traceback of
@@ -108,7 +111,7 @@ struct sed_batch {
     int cur() const { return (int)((runs - 1) & (nbuf - 1)); }
     ~sed_batch() {
         d_pd.release(); d_seqa.release(); d_seqb.release(); d_bnd.release(); d_ops.release();
-        d_tasks.release(); d_prog.release(); d_lane.release();
+        d_tasks.release(); d_prog.release(); d_lane.release(); d_chain.release();
         for (int i = 0; i < 2; ++i) {
             d_tb[i].release();
             d_res[i].release();
@@ -237,7 +240,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // batches too small to fill the GPU with one wave per pair (config 2, GUI calls).
     bool split = false;
     if (mode == SED_MODE_I32 && c->opt_split != 2) {
-        split = c->opt_split == 1 || (npairs <= 256 && max_n > 256);
+        split = c->opt_split == 1 || (npairs <= 256 && max_n > 256 && c->opt_chain != 1 && c->opt_chain < 3);
         if (split && !c->opt_R) R = 4;
         if (split && R != 4 && R != 8 && R != 16 && R != 32) split = false;
     }
@@ -302,6 +305,43 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     b->bnd_words = bndw;
     b->nlane = (int)lane_idx.size();
     b->nwave = npairs - b->nlane;
+
+    // ---- CHAIN mode (integer keys): single-stripe wave pairs run back to back, one chain per
+    // wave, so each pair's 63-step ramp overlaps the previous pair's drain (sed_kernels.hip) ----
+    std::vector<int32_t> chain_pairs, chain_off;
+    b->nchains = 0;
+    b->chain_dyn = false;
+    if (mode == SED_MODE_I32 && !split && c->opt_chain != 2 && (R == 4 || R == 8) && b->nwave > 0) {
+        const int resident = 1024 * 5;  // SIMDs x the chain kernel's waves per SIMD
+        bool ok = true;
+        for (int p = 0; p < npairs && ok; ++p)
+            if (!b->pd[p].lane && (len_a[p] < 1 || len_a[p] > ROWS || len_b[p] < 1)) ok = false;
+        if (ok && c->opt_chain >= 3) {  // static chains of opt_chain pairs (tests, A/B)
+            const int L = c->opt_chain;
+            double total = 0;
+            for (int p = 0; p < npairs; ++p)
+                if (!b->pd[p].lane) total += (double)((len_b[p] + 63) & ~63);
+            const int nch = std::max(1, (b->nwave + L - 1) / L);
+            const double target = total / nch;
+            double acc = 0;
+            chain_off.push_back(0);
+            for (int p = 0; p < npairs; ++p) {
+                if (b->pd[p].lane) continue;
+                chain_pairs.push_back(p);
+                acc += (double)((len_b[p] + 63) & ~63);
+                if (acc >= target * (double)chain_off.size() && (int)chain_off.size() < nch)
+                    chain_off.push_back((int32_t)chain_pairs.size());
+            }
+            if (chain_off.back() != (int32_t)chain_pairs.size()) chain_off.push_back((int32_t)chain_pairs.size());
+            b->nchains = (int)chain_off.size() - 1;
+        } else if (ok && (c->opt_chain == 1 || b->nwave >= 2 * resident)) {
+            // dynamic: `resident` persistent waves take the next pair from a device counter
+            for (int p = 0; p < npairs; ++p)
+                if (!b->pd[p].lane) chain_pairs.push_back(p);
+            b->nchains = std::min(b->nwave, resident);
+            b->chain_dyn = true;
+        }
+    }
     b->ntasks = (int)tasks.size();
     b->prog_words = progw;
     b->ops_words = opw;
@@ -335,7 +375,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
                    b->d_bnd.reserve(4 * std::max<uint64_t>(1, bndw)) &&
                    b->d_tasks.reserve(sizeof(int2) * std::max<size_t>(1, tasks.size())) &&
                    b->d_prog.reserve(4 * std::max<uint64_t>(1, progw)) &&
-                   b->d_lane.reserve(4 * std::max<size_t>(1, lane_idx.size()));
+                   b->d_lane.reserve(4 * std::max<size_t>(1, lane_idx.size())) &&
+                   b->d_chain.reserve(4 * (chain_pairs.size() + chain_off.size() + 2));
     for (int i = 0; i < b->nbuf && okalloc; ++i)
         okalloc = b->d_res[i].reserve(sizeof(sed_result) * std::max(1, npairs)) &&
                   (!want_tb || b->d_tb[i].reserve(4 * std::max<uint64_t>(1, tbw)));
@@ -354,6 +395,14 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     if (!tasks.empty() && (e = hipMemcpyAsync(b->d_tasks.p, tasks.data(), sizeof(int2) * tasks.size(),
                                               hipMemcpyHostToDevice, c->stream)) != hipSuccess)
         return c->hipfail(e, "upload tasks");
+    if (b->nchains &&
+        ((e = hipMemcpyAsync(b->d_chain.p, chain_pairs.data(), 4 * chain_pairs.size(), hipMemcpyHostToDevice,
+                             c->stream)) != hipSuccess ||
+         (!chain_off.empty() &&
+          (e = hipMemcpyAsync((int32_t *)b->d_chain.p + chain_pairs.size(), chain_off.data(), 4 * chain_off.size(),
+                              hipMemcpyHostToDevice, c->stream)) != hipSuccess)))
+        return c->hipfail(e, "upload chains");
+    b->chain_npairs = chain_pairs.size();
     if (!lane_idx.empty() && (e = hipMemcpyAsync(b->d_lane.p, lane_idx.data(), 4 * lane_idx.size(),
                                                  hipMemcpyHostToDevice, c->stream)) != hipSuccess)
         return c->hipfail(e, "upload lane list");
@@ -436,7 +485,19 @@ int run_batch(sed_batch *b) {
         return c->hipfail(e, "memset progress");
     const bool len = want_tb || !(b->flags & SED_NO_LEN);
     if (b->nwave > 0) {
-        if (b->mode == SED_MODE_I32)
+        if (b->mode == SED_MODE_I32 && b->nchains) {
+            L.chain_pairs = (const int32_t *)b->d_chain.p;
+            L.chain_off = (const int32_t *)b->d_chain.p + b->chain_npairs;
+            L.nchains = b->nchains;
+            L.chain_list = (int)b->chain_npairs;
+            L.chain_counter = nullptr;
+            if (b->chain_dyn) {
+                L.chain_counter = (uint32_t *)b->d_chain.p + b->chain_npairs + 1;
+                if ((e = hipMemsetAsync(L.chain_counter, 0, 4, c->stream)) != hipSuccess)
+                    return c->hipfail(e, "reset chain counter");
+            }
+            e = sed_launch_i32_chain(L, b->ip, len);
+        } else if (b->mode == SED_MODE_I32)
             e = sed_launch_i32(L, b->ip, len);
         else
             e = sed_launch_f64(L, (const double *)c->gtab.p, b->fp, b->mode == SED_MODE_F64_TYPED);
@@ -553,6 +614,10 @@ int sed_set_option(sed_ctx *c, int key, int value) {
         c->opt_lane = value;
         return SED_OK;
     }
+    if (key == SED_OPT_CHAIN && value >= 0 && value <= 1024) {
+        c->opt_chain = value;
+        return SED_OK;
+    }
     if (key == SED_OPT_ROWS_PER_LANE && (value == 0 || value == 1 || value == 2 || value == 4 || value == 8 ||
                                          value == 16 || value == 32)) {
         c->opt_R = value;
@@ -613,6 +678,7 @@ void sed_batch_destroy(sed_batch *b) {
 int sed_batch_mode(const sed_batch *b) { return b ? b->mode : SED_E_ARG; }
 int sed_batch_rows_per_lane(const sed_batch *b) { return b ? b->R : SED_E_ARG; }
 int sed_batch_lane_pairs(const sed_batch *b) { return b ? b->nlane : SED_E_ARG; }
+int sed_batch_chains(const sed_batch *b) { return b ? b->nchains : SED_E_ARG; }
 
 int sed_batch_run(sed_batch *b) {
     if (!b) return SED_E_ARG;

@@ -18,6 +18,7 @@ SED_OPT_MODE = 1
 SED_OPT_ROWS_PER_LANE = 2
 SED_OPT_SPLIT = 3
 SED_OPT_LANE = 4
+SED_OPT_CHAIN = 5
 MODE_NAMES = {1: "i32", 2: "f64", 3: "f64-typed"}
 
 _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
@@ -42,6 +43,7 @@ SIGNATURES = [
     ("sed_batch_mode", C.c_int, [C.c_void_p]),
     ("sed_batch_rows_per_lane", C.c_int, [C.c_void_p]),
     ("sed_batch_lane_pairs", C.c_int, [C.c_void_p]),
+    ("sed_batch_chains", C.c_int, [C.c_void_p]),
     ("sed_batch_run", C.c_int, [C.c_void_p]),
     ("sed_batch_sync", C.c_int, [C.c_void_p]),
     ("sed_batch_last_times", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
@@ -241,6 +243,10 @@ class Batch:
     @property
     def lane_pairs(self):
         return self._lib.sed_batch_lane_pairs(self.ptr)
+
+    @property
+    def chains(self):
+        return self._lib.sed_batch_chains(self.ptr)
 
     def run(self):
         self.ctx._check(self._lib.sed_batch_run(self.ptr), "sed_batch_run")

@@ -20,13 +20,14 @@ OPCH = "idu"
 IUPAC = "AGCUYRWSKMDVHBN"
 
 
-def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len=False):
+def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len=False, chain=0):
     """Run (s1, s2) pairs through the engine; returns [(dist, is_int, len, opstr)]."""
     plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
     ctx.set_mode(mode)
     ctx.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, R)
     ctx.set_option(sedgpu.SED_OPT_SPLIT, split)
     ctx.set_option(sedgpu.SED_OPT_LANE, lane)
+    ctx.set_option(sedgpu.SED_OPT_CHAIN, chain)
     ctx.set_costs(plan)
     packed = sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs], [plan.encode(b) for _, b in pairs])
     dist, is_int, ln, ops = ctx.run(packed, script, no_len=no_len)
@@ -40,6 +41,7 @@ def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len
     ctx.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
     ctx.set_option(sedgpu.SED_OPT_SPLIT, 0)
     ctx.set_option(sedgpu.SED_OPT_LANE, 0)
+    ctx.set_option(sedgpu.SED_OPT_CHAIN, 0)
     return out
 
 
@@ -196,3 +198,54 @@ def test_lane_f64_distance_vs_oracle(gpu, tables, alphabet):
         assert sum(1 for g in got if g[2] == -1) > 100  # the lane route ran
         _oracle_check(tables[user], pairs, gpu_run(gpu, tables[user], pairs, script=False, no_len=True, lane=2),
                       no_len=True)
+
+
+@pytest.mark.parametrize("R", [4, 8])
+def test_chain_mode_vs_oracle(gpu, tables, R):
+    """CHAIN mode (forced): single-stripe pairs back to back in one wave, lanes switching pairs
+    one step apart; ragged m (1..700, including 63/64/65 and multiples of 64), n up to 64R,
+    scripts / lengths / distance only, both tables; lane route off so short m chains too."""
+    rng = np.random.default_rng(500 + R)
+    rows = 64 * R
+    pairs = []
+    for _ in range(120):
+        n = int(rng.choice([rng.integers(1, rows + 1), rows, 1]))
+        m = int(rng.choice([rng.integers(1, 701), 63, 64, 65, 128, 1, 2, 33]))
+        a = "".join(rng.choice(list("ACGU"), size=n))
+        if rng.random() < 0.5:
+            b = "".join(c if rng.random() > 0.1 else rng.choice(list("ACGU")) for c in (a * 3)[:m])
+        else:
+            b = "".join(rng.choice(list("ACGU"), size=m))
+        pairs.append((a, b))
+    for user in (False, True):
+        _oracle_check(tables[user], pairs, gpu_run(gpu, tables[user], pairs, R=R, chain=1, lane=2))
+        _oracle_check(tables[user], pairs, gpu_run(gpu, tables[user], pairs, R=R, chain=1, lane=2, script=False))
+        _oracle_check(tables[user], pairs, gpu_run(gpu, tables[user], pairs, R=R, chain=1, lane=2, script=False,
+                                                   no_len=True), no_len=True)
+    # long chains (7 ragged pairs each: many switch windows per wave)
+    _oracle_check(tables[True], pairs, gpu_run(gpu, tables[True], pairs, R=R, chain=7, lane=2))
+    _oracle_check(tables[False], pairs, gpu_run(gpu, tables[False], pairs, R=R, chain=7, lane=2, script=False))
+    # mixed with lane-kernel pairs, default routing otherwise
+    _oracle_check(tables[True], pairs, gpu_run(gpu, tables[True], pairs, R=R, chain=1))
+
+
+def test_chain_mode_is_used(gpu, tables):
+    plan = sedcost.build_plan(tables[False], ["ACGU"], ["ACGU"])
+    gpu.set_costs(plan)
+    A = synth.pair_codes(np.arange(64, dtype=np.uint64), 512, 0)
+    B = synth.pair_codes(np.arange(64, dtype=np.uint64), 512, 1)
+    gpu.set_option(sedgpu.SED_OPT_CHAIN, 1)
+    try:
+        b = sedgpu.Batch(gpu, sedgpu.PackedPairs.from_arrays(A, B), True)
+        assert b.chains == 64 and b.rows_per_lane == 8  # dynamic: one persistent wave per pair here
+        b.run()
+        d, ii, ln, ops = b.results()
+        b.close()
+    finally:
+        gpu.set_option(sedgpu.SED_OPT_CHAIN, 0)
+    cs = oracle.Costs.from_plan(plan)
+    packed = sedgpu.PackedPairs.from_arrays(A, B)
+    for p in range(0, 64, 7):
+        o = oracle.pair(cs, A[p], B[p])
+        assert (d[p], ln[p]) == (o["dist"], o["len"])
+        assert np.array_equal(sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln[p])), o["ops"])

@@ -26,6 +26,11 @@ def pmc(path):
 
 stats = list(csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_stats.csv"))))
 shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+for w in ("c3", "c5", "c5n"):  # secondary workloads (kernel trace only)
+    f = os.path.join(src, "kt_" + w, "kt_kernel_stats.csv")
+    if os.path.exists(f):
+        shutil.copy(f, os.path.join(dst, "kernel_stats_%s.csv" % w))
+        shutil.copy(os.path.join(src, "kt_bench_%s.json" % w), os.path.join(dst, "bench_under_kernel_trace_%s.json" % w))
 fetch = pmc(os.path.join(src, "fetch", "pmc_counter_collection.csv"))
 write = pmc(os.path.join(src, "write", "pmc_counter_collection.csv"))
 sq = pmc(os.path.join(src, "sq", "pmc_counter_collection.csv"))
