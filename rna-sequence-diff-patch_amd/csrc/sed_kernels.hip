@@ -160,15 +160,16 @@ __device__ __forceinline__ void i32_reset(uint32_t (&V)[R], uint32_t &top_prev, 
 // first real column, whose neighbours are then exactly D[row][0], D[row-1][0] and the cell above.
 #define SED_SEL_SENT 0x0C0D0100u
 
-// RAMP groups: steps < 63 of a stripe (per-lane insert constant).  CAP: the group that produces
-// the sink cell (captured on its lane).  Branch-free selects, so no value lives across a
-// basic-block boundary.
-template <int R, bool TB, bool LEN, bool RAMP, bool CAP>
+// SLOW groups: the ramp (steps < 63 of a stripe: per-lane insert constant) and the group that
+// produces the sink cell (captured on its lane).  One variant for both: every extra variant is
+// another merge point where the register allocator inserts copies of the whole state.
+template <int R, bool TB, bool LEN, bool SLOW>
 __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                           uint32_t &bottom, uint32_t &selv, uint32_t &tch, uint32_t &sch,
                                           const uint2 *__restrict__ lch, uint32_t &outc, uint32_t (&W)[4],
                                           const int s0, const int lane, const uint32_t kins, const uint32_t kdel,
-                                          const int cap_step, const int cap_lane, const int cap_row, uint32_t &cap) {
+                                          const bool ramp, const int cap_step, const int cap_lane, const int cap_row,
+                                          uint32_t &cap) {
     constexpr int G = Grp<R>::G;
     // opaque copies: the four group variants sit in sibling branches, and without this the
     // compiler hoists the first step's V[r] + kins out of them (16 more live VGPRs -> spills)
@@ -182,9 +183,9 @@ __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)
     for (int u = 0; u < G; ++u) {
         const int s = s0 + u;
         uint32_t ki = kin;
-        if constexpr (RAMP) ki = kin & ~(uint32_t)((s - lane) >> 31);  // virtual column: insert adds nothing
+        if constexpr (SLOW) ki = ramp ? (kin & ~(uint32_t)((s - lane) >> 31)) : kin;  // virtual column: insert adds nothing
         i32_step<R, TB, LEN>(V, cv, top_prev, bottom, selv, tch, sch, tv[u], outc, W, u, ki, kde);
-        if constexpr (CAP) {
+        if constexpr (SLOW) {
             const bool hit = (s == cap_step) && (lane == cap_lane);
 #pragma unroll
             for (int r = 0; r < R; ++r) cap = (hit && r == cap_row) ? V[r] : cap;
@@ -315,18 +316,12 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             if (c + 1 < nchunks) { tnx = load_top(c + 1); snx = load_sel(c + 1); }
             for (int g = 0; g < 64 / G && s < SG; ++g, s += G) {
                 const bool capg = cap_step >= s && cap_step < s + G;
-#define SED_GROUP(RAMP, CAP)                                                                            \
-    i32_group<R, TB, LEN, RAMP, CAP>(V, cv, top_prev, bottom, selv, tch, sch, lch, outc, W, s, lane, kins, kdel, \
-                                     cap_step, cap_lane, cap_row, cap)
-                if (s < 63) {
-                    if (capg) SED_GROUP(true, true);
-                    else SED_GROUP(true, false);
-                } else if (capg) {
-                    SED_GROUP(false, true);
-                } else {
-                    SED_GROUP(false, false);
-                }
-#undef SED_GROUP
+                if (s < 63 || capg)
+                    i32_group<R, TB, LEN, true>(V, cv, top_prev, bottom, selv, tch, sch, lch, outc, W, s, lane, kins,
+                                                kdel, s < 63, cap_step, cap_lane, cap_row, cap);
+                else
+                    i32_group<R, TB, LEN, false>(V, cv, top_prev, bottom, selv, tch, sch, lch, outc, W, s, lane, kins,
+                                                 kdel, false, cap_step, cap_lane, cap_row, cap);
                 if constexpr (TB) {
                     uint32_t *gp = tbk + (uint64_t)(s / G) * 256u;  // wave-uniform base, per-lane 16-byte offset
                     store_tb(gp + lane * 4, W);
