@@ -47,8 +47,8 @@ enum {
 
 /* flags for sed_run_batch / sed_batch_create */
 #define SED_WANT_SCRIPT 1u
-/* sed_batch only: two traceback/result buffers and a second stream, so the traceback of
- * run k overlaps the DP kernel of run k+1 (device memory for the traceback doubles). */
+/* sed_batch only: three traceback/result buffers and a second stream, so the traceback of
+ * run k overlaps the DP kernel of run k+1 (device memory for the traceback triples). */
 #define SED_PIPELINE 2u
 /* distance only (no SED_WANT_SCRIPT): out_len is not computed (-1), which lets the integer
  * kernels drop the op-count field of their keys (5 instead of 6 VALU ops per cell). */

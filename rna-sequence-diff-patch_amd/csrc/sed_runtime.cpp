@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -92,13 +93,15 @@ struct sed_batch {
     bool chain_dyn = false;    // persistent waves + device counter instead of static chains
     int ntasks = 0;
     uint64_t prog_words = 0;
-    // SED_PIPELINE: run k uses traceback/result buffer k&1, so the traceback of
-    // run k (second stream) overlaps the DP of run k+1.
+    // SED_PIPELINE: run k uses traceback/result buffer k%3 and its traceback runs on a second
+    // stream, overlapping the DP of run k+1.  Three buffers, so the DP of run k+3 is the first
+    // to wait for that traceback: with two, a traceback starved of CUs during the next DP
+    // (it only gets them in that DP's tail) delayed the DP after it (~0.7 ms per 27 ms step).
     int nbuf = 1;
-    DevBuf d_tb[2], d_res[2];
+    DevBuf d_tb[3], d_res[3];
     hipStream_t tb_stream = nullptr;
     // per buffer: the event-log entry of the last run that used it (handles copied from `log`)
-    std::array<hipEvent_t, 4> evk[2] = {};
+    std::array<hipEvent_t, 4> evk[3] = {};
     long runs = 0;
     bool ran = false;
     // per-run event log (sed_batch_times): {dp start, dp end, tb start, tb end}
@@ -108,11 +111,11 @@ struct sed_batch {
     sed_f64_params fp{};
     std::vector<sed_result> h_res;
 
-    int cur() const { return (int)((runs - 1) & (nbuf - 1)); }
+    int cur() const { return (int)((runs - 1) % nbuf); }
     ~sed_batch() {
         d_pd.release(); d_seqa.release(); d_seqb.release(); d_bnd.release(); d_ops.release();
         d_tasks.release(); d_prog.release(); d_lane.release(); d_chain.release();
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < 3; ++i) {
             d_tb[i].release();
             d_res[i].release();
         }
@@ -190,7 +193,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     b->flags = flags;
     b->ran = false;
     b->runs = 0;
-    b->nbuf = (flags & SED_PIPELINE) ? 2 : 1;
+    b->nbuf = (flags & SED_PIPELINE) ? 3 : 1;
     b->n.assign(len_a, len_a + npairs);
     b->m.assign(len_b, len_b + npairs);
     int max_n = 0, max_m = 0;
@@ -437,9 +440,15 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         b->fp = fp;
     }
     if ((e = grow_log(b, 64)) != hipSuccess) return c->hipfail(e, "event create");
-    if (b->nbuf == 2 && !b->tb_stream &&
-        (e = hipStreamCreateWithFlags(&b->tb_stream, hipStreamNonBlocking)) != hipSuccess)
-        return c->hipfail(e, "traceback stream");
+    if (b->nbuf > 1 && !b->tb_stream) {
+        // experiment hook (SED_STREAM_PRIO=tb_low|both): the overlapped traceback at the lowest priority
+        int least = 0, greatest = 0;
+        (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+        const char *pr = getenv("SED_STREAM_PRIO");
+        const bool low = pr && (!strcmp(pr, "tb_low") || !strcmp(pr, "both"));
+        if ((e = hipStreamCreateWithPriority(&b->tb_stream, hipStreamNonBlocking, low ? least : 0)) != hipSuccess)
+            return c->hipfail(e, "traceback stream");
+    }
     return SED_OK;
 }
 
@@ -450,12 +459,12 @@ int run_batch(sed_batch *b) {
         ++b->runs;
         return SED_OK;
     }
-    const int k = (int)(b->runs & (b->nbuf - 1));
+    const int k = (int)(b->runs % b->nbuf);
     const bool want_tb = (b->flags & SED_WANT_SCRIPT) != 0;
     hipError_t e;
     if (b->nlog == b->log.size() && (e = grow_log(b, 64)) != hipSuccess) return c->hipfail(e, "event create");
     const std::array<hipEvent_t, 4> lg = b->log[b->nlog++];
-    hipStream_t ts = b->nbuf == 2 ? b->tb_stream : c->stream;
+    hipStream_t ts = b->nbuf > 1 ? b->tb_stream : c->stream;
     sed_launch L{};
     L.pd = (const sed_pair_desc *)b->d_pd.p;
     L.npairs = b->npairs;
@@ -471,7 +480,8 @@ int run_batch(sed_batch *b) {
     L.prog = (uint32_t *)b->d_prog.p;
     L.ntasks = b->split ? b->ntasks : 0;
     // buffer k was last read by the traceback of run runs-2
-    if (b->nbuf == 2 && want_tb && b->runs >= 2 && (e = hipStreamWaitEvent(c->stream, b->evk[k][3], 0)) != hipSuccess)
+    if (b->nbuf > 1 && want_tb && b->runs >= b->nbuf &&
+        (e = hipStreamWaitEvent(c->stream, b->evk[k][3], 0)) != hipSuccess)
         return c->hipfail(e, "stream wait");
     // Only the event-log records sit between kernels: each record is a packet on the queue, and for
     // the ~50 us lane kernel (config 5) every avoided record is measurable.
@@ -580,7 +590,11 @@ sed_ctx *sed_create(int device) {
     }
     sed_ctx *c = new sed_ctx();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    int least = 0, greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+    const char *pr = getenv("SED_STREAM_PRIO");
+    const bool high = pr && (!strcmp(pr, "dp_high") || !strcmp(pr, "both"));
+    if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, high ? greatest : 0) != hipSuccess) {
         (void)hipGetLastError();
         delete c;
         return nullptr;
