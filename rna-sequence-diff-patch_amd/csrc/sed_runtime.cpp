@@ -798,10 +798,38 @@ int sed_run_batch(sed_ctx *c, const uint8_t *codes_a, const int64_t *off_a, cons
         c->scratch = new sed_batch();
         c->scratch->ctx = c;
     }
-    int rc = fill_batch(c->scratch, codes_a, off_a, len_a, codes_b, off_b, len_b, npairs, flags);
-    if (rc != SED_OK) return rc;
-    if ((rc = run_batch(c->scratch)) != SED_OK) return rc;
-    return fetch_results(c->scratch, out_dist, out_is_int, out_len, out_ops, ops_off);
+    if (npairs < 0 || (npairs > 0 && (!off_a || !len_a || !off_b || !len_b)))
+        return c->fail(SED_E_ARG, "bad batch arguments");
+    // Host-buffer batches are cut into chunks whose traceback workspace (2 bits per cell plus the
+    // wavefront skew) stays under SED_TB_BUDGET_GB (default 48): a list of many long pairs then
+    // runs in several launches instead of failing with SED_E_OOM.
+    double budget = 48e9;
+    if (const char *e = getenv("SED_TB_BUDGET_GB")) budget = std::max(1e6, atof(e) * 1e9);
+    int32_t p0 = 0;
+    while (p0 < npairs || (npairs == 0 && p0 == 0)) {
+        int32_t p1 = p0;
+        double bytes = 0;
+        if (flags & SED_WANT_SCRIPT) {
+            while (p1 < npairs) {
+                const double pb = 0.25 * (double)std::max(0, len_a[p1]) * (double)(std::max(0, len_b[p1]) + 127);
+                if (p1 > p0 && bytes + pb > budget) break;
+                bytes += pb;
+                ++p1;
+            }
+        } else {
+            p1 = npairs;
+        }
+        const int32_t np = p1 - p0;
+        int rc = fill_batch(c->scratch, codes_a, off_a + p0, len_a + p0, codes_b, off_b + p0, len_b + p0, np, flags);
+        if (rc != SED_OK) return rc;
+        if ((rc = run_batch(c->scratch)) != SED_OK) return rc;
+        rc = fetch_results(c->scratch, out_dist ? out_dist + p0 : nullptr, out_is_int ? out_is_int + p0 : nullptr,
+                           out_len ? out_len + p0 : nullptr, out_ops, ops_off ? ops_off + p0 : nullptr);
+        if (rc != SED_OK) return rc;
+        if (npairs == 0) break;
+        p0 = p1;
+    }
+    return SED_OK;
 }
 
 int sed_full_matrix(sed_ctx *c, const uint8_t *codes_a, int32_t n, const uint8_t *codes_b, int32_t m, double *D,

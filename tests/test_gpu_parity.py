@@ -249,3 +249,13 @@ def test_chain_mode_is_used(gpu, tables):
         o = oracle.pair(cs, A[p], B[p])
         assert (d[p], ln[p]) == (o["dist"], o["len"])
         assert np.array_equal(sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln[p])), o["ops"])
+
+
+def test_script_batches_are_chunked_by_traceback_budget(gpu, tables, monkeypatch):
+    """sed_run_batch cuts a script batch into several launches when its traceback workspace
+    exceeds SED_TB_BUDGET_GB; results are unchanged (here ~30 chunks of ~1 MB)."""
+    pairs = _random_pairs(909, 90, "ACGU", 0, 900, related=True)
+    monkeypatch.setenv("SED_TB_BUDGET_GB", "0.001")
+    got = gpu_run(gpu, tables[True], pairs)
+    monkeypatch.delenv("SED_TB_BUDGET_GB")
+    _oracle_check(tables[True], pairs, got)
