@@ -853,13 +853,18 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
 // 16-byte aligned block of codes last read is kept in registers: a diagonal
 // run stays in it for up to four steps.
 // ---------------------------------------------------------------------------
-template <int R>
+// UNI = true: one pair per workgroup, taken from blockIdx only, so the whole walk is wave-uniform
+// and the compiler runs it on the scalar unit (s_load of the 16-byte blocks, SALU arithmetic).
+// A single lane's dependent VALU chain issues at ~8 cycles per instruction; for a lone pair
+// (config 2, the GUI) the scalar walk is the faster one.  Batches keep one lane per pair.
+template <int R, bool UNI = false>
 __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
                                                            const uint32_t *__restrict__ tb,
                                                            const sed_result *__restrict__ res,
                                                            uint32_t *__restrict__ ops) {
     constexpr int G = Grp<R>::G;
-    const int pair = blockIdx.x * blockDim.x + threadIdx.x;
+    if (UNI && threadIdx.x != 0) return;
+    const int pair = UNI ? (int)__builtin_amdgcn_readfirstlane(blockIdx.x) : (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (pair >= npairs) return;
     const sed_pair_desc d = pd[pair];
     if (d.lane) return;  // scripted by sed_lane.hip
@@ -1022,12 +1027,18 @@ hipError_t sed_launch_f64(const sed_launch &L, const double *gtab, const sed_f64
 }
 
 hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops) {
-    const int grid = (L.npairs + 63) / 64;
+    // up to one pair per CU: a wave-uniform (scalar) walk per pair; beyond: one lane per pair
+    const bool uni = L.npairs <= 256;
+    const int grid = uni ? L.npairs : (L.npairs + 63) / 64;
     switch (L.R) {
-#define CASE(RR)                                                                                              \
-    case RR:                                                                                                  \
-        hipLaunchKernelGGL(sed_traceback_kernel<RR>, dim3(grid), dim3(64), 0, L.stream, L.pd, L.npairs, L.tb, \
-                           L.res, ops);                                                                      \
+#define CASE(RR)                                                                                                 \
+    case RR:                                                                                                     \
+        if (uni)                                                                                                 \
+            hipLaunchKernelGGL((sed_traceback_kernel<RR, true>), dim3(grid), dim3(64), 0, L.stream, L.pd,        \
+                               L.npairs, L.tb, L.res, ops);                                                     \
+        else                                                                                                     \
+            hipLaunchKernelGGL((sed_traceback_kernel<RR, false>), dim3(grid), dim3(64), 0, L.stream, L.pd,       \
+                               L.npairs, L.tb, L.res, ops);                                                     \
         break;
         CASE(4) CASE(8) CASE(16) CASE(32)
 #undef CASE
