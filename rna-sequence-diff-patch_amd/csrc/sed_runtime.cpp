@@ -440,15 +440,9 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         b->fp = fp;
     }
     if ((e = grow_log(b, 64)) != hipSuccess) return c->hipfail(e, "event create");
-    if (b->nbuf > 1 && !b->tb_stream) {
-        // experiment hook (SED_STREAM_PRIO=tb_low|both): the overlapped traceback at the lowest priority
-        int least = 0, greatest = 0;
-        (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
-        const char *pr = getenv("SED_STREAM_PRIO");
-        const bool low = pr && (!strcmp(pr, "tb_low") || !strcmp(pr, "both"));
-        if ((e = hipStreamCreateWithPriority(&b->tb_stream, hipStreamNonBlocking, low ? least : 0)) != hipSuccess)
-            return c->hipfail(e, "traceback stream");
-    }
+    if (b->nbuf > 1 && !b->tb_stream &&
+        (e = hipStreamCreateWithFlags(&b->tb_stream, hipStreamNonBlocking)) != hipSuccess)
+        return c->hipfail(e, "traceback stream");
     return SED_OK;
 }
 
@@ -590,11 +584,7 @@ sed_ctx *sed_create(int device) {
     }
     sed_ctx *c = new sed_ctx();
     c->device = device;
-    int least = 0, greatest = 0;
-    (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
-    const char *pr = getenv("SED_STREAM_PRIO");
-    const bool high = pr && (!strcmp(pr, "dp_high") || !strcmp(pr, "both"));
-    if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, high ? greatest : 0) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         (void)hipGetLastError();
         delete c;
         return nullptr;
