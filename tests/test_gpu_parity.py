@@ -259,3 +259,21 @@ def test_script_batches_are_chunked_by_traceback_budget(gpu, tables, monkeypatch
     got = gpu_run(gpu, tables[True], pairs)
     monkeypatch.delenv("SED_TB_BUDGET_GB")
     _oracle_check(tables[True], pairs, got)
+
+
+def test_large_pairs_across_the_integer_key_limits(gpu, tables):
+    """Near the packed-key limits (L < 2^14, D < 2^16 - 256 for the padded problem): a 12000 x 4000
+    pair still runs the integer kernel, a 9000 x 9000 pair falls back to fp64; both bit-exact."""
+    rng = np.random.default_rng(1234)
+    a1 = "".join(rng.choice(list("ACGU"), size=12000))
+    b1 = "".join(c if rng.random() > 0.15 else rng.choice(list("ACGU")) for c in a1[:4000])
+    a2 = "".join(rng.choice(list("ACGU"), size=9000))
+    b2 = "".join(c if rng.random() > 0.15 else rng.choice(list("ACGU")) for c in a2)
+    for pairs in ([(a1, b1)], [(a2, b2)]):
+        plan = sedcost.build_plan(tables[True], [p[0] for p in pairs], [p[1] for p in pairs])
+        gpu.set_costs(plan)
+        b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(x) for x, _ in pairs],
+                                                 [plan.encode(y) for _, y in pairs]), True)
+        assert b.mode == ("i32" if len(pairs[0][0]) == 12000 else "f64")
+        b.close()
+        _oracle_check(tables[True], pairs, gpu_run(gpu, tables[True], pairs))
