@@ -853,18 +853,13 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
 // 16-byte aligned block of codes last read is kept in registers: a diagonal
 // run stays in it for up to four steps.
 // ---------------------------------------------------------------------------
-// UNI = true: one pair per workgroup, taken from blockIdx only, so the whole walk is wave-uniform
-// and the compiler runs it on the scalar unit (s_load of the 16-byte blocks, SALU arithmetic).
-// A single lane's dependent VALU chain issues at ~8 cycles per instruction; for a lone pair
-// (config 2, the GUI) the scalar walk is the faster one.  Batches keep one lane per pair.
-template <int R, bool UNI = false>
+template <int R>
 __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
                                                            const uint32_t *__restrict__ tb,
                                                            const sed_result *__restrict__ res,
                                                            uint32_t *__restrict__ ops) {
     constexpr int G = Grp<R>::G;
-    if (UNI && threadIdx.x != 0) return;
-    const int pair = UNI ? (int)__builtin_amdgcn_readfirstlane(blockIdx.x) : (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int pair = blockIdx.x * blockDim.x + threadIdx.x;
     if (pair >= npairs) return;
     const sed_pair_desc d = pd[pair];
     if (d.lane) return;  // scripted by sed_lane.hip
@@ -917,6 +912,93 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
                 }
             }
             if (i == 0 || j == 0) break;
+        }
+    }
+    while (j > 0) { emit(0u); --j; }
+    while (i > 0) { emit(1u); --i; }
+}
+
+
+// Few pairs (config 2, the GUI): one pair per wave, the walk itself wave-uniform (scalar unit),
+// and the wave's 64 lanes fetch a window of 64 code blocks at once.  A lone walk is bound by the
+// latency of its dependent block loads (a new 16-byte block every ~R steps of a diagonal path);
+// the window covers NT = G lanes x NS = R step-groups, i.e. the next ~50-64 steps of any path
+// direction, so one load latency serves them all.  Blocks move from the window's VGPRs to SGPRs
+// with v_readlane when the walk enters them.
+template <int R>
+__global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair_desc *__restrict__ pd,
+                                                                  int npairs, const uint32_t *__restrict__ tb,
+                                                                  const sed_result *__restrict__ res,
+                                                                  uint32_t *__restrict__ ops) {
+    constexpr int G = Grp<R>::G, NT = G, NS = R;  // NT * NS = 64 blocks
+    constexpr int LR = R == 4 ? 2 : R == 8 ? 3 : R == 16 ? 4 : 5, LG = 6 - LR;
+    static_assert((1 << LR) == R, "R must be a power of two in 4..32");
+    const int lane = threadIdx.x;
+    const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x);
+    if (pair >= npairs) return;
+    const sed_pair_desc d = pd[pair];
+    if (d.lane) return;  // scripted by sed_lane.hip
+    const int n = d.n, m = d.m;
+    const int SG = (m + 63 + G - 1) / G * G;
+    const uint64_t stripe_words = (uint64_t)(SG / G) * 256u;
+    uint32_t *out = ops + d.ops_off;
+    // ops are emitted sink -> origin, i.e. from position q-1 down; acc = acc<<2 | op leaves the op of
+    // position q in bits 1:0 and position q+p in bits 2p+1:2p when a word [q, q+16) completes
+    uint32_t q = (uint32_t)__builtin_amdgcn_readfirstlane(res[pair].len);
+    uint32_t acc = 0;
+    auto emit = [&](uint32_t op) {
+        acc = (acc << 2) | op;
+        if ((--q & 15u) == 0) out[q >> 4] = acc;  // every lane stores the same word (no exec switching)
+    };
+    int i = n, j = m;
+    if (i > 0 && j > 0) {
+        const int rr = i - 1;
+        int k = rr >> (6 + LR);
+        int t = (rr >> LR) & 63;
+        uint32_t r = (uint32_t)rr & (R - 1);
+        int s = j - 1 + t;  // the step at which lane t computed column j
+        const uint32_t *base = tb + d.tb_off + (uint64_t)k * stripe_words;
+        int wt = -1, wsg = -1;  // window corner (highest lane, highest step-group); -1: none loaded
+        uint4 wv = make_uint4(0, 0, 0, 0);
+        uint64_t lo = 0, hi = 0;  // codes 0..31 and 32..63 of the block being walked
+        uint32_t fresh = 1;  // integer flags throughout: bools of uniform values round-trip through VALU masks
+        while (true) {
+            if (fresh) {  // entered another block: from the window, reloading it first if needed
+                const int sg = s >> LG;
+                if (!(t <= wt && t > wt - NT && sg <= wsg && sg > wsg - NS)) {
+                    wt = t;
+                    wsg = sg;
+                    const int lt = t - lane / NS, ls = sg - lane % NS;
+                    wv = (lt >= 0 && ls >= 0) ? *reinterpret_cast<const uint4 *>(base + ((uint64_t)ls * 64u + lt) * 4u)
+                                              : make_uint4(0, 0, 0, 0);
+                }
+                const int L = (wt - t) * NS + (wsg - sg);
+                lo = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(wv.x, L) |
+                     ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(wv.y, L) << 32);
+                hi = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(wv.z, L) |
+                     ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(wv.w, L) << 32);
+            }
+            const uint32_t c = ((uint32_t)(s & (G - 1)) << LR) | r;  // code index inside the block
+            const uint32_t op = (uint32_t)(((c & 32u) ? hi : lo) >> (2u * c & 63u)) & 3u;
+            emit(op);
+            const uint32_t di = (op + 1u) >> 1, dj = (5u >> op) & 1u;  // row move (del, upd), column move (ins, upd)
+            i -= (int)di;
+            j -= (int)dj;
+            if (min(i, j) == 0) break;
+            const uint32_t wrap = di & ((r - 1u) >> 31);  // moved up out of the lane's rows (r was 0)
+            r = (r - di) & (R - 1);
+            const int s_old = s;
+            s -= (int)(dj + wrap);
+            fresh = wrap | ((uint32_t)(s ^ s_old) >> LG);
+            if (wrap) {
+                if (--t < 0) {  // the stripe above
+                    t = 63;
+                    --k;
+                    base -= stripe_words;
+                    s = j - 1 + t;
+                    wt = -1;
+                }
+            }
         }
     }
     while (j > 0) { emit(0u); --j; }
@@ -1027,17 +1109,17 @@ hipError_t sed_launch_f64(const sed_launch &L, const double *gtab, const sed_f64
 }
 
 hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops) {
-    // up to one pair per CU: a wave-uniform (scalar) walk per pair; beyond: one lane per pair
+    // up to one pair per CU: a wave-uniform walk per pair over windows of blocks; beyond: one lane per pair
     const bool uni = L.npairs <= 256;
     const int grid = uni ? L.npairs : (L.npairs + 63) / 64;
     switch (L.R) {
 #define CASE(RR)                                                                                                 \
     case RR:                                                                                                     \
         if (uni)                                                                                                 \
-            hipLaunchKernelGGL((sed_traceback_kernel<RR, true>), dim3(grid), dim3(64), 0, L.stream, L.pd,        \
+            hipLaunchKernelGGL((sed_traceback_window_kernel<RR>), dim3(grid), dim3(64), 0, L.stream, L.pd,       \
                                L.npairs, L.tb, L.res, ops);                                                     \
         else                                                                                                     \
-            hipLaunchKernelGGL((sed_traceback_kernel<RR, false>), dim3(grid), dim3(64), 0, L.stream, L.pd,       \
+            hipLaunchKernelGGL((sed_traceback_kernel<RR>), dim3(grid), dim3(64), 0, L.stream, L.pd,              \
                                L.npairs, L.tb, L.res, ops);                                                     \
         break;
         CASE(4) CASE(8) CASE(16) CASE(32)

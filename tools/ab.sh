@@ -7,6 +7,6 @@ out=gpurun_out/ab.jsonl
 for r in $(seq 1 $N); do
   for L in $A $B; do
     SED_LIBRARY=$PWD/rna-sequence-diff-patch_amd/$L timeout -k 10 200 python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ${AB_ARGS} > gpurun_out/ab.json 2> gpurun_out/ab.log
-    python3 -c "import json; d=json.load(open('gpurun_out/ab.json')); print(json.dumps({'lib':'$L','round':$r,'value':d['value'],'dp_ms':d['roofline']['kernel_ms'],'valid':d.get('script_valid_rate')}))" >> $out
+    python3 -c "import json; d=json.load(open('gpurun_out/ab.json')); print(json.dumps({'lib':'$L','round':$r,'value':d['value'],'dp_ms':d['roofline']['kernel_ms'],'valid':d.get('script_valid_rate'),'tb_ms':d.get('traceback_ms'),'step_ms':d['ms_per_step']}))" >> $out
   done
 done
