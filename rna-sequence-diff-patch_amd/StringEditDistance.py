@@ -234,6 +234,8 @@ class DPMatrix:
 
     def script(self):
         """Canonical op codes (0 insert, 1 delete, 2 update), origin -> sink."""
+        global _script_hint
+        _script_hint = True
         if self._script is None:
             self._run(True)
         return self._script
@@ -304,12 +306,22 @@ class DPMatrix:
         return '[' + ', '.join(repr(r) for r in self) + ']'
 
 
+# One-deep predictor of the caller's pattern: True when the matrix of the previous wagnerFisher call
+# was asked for its script (the GUI: wagnerFisher -> create_paths -> generate_es).  The next call then
+# runs DP + traceback in one engine call instead of a distance run followed by a script run; callers
+# that only read distances (IRMethods.wf_score) keep the cheaper distance-only run.  Either way the
+# matrix is computed eagerly, as in the reference, and the results are the same.
+_script_hint = False
+
+
 def wagnerFisher(str1, str2, userCosts=False):
     """Weighted Wagner–Fischer matrix of str1 (rows) -> str2 (columns) (reference :133-224)."""
+    global _script_hint
     table = _table(userCosts)
     sedcost.check_pair(table, str1, str2)
     dp = DPMatrix(str1, str2, sedcost.build_plan(table, [str1], [str2]))
-    dp._run(False)
+    want, _script_hint = _script_hint, False
+    dp._run(want)
     return dp
 
 

@@ -173,3 +173,23 @@ def test_search_collection_matches_reference(SED):
         wfsearch.search_collection(s["query"], None, coll, wfsearch.wf_score, callback=seen.append)
         assert [[a, b] for a, b in seen[0]] == want
         assert wfsearch.wf_score(s["query"], want[3][0]) == want[3][1]
+
+
+def test_script_hint_runs_agree(SED):
+    """wagnerFisher runs distance-only, or DP + traceback when the previous matrix was asked for its
+    script (the GUI pattern).  Both runs must give the same value, type, canonical path and script."""
+    for r in load_golden("g1_small.json")[:120]:
+        seen = []
+        for hint in (False, True):
+            SED._script_hint = hint
+            dp = SED.wagnerFisher(r["s1"], r["s2"], r["user"])
+            assert (dp._script is not None) == hint
+            v = dp[len(dp) - 1][len(dp[0]) - 1].value
+            assert (float(v), isinstance(v, int)) == (float.fromhex(r["dist"][0]), r["dist"][1])
+            assert "".join("idu"[o] for o in SED.create_paths(dp)[0].ops) == r["canon"]
+            assert SED._script_hint  # create_paths asked for the script: the next call predicts it
+            seen.append((v, type(v), list(dp.script())))
+        assert seen[0] == seen[1]
+    SED._script_hint = True
+    assert SED.wagnerFisher("ACGU", "AGU")._script is not None
+    assert SED.wagnerFisher("ACGU", "AGU")._script is None  # nobody asked for the last script: distance-only again
