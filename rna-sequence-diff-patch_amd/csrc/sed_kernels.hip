@@ -67,6 +67,13 @@ __device__ __forceinline__ double dpp_rol1_f64(double src) {
 }
 
 __device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) { return min(min(a, b), c); }
+// An opaque v_min3_u32: over three selects (tie keys of the fp64 kernel) the compiler rewrites
+// min(min(a, b), c) into select-of-min chains that cost one op more per cell.
+__device__ __forceinline__ uint32_t umin3_op(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 
 // relaxed agent-scope load = global_load sc1: bypasses this CU's L1 so a
 // stripe reads the bottom row its own wave stored during the previous stripe.
@@ -636,7 +643,7 @@ __device__ __forceinline__ void f64_step(double (&D)[R], uint32_t (&LK)[R], uint
         const uint32_t ka = ea ? LK[r] + 4u : 0xFFFFFFFFu;
         const uint32_t kb = eb ? lup + 5u : 0xFFFFFFFFu;
         const uint32_t kc = ec ? ldiag + 6u : 0xFFFFFFFFu;
-        const uint32_t km = umin3(ka, kb, kc);
+        const uint32_t km = umin3_op(ka, kb, kc);
         const uint32_t ln = km & ~3u;
         uint32_t tn = 0;
         if constexpr (TYPED) {
