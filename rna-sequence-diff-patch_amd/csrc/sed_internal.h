@@ -33,6 +33,8 @@ struct sed_i32_params {
     uint32_t costrow[4];
     uint32_t kins, kdel;
     uint32_t ins, del;
+    uint32_t epoch;  // SPLIT hand-off counters: 1..32767 per run (sed_kernels.hip: wait_progress)
+    uint32_t pad;
 };
 
 struct sed_f64_params {

@@ -212,22 +212,28 @@ template <int R> struct I32Waves { static constexpr int value = R >= 32 ? 4 : (R
 // producer = every lane's plain stores -> s_waitcnt vmcnt(0) -> lane 0 agent release fence ->
 // s_waitcnt -> relaxed agent store of the published column count; consumer = relaxed agent
 // poll (bounded, s_sleep) -> agent acquire fence -> L1-bypassing sc1 loads.
-__device__ __forceinline__ void publish_progress(uint32_t *prog, uint32_t cols, int lane) {
+// Counter word = poison << 31 | epoch << 16 | columns.  The run's epoch (1..32767, prm.epoch)
+// makes the previous run's counts read as "nothing yet", so the counters need no reset between
+// runs (the host zeroes them when the epoch wraps).  A stripe that gave up waiting publishes
+// with the poison bit; its consumer then stops waiting too, and the last stripe reports err.
+#define SED_PROG_POISON 0x80000000u
+__device__ __forceinline__ void publish_progress(uint32_t *prog, uint32_t tag, uint32_t cols, int lane) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(prog, cols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(prog, tag | cols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
-__device__ __forceinline__ bool wait_progress(const uint32_t *prog, uint32_t need) {
-    uint32_t spins = 0;
-    while (__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+__device__ __forceinline__ bool wait_progress(const uint32_t *prog, uint32_t epoch_tag, uint32_t need) {
+    uint32_t spins = 0, v;
+    while (((v = __hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & ~SED_PROG_POISON) <
+           (epoch_tag | need)) {
         __builtin_amdgcn_s_sleep(2);
         if (++spins > (1u << 24)) return false;  // producer never came: give up, flag the pair
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    return true;
+    return !(v & SED_PROG_POISON);
 }
 
 // SPLIT = false: one wave per pair walks all of its stripes (batches).
@@ -303,7 +309,7 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             const int j = 64 * c + lane + 1;
             if (k == 0) return i32_border((uint32_t)j, prm.ins);  // row 0: D = j*insert, L = j
             if constexpr (SPLIT) {  // after one timeout stop waiting: the kernel must still drain quickly
-                if (ok) ok = wait_progress(prog + d.prog_off + k - 1, (uint32_t)min(m, 64 * c + 64));
+                if (ok) ok = wait_progress(prog + d.prog_off + k - 1, prm.epoch << 16, (uint32_t)min(m, 64 * c + 64));
             }
             return load_sc1(bnd_in + j + 64);
         };
@@ -337,7 +343,9 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             // lane i holds lane 63's bottom cell of step s-64+i, i.e. column s-126+i at bnd index col+64
             if (!last) {
                 bnd_out[s - 62 + lane] = outc;
-                if constexpr (SPLIT) publish_progress(prog + d.prog_off + k, (uint32_t)min(m, max(0, s - 63)), lane);
+                if constexpr (SPLIT)
+                    publish_progress(prog + d.prog_off + k, (prm.epoch << 16) | (ok ? 0u : SED_PROG_POISON),
+                                     (uint32_t)min(m, max(0, s - 63)), lane);
             }
             tch = tnx;
             sch = snx;
@@ -350,8 +358,8 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
         res[pair].dist = (double)D;
         res[pair].len = LEN ? (int32_t)((cap >> 2) & 0x3FFFu) : -1;
         res[pair].is_int = (D == 0);
+        res[pair].err = ok ? 0 : 1;  // SPLIT: a timed-out wait anywhere up the stripe chain poisons the pair
     }
-    if (SPLIT && !ok && lane == 0) res[pair].err = 1;  // a timed-out wait poisons the pair (err zeroed per run)
 }
 
 // ---------------------------------------------------------------------------

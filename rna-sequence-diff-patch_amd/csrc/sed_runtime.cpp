@@ -480,11 +480,11 @@ int run_batch(sed_batch *b) {
     // Only the event-log records sit between kernels: each record is a packet on the queue, and for
     // the ~50 us lane kernel (config 5) every avoided record is measurable.
     if ((e = hipEventRecord(lg[0], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
-    // per-run state (SPLIT only): result error flags and the hand-off counters; the other kernels
-    // write every result field and never set err (buffers are zeroed once at creation)
-    if (b->split && (e = hipMemsetAsync(L.res, 0, sizeof(sed_result) * b->npairs, c->stream)) != hipSuccess)
-        return c->hipfail(e, "memset results");
-    if (b->split && b->prog_words &&
+    // SPLIT hand-off counters carry the run's epoch (1..32767), so they are zeroed only when it wraps;
+    // every kernel writes all result fields, err included
+    sed_i32_params ip = b->ip;
+    ip.epoch = (uint32_t)(b->runs % 32767u) + 1u;
+    if (b->split && b->prog_words && ip.epoch == 1 &&
         (e = hipMemsetAsync(b->d_prog.p, 0, 4 * b->prog_words, c->stream)) != hipSuccess)
         return c->hipfail(e, "memset progress");
     const bool len = want_tb || !(b->flags & SED_NO_LEN);
@@ -500,16 +500,16 @@ int run_batch(sed_batch *b) {
                 if ((e = hipMemsetAsync(L.chain_counter, 0, 4, c->stream)) != hipSuccess)
                     return c->hipfail(e, "reset chain counter");
             }
-            e = sed_launch_i32_chain(L, b->ip, len);
+            e = sed_launch_i32_chain(L, ip, len);
         } else if (b->mode == SED_MODE_I32)
-            e = sed_launch_i32(L, b->ip, len);
+            e = sed_launch_i32(L, ip, len);
         else
             e = sed_launch_f64(L, (const double *)c->gtab.p, b->fp, b->mode == SED_MODE_F64_TYPED);
         if (e != hipSuccess) return c->hipfail(e, "DP kernel launch");
     }
     if (b->nlane > 0) {
         if (b->mode == SED_MODE_I32)
-            e = sed_launch_lane_i32(L, (const int32_t *)b->d_lane.p, b->nlane, b->ip, len);
+            e = sed_launch_lane_i32(L, (const int32_t *)b->d_lane.p, b->nlane, ip, len);
         else
             e = sed_launch_lane_f64(L, (const int32_t *)b->d_lane.p, b->nlane, (const double *)c->gtab.p, c->ins,
                                     c->del, c->K);
