@@ -150,6 +150,7 @@ def main():
                     help="run DP and traceback back to back on one stream (no overlap across steps)")
     ap.add_argument("--rows-per-lane", type=int, default=0)
     ap.add_argument("--no-lane", action="store_true", help="route short pairs to the wave kernels too (A/B)")
+    ap.add_argument("--no-lane-x2", action="store_true", help="distance-only lane pairs one per lane (no 16-bit packing)")
     ap.add_argument("--split", type=int, default=0, help="SED_OPT_SPLIT: 0 auto, 1 force, 2 off (A/B)")
     ap.add_argument("--chain", type=int, default=0,
                     help="SED_OPT_CHAIN: 0 auto, 1 force, 2 off, L>=3 force with chains of L pairs (A/B)")
@@ -211,6 +212,8 @@ def main():
         ctx.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, args.rows_per_lane)
     if args.no_lane:
         ctx.set_option(sedgpu.SED_OPT_LANE, 2)
+    elif args.no_lane_x2:
+        ctx.set_option(sedgpu.SED_OPT_LANE, 3)
     if args.chain:
         ctx.set_option(sedgpu.SED_OPT_CHAIN, args.chain)
     if args.split:

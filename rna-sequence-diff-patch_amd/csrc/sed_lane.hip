@@ -132,6 +132,98 @@ __global__ __launch_bounds__(256) void sed_lane_i32_kernel(const sed_pair_desc *
     }
 }
 
+// Distance only, two pairs per lane (SED_NO_LEN batches: config 5, wfsearch).  Pair P lives in
+// the low 16 bits of every cell word and pair Q in the high 16 bits; both have the same n, so one
+// row loop serves both.  Distance keys need no L/op field, so a cell is D alone (< 2^16, the
+// integer-mode bound), and packed 16-bit ops do two cells at once:
+//   perm (P's and Q's update costs in one word) + 3 v_pk_add_u16 + 2 v_pk_min_u16 = 6 VALU / 2 cells
+// instead of 5 VALU / cell.  Both halves stay below 2^16 - 256, so no half ever wraps.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));  // v_pk_*_u16 operands
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t,
+                              __builtin_elementwise_min(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+}
+
+__global__ __launch_bounds__(256) void sed_lane_i32x2_kernel(const sed_pair_desc *__restrict__ pd,
+                                                             const int32_t *__restrict__ idx, int nlanes,
+                                                             const uint32_t *__restrict__ seqa,
+                                                             const uint32_t *__restrict__ seqb,
+                                                             sed_result *__restrict__ res, sed_i32_params prm) {
+    constexpr int MM = SED_LANE_MAXM;
+    static_assert(MM == 32, "str2 codes are read as two 16-symbol words");
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nlanes) return;
+    const int P = idx[2 * t], Q = idx[2 * t + 1];
+    const sed_pair_desc dP = pd[P], dQ = pd[Q];
+    const int n = dP.n, mP = dP.m, mQ = dQ.m;  // host guarantees dQ.n == n, 1 <= n <= MAXN, 1 <= m <= MM
+    const uint32_t kins = prm.ins * 0x10001u, kdel = prm.del * 0x10001u;
+    uint32_t colrow[4];  // transposed cost table, as in sed_lane_i32_kernel
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) w |= ((prm.costrow[a] >> (8 * b)) & 0xFFu) << (8 * a);
+        colrow[b] = w;
+    }
+    const uint32_t *pbP = seqb + dP.b_off, *pbQ = seqb + dQ.b_off;
+    const uint32_t wP0 = pbP[0], wP1 = pbP[1], wQ0 = pbQ[0], wQ1 = pbQ[1];
+    uint32_t colP[MM], colQ[MM], V[MM + 1];
+#pragma unroll
+    for (int j = 0; j < MM; ++j) {
+        const uint32_t bp = ((j < 16 ? wP0 : wP1) >> (2 * (j & 15))) & 3u;
+        const uint32_t bq = ((j < 16 ? wQ0 : wQ1) >> (2 * (j & 15))) & 3u;
+        colP[j] = (bp & 2u) ? ((bp & 1u) ? colrow[3] : colrow[2]) : ((bp & 1u) ? colrow[1] : colrow[0]);
+        colQ[j] = (bq & 2u) ? ((bq & 1u) ? colrow[3] : colrow[2]) : ((bq & 1u) ? colrow[1] : colrow[0]);
+    }
+#pragma unroll
+    for (int j = 0; j <= MM; ++j) V[j] = (uint32_t)j * kins;  // row 0: j inserts, both halves
+    const uint32_t *paP = seqa + dP.a_off, *paQ = seqa + dQ.a_off;
+    uint32_t waP = 0, waQ = 0, colv = 0;
+    for (int i = 0; i < n; ++i) {
+        if ((i & 15) == 0) {
+            waP = paP[i >> 4];
+            waQ = paQ[i >> 4];
+        }
+        const uint32_t aP = (waP >> (2 * (i & 15))) & 3u, aQ = (waQ >> (2 * (i & 15))) & 3u;
+        // perm: byte0 <- colP byte aP (S1), byte2 <- colQ byte aQ (S0), bytes 1, 3 <- 0
+        const uint32_t sel = 0x0C000C00u | aP | ((4u + aQ) << 16);
+        uint32_t dg = pk_add(V[0], __builtin_amdgcn_perm(colQ[0], colP[0], sel));
+        colv += kdel;  // column 0: i deletes
+        V[0] = colv;
+        uint32_t left = colv;
+#pragma unroll
+        for (int j = 1; j <= MM; ++j) {
+            const uint32_t up = V[j];
+            const uint32_t cdel = pk_add(up, kdel);
+            const uint32_t dnext = j < MM ? pk_add(up, __builtin_amdgcn_perm(colQ[j], colP[j], sel)) : 0u;
+            const uint32_t v = pk_min(pk_min(pk_add(left, kins), cdel), dg);
+            dg = dnext;
+            V[j] = v;
+            left = v;
+        }
+    }
+    uint32_t capP = V[1], capQ = V[1];
+#pragma unroll
+    for (int j = 2; j <= MM; ++j) {
+        capP = (j == mP) ? V[j] : capP;
+        capQ = (j == mQ) ? V[j] : capQ;
+    }
+    sed_result r;
+    r.len = -1;
+    r.err = 0;
+    r.pad[0] = r.pad[1] = 0;
+    const uint32_t DP = capP & 0xFFFFu, DQ = capQ >> 16;
+    r.dist = (double)DP;
+    r.is_int = (DP == 0);
+    res[P] = r;
+    r.dist = (double)DQ;
+    r.is_int = (DQ == 0);
+    res[Q] = r;
+}
+
 // fp64 distance-only variant (SED_MODE_F64 = "simple typing", SED_NO_LEN): short pairs whose
 // alphabet or costs rule out the integer keys (IUPAC codes, N in piRNA data; config 5 with N).
 // Cells follow the reference exactly: borders j*insert and i*delete are products
@@ -199,6 +291,13 @@ hipError_t sed_launch_lane_f64(const sed_launch &L, const int32_t *idx, int nidx
     if (nidx <= 0) return hipSuccess;
     hipLaunchKernelGGL((sed_lane_f64_kernel<SED_LANE_MAXM>), dim3((nidx + 255) / 256), dim3(256), 0, L.stream, L.pd,
                        idx, nidx, (const uint8_t *)L.seqa, (const uint8_t *)L.seqb, L.res, gtab, ins, del, K);
+    return hipGetLastError();
+}
+
+hipError_t sed_launch_lane_i32x2(const sed_launch &L, const int32_t *idx, int nlanes, const sed_i32_params &prm) {
+    if (nlanes <= 0) return hipSuccess;
+    hipLaunchKernelGGL(sed_lane_i32x2_kernel, dim3((nlanes + 255) / 256), dim3(256), 0, L.stream, L.pd, idx, nlanes,
+                       (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.res, prm);
     return hipGetLastError();
 }
 

@@ -88,6 +88,7 @@ struct sed_batch {
     DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops, d_tasks, d_prog, d_lane, d_chain;
     bool split = false;
     int nlane = 0, nwave = 0;  // pairs on the lane-per-pair kernel / on the wave kernels
+    int nlane_x2 = 0;          // > 0: lane pairs run two per lane (distance only), in this many lanes
     int nchains = 0;           // CHAIN mode: wave pairs run as nchains back-to-back chains (0 = off)
     size_t chain_npairs = 0;   // d_chain = [chain_pairs (chain_npairs) | chain_off (nchains + 1) | counter]
     bool chain_dyn = false;    // persistent waves + device counter instead of static chains
@@ -308,6 +309,23 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     b->bnd_words = bndw;
     b->nlane = (int)lane_idx.size();
     b->nwave = npairs - b->nlane;
+    // distance-only integer lane pairs: two pairs of equal n per lane (sed_lane.hip: i32x2). Stable
+    // sort by n, pair neighbours of equal n; a pair without a partner shares its lane with itself.
+    b->nlane_x2 = 0;
+    if (mode == SED_MODE_I32 && !want_tb && (flags & SED_NO_LEN) && c->opt_lane != 3 && !lane_idx.empty()) {
+        std::stable_sort(lane_idx.begin(), lane_idx.end(), [&](int32_t x, int32_t y) { return len_a[x] < len_a[y]; });
+        std::vector<int32_t> two;
+        two.reserve(lane_idx.size() + 1);
+        for (size_t q = 0; q < lane_idx.size();) {
+            const int32_t x = lane_idx[q];
+            const bool partner = q + 1 < lane_idx.size() && len_a[lane_idx[q + 1]] == len_a[x];
+            two.push_back(x);
+            two.push_back(partner ? lane_idx[q + 1] : x);
+            q += partner ? 2 : 1;
+        }
+        lane_idx.swap(two);
+        b->nlane_x2 = (int)(lane_idx.size() / 2);
+    }
 
     // ---- CHAIN mode (integer keys): single-stripe wave pairs run back to back, one chain per
     // wave, so each pair's 63-step ramp overlaps the previous pair's drain (sed_kernels.hip) ----
@@ -508,7 +526,9 @@ int run_batch(sed_batch *b) {
         if (e != hipSuccess) return c->hipfail(e, "DP kernel launch");
     }
     if (b->nlane > 0) {
-        if (b->mode == SED_MODE_I32)
+        if (b->nlane_x2 > 0)
+            e = sed_launch_lane_i32x2(L, (const int32_t *)b->d_lane.p, b->nlane_x2, ip);
+        else if (b->mode == SED_MODE_I32)
             e = sed_launch_lane_i32(L, (const int32_t *)b->d_lane.p, b->nlane, ip, len);
         else
             e = sed_launch_lane_f64(L, (const int32_t *)b->d_lane.p, b->nlane, (const double *)c->gtab.p, c->ins,
@@ -614,7 +634,7 @@ int sed_set_option(sed_ctx *c, int key, int value) {
         c->opt_split = value;
         return SED_OK;
     }
-    if (key == SED_OPT_LANE && value >= 0 && value <= 2) {
+    if (key == SED_OPT_LANE && value >= 0 && value <= 3) {
         c->opt_lane = value;
         return SED_OK;
     }
@@ -683,6 +703,7 @@ int sed_batch_mode(const sed_batch *b) { return b ? b->mode : SED_E_ARG; }
 int sed_batch_rows_per_lane(const sed_batch *b) { return b ? b->R : SED_E_ARG; }
 int sed_batch_lane_pairs(const sed_batch *b) { return b ? b->nlane : SED_E_ARG; }
 int sed_batch_chains(const sed_batch *b) { return b ? b->nchains : SED_E_ARG; }
+int sed_batch_lane_x2(const sed_batch *b) { return b ? b->nlane_x2 : SED_E_ARG; }
 
 int sed_batch_run(sed_batch *b) {
     if (!b) return SED_E_ARG;

@@ -44,6 +44,7 @@ SIGNATURES = [
     ("sed_batch_rows_per_lane", C.c_int, [C.c_void_p]),
     ("sed_batch_lane_pairs", C.c_int, [C.c_void_p]),
     ("sed_batch_chains", C.c_int, [C.c_void_p]),
+    ("sed_batch_lane_x2", C.c_int, [C.c_void_p]),
     ("sed_batch_run", C.c_int, [C.c_void_p]),
     ("sed_batch_sync", C.c_int, [C.c_void_p]),
     ("sed_batch_last_times", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
@@ -247,6 +248,11 @@ class Batch:
     @property
     def chains(self):
         return self._lib.sed_batch_chains(self.ptr)
+
+    @property
+    def lane_x2(self):
+        """Lanes running two distance-only pairs each (packed 16-bit cells); 0 = one pair per lane."""
+        return self._lib.sed_batch_lane_x2(self.ptr)
 
     def run(self):
         self.ctx._check(self._lib.sed_batch_run(self.ptr), "sed_batch_run")

@@ -277,3 +277,25 @@ def test_large_pairs_across_the_integer_key_limits(gpu, tables):
         assert b.mode == ("i32" if len(pairs[0][0]) == 12000 else "f64")
         b.close()
         _oracle_check(tables[True], pairs, gpu_run(gpu, tables[True], pairs))
+
+
+@pytest.mark.parametrize("user", [False, True])
+def test_lane_x2_packed_distance_vs_oracle(gpu, tables, user):
+    """Distance-only lane pairs run two per lane in 16-bit halves (pairs of equal n; a pair without
+    a partner shares its lane with itself).  Same results as one pair per lane and as the oracle."""
+    rng = np.random.default_rng(404 + user)
+    pairs = []
+    for _ in range(500):
+        n = int(rng.choice([rng.integers(1, 8), rng.integers(20, 33), rng.integers(1, 513)]))
+        m = int(rng.integers(1, 33))
+        pairs.append(("".join(rng.choice(list("ACGU"), size=n)), "".join(rng.choice(list("ACGU"), size=m))))
+    pairs += [("A", "A"), ("G" * 512, "C" * 32), ("ACGU" * 128, "U"), ("C" * 511, "A" * 32)]
+    plan = sedcost.build_plan(tables[user], [a for a, _ in pairs], [b for _, b in pairs])
+    gpu.set_costs(plan)
+    b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs],
+                                             [plan.encode(y) for _, y in pairs]), False, no_len=True)
+    assert b.lane_pairs == len(pairs) and (len(pairs) + 1) // 2 <= b.lane_x2 < len(pairs)
+    b.close()
+    got = gpu_run(gpu, tables[user], pairs, script=False, no_len=True)
+    _oracle_check(tables[user], pairs, got, no_len=True)
+    assert got == gpu_run(gpu, tables[user], pairs, script=False, no_len=True, lane=3)
