@@ -101,27 +101,16 @@ __device__ __forceinline__ void store_tb(uint32_t *p, const uint32_t (&w)[4]) {
 // reset to its column-0 state right before its first step, and a lane past
 // column m computes columns that nothing reads.
 // ---------------------------------------------------------------------------
-#ifndef SED_I32_LDS_CHUNK
-#define SED_I32_LDS_CHUNK 1  // lane 0's per-step inputs from an LDS broadcast read instead of DPP rotations
-#endif
-
 // One column step of a lane's R rows.  tv = {top, sel} of this step's column
 // for lane 0 (the stripe's top row and str2 symbol): every lane reads the same
 // LDS word, only lane 0 keeps it (the DPP move's `old` operand).
 template <int R, bool TB, bool LEN>
 __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
-                                         uint32_t &bottom, uint32_t &selv, uint32_t &tch, uint32_t &sch,
-                                         const uint2 tv, uint32_t &outc, uint32_t (&W)[4], const int u,
+                                         uint32_t &bottom, uint32_t &selv, const uint2 tv, uint32_t &outc,
+                                         uint32_t (&W)[4], const int u,
                                          const uint32_t kins, const uint32_t kdel) {
-#if SED_I32_LDS_CHUNK
     const uint32_t topv = dpp_shr1(tv.x, bottom);  // cell above the band, this column
     selv = dpp_shr1(tv.y, selv);                   // perm selector of this column's str2 symbol
-#else
-    const uint32_t topv = dpp_shr1(tch, bottom);
-    selv = dpp_shr1(sch, selv);
-    tch = dpp_rol1(tch);
-    sch = dpp_rol1(sch);
-#endif
     uint32_t up = topv, diag = top_prev;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -172,8 +161,8 @@ __device__ __forceinline__ void i32_reset(uint32_t (&V)[R], uint32_t &top_prev, 
 // another merge point where the register allocator inserts copies of the whole state.
 template <int R, bool TB, bool LEN, bool SLOW>
 __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
-                                          uint32_t &bottom, uint32_t &selv, uint32_t &tch, uint32_t &sch,
-                                          const uint2 *__restrict__ lch, uint32_t &outc, uint32_t (&W)[4],
+                                          uint32_t &bottom, uint32_t &selv, const uint2 *__restrict__ lch,
+                                          uint32_t &outc, uint32_t (&W)[4],
                                           const int s0, const int lane, const uint32_t kins, const uint32_t kdel,
                                           const bool ramp, const int cap_step, const int cap_lane, const int cap_row,
                                           uint32_t &cap) {
@@ -185,13 +174,13 @@ __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)
     uint2 tv[G];
     const uint2 *lp = lch + (s0 & 63);  // G divides 64: a group never wraps the chunk
 #pragma unroll
-    for (int u = 0; u < G; ++u) tv[u] = SED_I32_LDS_CHUNK ? lp[u] : make_uint2(0, 0);
+    for (int u = 0; u < G; ++u) tv[u] = lp[u];
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         const int s = s0 + u;
         uint32_t ki = kin;
         if constexpr (SLOW) ki = ramp ? (kin & ~(uint32_t)((s - lane) >> 31)) : kin;  // virtual column: insert adds nothing
-        i32_step<R, TB, LEN>(V, cv, top_prev, bottom, selv, tch, sch, tv[u], outc, W, u, ki, kde);
+        i32_step<R, TB, LEN>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u, ki, kde);
         if constexpr (SLOW) {
             const bool hit = (s == cap_step) && (lane == cap_lane);
 #pragma unroll
@@ -319,7 +308,7 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             return 0x0C000100u | ((4u + b) << 16);  // perm: byte2 <- cost byte b, bytes1:0 <- 6
         };
         uint32_t tch = load_top(0), sch = load_sel(0);
-        if (SED_I32_LDS_CHUNK) lch[lane] = make_uint2(tch, sch);
+        lch[lane] = make_uint2(tch, sch);
         uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * 256u;
         const bool last = (k == nstripes - 1);
         const int cap_step = last ? m - 1 + cap_lane : -1;
@@ -330,10 +319,10 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             for (int g = 0; g < 64 / G && s < SG; ++g, s += G) {
                 const bool capg = cap_step >= s && cap_step < s + G;
                 if (s < 63 || capg)
-                    i32_group<R, TB, LEN, true>(V, cv, top_prev, bottom, selv, tch, sch, lch, outc, W, s, lane, kins,
+                    i32_group<R, TB, LEN, true>(V, cv, top_prev, bottom, selv, lch, outc, W, s, lane, kins,
                                                 kdel, s < 63, cap_step, cap_lane, cap_row, cap);
                 else
-                    i32_group<R, TB, LEN, false>(V, cv, top_prev, bottom, selv, tch, sch, lch, outc, W, s, lane, kins,
+                    i32_group<R, TB, LEN, false>(V, cv, top_prev, bottom, selv, lch, outc, W, s, lane, kins,
                                                  kdel, false, cap_step, cap_lane, cap_row, cap);
                 if constexpr (TB) {
                     uint32_t *gp = tbk + (uint64_t)(s / G) * 256u;  // wave-uniform base, per-lane 16-byte offset
@@ -349,7 +338,7 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             }
             tch = tnx;
             sch = snx;
-            if (SED_I32_LDS_CHUNK) lch[lane] = make_uint2(tch, sch);  // after the chunk's last LDS read (in order)
+            lch[lane] = make_uint2(tch, sch);  // after the chunk's last LDS read (in order)
         }
         if (!last) __builtin_amdgcn_s_waitcnt(0);  // own bottom-row stores done before the next stripe reads them
     }
@@ -424,13 +413,12 @@ __device__ __forceinline__ void i32_chain_group(uint32_t (&V)[R], uint32_t (&cv)
     const uint2 *lp = lch + (s0 & 63);
 #pragma unroll
     for (int u = 0; u < G; ++u) tv[u] = lp[u];
-    uint32_t tch = 0, sch = 0;
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         const int s = s0 + u;
         uint32_t ki = kin;
         if constexpr (GEN) ki = ramp ? (kin & ~(uint32_t)((s - lane) >> 31)) : kin;
-        i32_step<R, TB, LEN>(V, cv, top_prev, bottom, selv, tch, sch, tv[u], outc, W, u, ki, kde);
+        i32_step<R, TB, LEN>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u, ki, kde);
         if constexpr (GEN) {
             const bool hA = (s == csA) && (lane == clA), hB = (s == csB) && (lane == clB);
 #pragma unroll
