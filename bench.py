@@ -43,7 +43,7 @@ SIMDS, CLOCK = 1024, 2.4e9
 # the nominal 2-cycle ops do not pair when interleaved with the 4-cycle v_perm/v_min3/v_alignbit).
 # Ops per cell: perm + 3 add + min3 (+ and for the op-count field) (+ alignbit for the traceback).
 VALU_CYCLES_PER_OP = 4.0
-CELL_OPS = {"script": 7, "len": 6, "nolen": 5}
+CELL_OPS = {"script": 7, "len": 6, "nolen": 5, "nolen_x2": 3}  # x2: 6 packed 16-bit ops per 2 cells
 
 WORKLOADS = {
     # name: (pairs per GPU, n, m, cost table, description)
@@ -150,7 +150,8 @@ def main():
                     help="run DP and traceback back to back on one stream (no overlap across steps)")
     ap.add_argument("--rows-per-lane", type=int, default=0)
     ap.add_argument("--no-lane", action="store_true", help="route short pairs to the wave kernels too (A/B)")
-    ap.add_argument("--no-lane-x2", action="store_true", help="distance-only lane pairs one per lane (no 16-bit packing)")
+    ap.add_argument("--no-pack", action="store_true",
+                    help="distance-only pairs one per lane / wave (no packed 16-bit cells; A/B)")
     ap.add_argument("--split", type=int, default=0, help="SED_OPT_SPLIT: 0 auto, 1 force, 2 off (A/B)")
     ap.add_argument("--chain", type=int, default=0,
                     help="SED_OPT_CHAIN: 0 auto, 1 force, 2 off, L>=3 force with chains of L pairs (A/B)")
@@ -212,8 +213,8 @@ def main():
         ctx.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, args.rows_per_lane)
     if args.no_lane:
         ctx.set_option(sedgpu.SED_OPT_LANE, 2)
-    elif args.no_lane_x2:
-        ctx.set_option(sedgpu.SED_OPT_LANE, 3)
+    if args.no_pack:
+        ctx.set_option(sedgpu.SED_OPT_PACK, 2)
     if args.chain:
         ctx.set_option(sedgpu.SED_OPT_CHAIN, args.chain)
     if args.split:
@@ -311,23 +312,29 @@ def main():
             pm = json.load(f)
         if pm.get("workload") == desc and batch.mode == "i32" and want_script and P == WORKLOADS[args.workload][0]:
             traffic = pm.get("hbm_bytes_per_launch")
-    ops_cell = CELL_OPS["script" if want_script else "nolen"] if batch.mode == "i32" else None
+    nl, npk = batch.lane_pairs, batch.packed_pairs
+    lane_x2 = batch.mode == "i32" and not want_script and nl > 0 and not args.no_pack
+    wave_x2 = npk - (nl if lane_x2 else 0)  # wave pairs computed two per wave
+    ops_cell = None
+    if batch.mode == "i32":
+        ops_cell = CELL_OPS["script" if want_script else ("nolen_x2" if npk == P else "nolen")]
     valu_peak = SIMDS * CLOCK * 64 / (VALU_CYCLES_PER_OP * ops_cell) if ops_cell else None
     rate = cells / (dp_avg * 1e-3)
-    nl = batch.lane_pairs
     if batch.mode != "i32":
-        kname = "sed_lane_f64_kernel" if nl == P else ("sed_wf_f64_kernel" if nl == 0 else
-                                                       "sed_wf_f64_kernel+sed_lane_f64_kernel")
+        parts = (["sed_wf_f64_kernel"] if nl < P else []) + (["sed_lane_f64_kernel"] if nl else [])
     else:
-        kname = "sed_lane_i32_kernel" if nl == P else ("sed_wf_i32_kernel" if nl == 0 else
-                                                       "sed_wf_i32_kernel+sed_lane_i32_kernel")
+        wave_k = "sed_wf_i32_chain_kernel" if batch.chains else "sed_wf_i32_kernel"
+        parts = ((["sed_wf_i32x2_kernel"] if wave_x2 else []) + ([wave_k] if nl + wave_x2 < P else []) +
+                 ([("sed_lane_i32x2_kernel" if lane_x2 else "sed_lane_i32_kernel")] if nl else []))
+    kname = "+".join(parts)
     line = {
         "metric": METRIC, "value": value, "unit": "cells/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u32" if batch.mode == "i32" else "f64", "data": "synthetic",
         "config": {"workload": desc, "pairs_per_gpu": P, "n": n, "m": m, "costs": costs_file,
                    "script": want_script, "pipeline": pipeline, "mode": batch.mode,
-                   "rows_per_lane": batch.rows_per_lane, "lane_pairs": nl, "chains": batch.chains,
+                   "rows_per_lane": batch.rows_per_lane, "lane_pairs": nl, "packed_pairs": npk,
+                   "chains": batch.chains,
                    "parallelism": "dp%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -59,11 +59,12 @@ enum {
 #define SED_OPT_ROWS_PER_LANE 2 /* 0 auto, else 4,8,16,32 (integer) / 4,8 (fp64) */
 #define SED_OPT_SPLIT 3         /* integer kernel, one wave per stripe: 0 auto (small batches of long
                                    pairs), 1 always, 2 never */
-#define SED_OPT_LANE 4          /* one lane per pair for short str2 (m <= 32, n <= 512): 0 auto (on), 2 never,
-                                   3 on but never two pairs per lane (distance-only batches pack two by default) */
+#define SED_OPT_LANE 4          /* one lane per pair for short str2 (m <= 32, n <= 512): 0 auto (on), 2 never */
 #define SED_OPT_CHAIN 5         /* integer kernel, single-stripe pairs run back to back in one wave (no
                                    per-pair ramp): 0 auto (large batches), 1 whenever eligible, 2 never,
                                    L >= 3 whenever eligible with chains of L pairs */
+#define SED_OPT_PACK 6          /* distance-only integer batches (SED_NO_LEN): two pairs per lane (equal n) or per
+                                   wave (equal n and m) in packed 16-bit cells: 0 auto (on), 2 never */
 
 /* modes reported by sed_batch_mode */
 #define SED_MODE_I32 1
@@ -111,8 +112,7 @@ int sed_batch_mode(const sed_batch *b);               /* SED_MODE_* chosen for t
 int sed_batch_rows_per_lane(const sed_batch *b);
 int sed_batch_lane_pairs(const sed_batch *b);         /* pairs on the lane-per-pair kernel (short str2) */
 int sed_batch_chains(const sed_batch *b);             /* CHAIN mode: number of chains (0 = not used) */
-int sed_batch_lane_x2(const sed_batch *b);            /* distance-only lane pairs packed two per lane: lanes used
-                                                          (0 = one pair per lane) */
+int sed_batch_packed_pairs(const sed_batch *b);       /* pairs computed two per lane / wave (SED_OPT_PACK) */
 int sed_batch_run(sed_batch *b);                      /* enqueue on the context stream, returns at once */
 int sed_batch_sync(sed_batch *b);                     /* wait for the last run */
 /* device time of the last run, from HIP events on the launching stream (ms) */

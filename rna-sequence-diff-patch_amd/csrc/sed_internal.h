@@ -84,6 +84,8 @@ hipError_t sed_launch_f64_full(const sed_launch &L, const double *gtab, const se
 #define SED_LANE_MAXM 32
 #define SED_LANE_MAXN 512
 hipError_t sed_launch_lane_i32(const sed_launch &L, const int32_t *idx, int nidx, const sed_i32_params &prm, bool len);
+// distance only, two pairs of equal shape per wave (packed 16-bit cells); list holds 2 * nwaves pair indices
+hipError_t sed_launch_i32x2(const sed_launch &L, const int32_t *list, int nwaves, const sed_i32_params &prm);
 // distance only, two pairs of equal n per lane (packed 16-bit cells); idx holds 2 * nlanes pair indices
 hipError_t sed_launch_lane_i32x2(const sed_launch &L, const int32_t *idx, int nlanes, const sed_i32_params &prm);
 // fp64 distance-only lane kernel (SED_MODE_F64 with SED_NO_LEN): gtab = the {value, flag} table.

@@ -352,6 +352,155 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
 }
 
 // ---------------------------------------------------------------------------
+// Distance only, two pairs per wave (SED_NO_LEN batches of equal-shape pairs): pair P in the low
+// 16 bits of every cell word, pair Q in the high 16 bits.  A distance key is D alone, below
+// 2^16 - 256 (the integer-mode bound), so the halves never wrap into each other and packed 16-bit
+// ops do two cells at once: perm + 3 v_pk_add_u16 + 2 v_pk_min_u16 = 6 VALU / 2 cells instead
+// of 5 VALU / cell.  The rest is the stripe kernel's schedule (virtual-column ramp, lane-0 LDS
+// chunk, in-place bottom rows in P's buffer); both pairs have the same n and m, so they share the
+// stripes, the steps and the sink cell.
+// ---------------------------------------------------------------------------
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t,
+                              __builtin_elementwise_min(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+}
+#define SED_SEL_SENT_X2 0x0C0D0C0Du  // both halves: update cost 0xFF (virtual columns)
+
+template <int R, bool SLOW>
+__device__ __forceinline__ void x2_group(uint32_t (&V)[R], const uint32_t (&cP)[R], const uint32_t (&cQ)[R],
+                                         uint32_t &top_prev, uint32_t &bottom, uint32_t &selv,
+                                         const uint2 *__restrict__ lch, uint32_t &outc, const int s0, const int lane,
+                                         const uint32_t kins, const uint32_t kdel, const bool ramp,
+                                         const int cap_step, const int cap_lane, const int cap_row, uint32_t &cap) {
+    constexpr int G = Grp<R>::G;
+    uint32_t kin = kins, kde = kdel;
+    asm volatile("" : "+v"(kin), "+v"(kde));  // see i32_group
+    uint2 tv[G];
+    const uint2 *lp = lch + (s0 & 63);
+#pragma unroll
+    for (int u = 0; u < G; ++u) tv[u] = lp[u];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+        const int s = s0 + u;
+        uint32_t ki = kin;
+        if constexpr (SLOW) ki = ramp ? (kin & ~(uint32_t)((s - lane) >> 31)) : kin;
+        const uint32_t topv = dpp_shr1(tv[u].x, bottom);
+        selv = dpp_shr1(tv[u].y, selv);
+        uint32_t up = topv, diag = top_prev;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t left = V[r];
+            const uint32_t mm = pk_min(pk_min(pk_add(left, ki), pk_add(up, kde)),
+                                       pk_add(diag, __builtin_amdgcn_perm(cQ[r], cP[r], selv)));
+            diag = left;
+            up = mm;
+            V[r] = mm;
+        }
+        top_prev = topv;
+        bottom = V[R - 1];
+        outc = dpp_shl1(bottom, outc);
+        if constexpr (SLOW) {
+            const bool hit = (s == cap_step) && (lane == cap_lane);
+#pragma unroll
+            for (int r = 0; r < R; ++r) cap = (hit && r == cap_row) ? V[r] : cap;
+        }
+    }
+}
+
+// occupancy targets with room for both pairs' cost rows (2R) next to the packed row values (R)
+template <int R> struct X2Waves { static constexpr int value = R >= 32 ? 3 : (R == 16 ? 5 : (R == 8 ? 7 : 8)); };
+template <int R>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(X2Waves<R>::value))) void
+sed_wf_i32x2_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restrict__ list, int nwaves,
+                    const uint32_t *__restrict__ seqa, const uint32_t *__restrict__ seqb,
+                    uint32_t *__restrict__ bnd, sed_result *__restrict__ res, sed_i32_params prm) {
+    constexpr int ROWS = 64 * R;
+    constexpr int G = Grp<R>::G;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (w >= nwaves) return;
+    const int P = __builtin_amdgcn_readfirstlane(list[2 * w]), Q = __builtin_amdgcn_readfirstlane(list[2 * w + 1]);
+    const sed_pair_desc dP = pd[P], dQ = pd[Q];
+    const int n = dP.n, m = dP.m;  // host: dQ has the same n, m >= 1
+    const uint32_t kins = prm.ins * 0x10001u, kdel = prm.del * 0x10001u;
+    const int nstripes = (n + ROWS - 1) / ROWS;
+    const int SG = (m + 63 + G - 1) / G * G;
+    const int nchunks = (SG + 63) >> 6;
+    const uint32_t *paP = seqa + dP.a_off, *paQ = seqa + dQ.a_off;
+    const uint32_t *pbP = seqb + dP.b_off, *pbQ = seqb + dQ.b_off;
+    const int wsink = (n - 1) % ROWS;
+    const int cap_lane = wsink / R, cap_row = wsink % R;
+    uint32_t cap = 0;
+    __shared__ uint2 lds_chunk[4][64];
+    uint2 *lch = lds_chunk[threadIdx.x >> 6];
+    uint32_t *bnd_io = bnd + dP.bnd_off;  // in place, as in the stripe kernel
+
+    for (int k = 0; k < nstripes; ++k) {
+        const int row0 = k * ROWS + lane * R;
+        uint32_t cP[R], cQ[R], V[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int ri = row0 + r;
+            const uint32_t aP = (paP[ri >> 4] >> ((ri & 15) * 2)) & 3u, aQ = (paQ[ri >> 4] >> ((ri & 15) * 2)) & 3u;
+            cP[r] = aP == 0 ? prm.costrow[0] : aP == 1 ? prm.costrow[1] : aP == 2 ? prm.costrow[2] : prm.costrow[3];
+            cQ[r] = aQ == 0 ? prm.costrow[0] : aQ == 1 ? prm.costrow[1] : aQ == 2 ? prm.costrow[2] : prm.costrow[3];
+        }
+        uint32_t top_prev = (uint32_t)row0 * kdel;  // column 0: i deletes, both halves
+#pragma unroll
+        for (int r = 0; r < R; ++r) V[r] = (uint32_t)(row0 + r + 1) * kdel;
+        uint32_t bottom = V[R - 1], selv = SED_SEL_SENT_X2, outc = 0;
+        auto load_top = [&](int c) -> uint32_t {
+            const int j = 64 * c + lane + 1;
+            if (k == 0) return (uint32_t)j * kins;  // row 0: j inserts
+            return load_sc1(bnd_io + j + 64);
+        };
+        auto load_sel = [&](int c) -> uint32_t {
+            const int ci = 64 * c + lane;
+            const uint32_t bp = (pbP[ci >> 4] >> ((ci & 15) * 2)) & 3u, bq = (pbQ[ci >> 4] >> ((ci & 15) * 2)) & 3u;
+            return 0x0C000C00u | bp | ((4u + bq) << 16);  // byte0 <- cP byte bP, byte2 <- cQ byte bQ
+        };
+        uint32_t tch = load_top(0), sch = load_sel(0);
+        lch[lane] = make_uint2(tch, sch);
+        const bool last = (k == nstripes - 1);
+        const int cap_step = last ? m - 1 + cap_lane : -1;
+        int s = 0;
+        for (int c = 0; c < nchunks; ++c) {
+            uint32_t tnx = 0, snx = 0;
+            if (c + 1 < nchunks) { tnx = load_top(c + 1); snx = load_sel(c + 1); }
+            for (int g = 0; g < 64 / G && s < SG; ++g, s += G) {
+                const bool capg = cap_step >= s && cap_step < s + G;
+                if (s < 63 || capg)
+                    x2_group<R, true>(V, cP, cQ, top_prev, bottom, selv, lch, outc, s, lane, kins, kdel, s < 63,
+                                      cap_step, cap_lane, cap_row, cap);
+                else
+                    x2_group<R, false>(V, cP, cQ, top_prev, bottom, selv, lch, outc, s, lane, kins, kdel, false,
+                                       cap_step, cap_lane, cap_row, cap);
+            }
+            if (!last) bnd_io[s - 62 + lane] = outc;
+            lch[lane] = make_uint2(tnx, snx);
+        }
+        if (!last) __builtin_amdgcn_s_waitcnt(0);
+    }
+    if (lane == cap_lane) {
+        sed_result r;
+        r.len = -1;
+        r.err = 0;
+        r.pad[0] = r.pad[1] = 0;
+        const uint32_t DP = cap & 0xFFFFu, DQ = cap >> 16;
+        r.dist = (double)DP;
+        r.is_int = (DP == 0);
+        res[P] = r;
+        r.dist = (double)DQ;
+        r.is_int = (DQ == 0);
+        res[Q] = r;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // CHAIN mode (integer keys, single-stripe pairs: n <= 64R).  One wave runs a chain of pairs
 // back to back so that a pair's 63-step wavefront ramp overlaps the previous pair's drain.
 // Pair q of the chain owns global steps [T_q, T_q + S_q) for lane 0, S_q = m_q rounded up to
@@ -1066,6 +1215,20 @@ hipError_t sed_launch_i32_chain(const sed_launch &L, const sed_i32_params &prm, 
 #undef CASE
     default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t sed_launch_i32x2(const sed_launch &L, const int32_t *list, int nwaves, const sed_i32_params &prm) {
+    if (nwaves <= 0) return hipSuccess;
+    const dim3 grid((nwaves + 3) / 4), block(256);
+    const uint32_t *a = (const uint32_t *)L.seqa, *b = (const uint32_t *)L.seqb;
+    switch (L.R) {
+    case 4: hipLaunchKernelGGL((sed_wf_i32x2_kernel<4>), grid, block, 0, L.stream, L.pd, list, nwaves, a, b, L.bnd, L.res, prm); break;
+    case 8: hipLaunchKernelGGL((sed_wf_i32x2_kernel<8>), grid, block, 0, L.stream, L.pd, list, nwaves, a, b, L.bnd, L.res, prm); break;
+    case 16: hipLaunchKernelGGL((sed_wf_i32x2_kernel<16>), grid, block, 0, L.stream, L.pd, list, nwaves, a, b, L.bnd, L.res, prm); break;
+    case 32: hipLaunchKernelGGL((sed_wf_i32x2_kernel<32>), grid, block, 0, L.stream, L.pd, list, nwaves, a, b, L.bnd, L.res, prm); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm, bool len) {

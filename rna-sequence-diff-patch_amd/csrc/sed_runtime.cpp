@@ -58,7 +58,7 @@ struct sed_ctx {
     int ins_int = 0, del_int = 0;
     DevBuf gtab;  // fp64 kernel table: per entry {value bits, is-int flag}
     // options
-    int opt_mode = 0, opt_R = 0, opt_split = 0, opt_lane = 0, opt_chain = 0;
+    int opt_mode = 0, opt_R = 0, opt_split = 0, opt_lane = 0, opt_chain = 0, opt_pack = 0;
     DevBuf selftest;
     sed_batch *scratch = nullptr;
 
@@ -85,10 +85,11 @@ struct sed_batch {
     std::vector<int32_t> n, m;
     uint64_t tb_words = 0, bnd_words = 0, ops_words = 0;
     double cells = 0, algo_bytes = 0;
-    DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops, d_tasks, d_prog, d_lane, d_chain;
+    DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops, d_tasks, d_prog, d_lane, d_chain, d_x2;
     bool split = false;
     int nlane = 0, nwave = 0;  // pairs on the lane-per-pair kernel / on the wave kernels
     int nlane_x2 = 0;          // > 0: lane pairs run two per lane (distance only), in this many lanes
+    int nwave_x2 = 0;          // distance-only wave pairs of equal shape run two per wave, in this many waves
     int nchains = 0;           // CHAIN mode: wave pairs run as nchains back-to-back chains (0 = off)
     size_t chain_npairs = 0;   // d_chain = [chain_pairs (chain_npairs) | chain_off (nchains + 1) | counter]
     bool chain_dyn = false;    // persistent waves + device counter instead of static chains
@@ -115,7 +116,7 @@ struct sed_batch {
     int cur() const { return (int)((runs - 1) % nbuf); }
     ~sed_batch() {
         d_pd.release(); d_seqa.release(); d_seqb.release(); d_bnd.release(); d_ops.release();
-        d_tasks.release(); d_prog.release(); d_lane.release(); d_chain.release();
+        d_tasks.release(); d_prog.release(); d_lane.release(); d_chain.release(); d_x2.release();
         for (int i = 0; i < 3; ++i) {
             d_tb[i].release();
             d_res[i].release();
@@ -312,7 +313,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // distance-only integer lane pairs: two pairs of equal n per lane (sed_lane.hip: i32x2). Stable
     // sort by n, pair neighbours of equal n; a pair without a partner shares its lane with itself.
     b->nlane_x2 = 0;
-    if (mode == SED_MODE_I32 && !want_tb && (flags & SED_NO_LEN) && c->opt_lane != 3 && !lane_idx.empty()) {
+    if (mode == SED_MODE_I32 && !want_tb && (flags & SED_NO_LEN) && c->opt_pack != 2 && !lane_idx.empty()) {
         std::stable_sort(lane_idx.begin(), lane_idx.end(), [&](int32_t x, int32_t y) { return len_a[x] < len_a[y]; });
         std::vector<int32_t> two;
         two.reserve(lane_idx.size() + 1);
@@ -325,6 +326,32 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         }
         lane_idx.swap(two);
         b->nlane_x2 = (int)(lane_idx.size() / 2);
+    }
+
+    // distance-only integer wave pairs: two of identical shape per wave (sed_kernels.hip: i32x2). They are
+    // marked lane = 2 so that the other wave kernels (and CHAIN mode) skip them.
+    std::vector<int32_t> x2;
+    b->nwave_x2 = 0;
+    if (mode == SED_MODE_I32 && !split && !want_tb && (flags & SED_NO_LEN) && c->opt_pack != 2 && b->nwave > 1) {
+        std::vector<int32_t> w;
+        for (int p = 0; p < npairs; ++p)
+            if (!b->pd[p].lane && len_a[p] > 0 && len_b[p] > 0) w.push_back(p);
+        std::stable_sort(w.begin(), w.end(), [&](int32_t x, int32_t y) {
+            return len_a[x] != len_a[y] ? len_a[x] < len_a[y] : len_b[x] < len_b[y];
+        });
+        for (size_t q = 0; q + 1 < w.size();) {
+            const int32_t x = w[q], y = w[q + 1];
+            if (len_a[x] == len_a[y] && len_b[x] == len_b[y]) {
+                x2.push_back(x);
+                x2.push_back(y);
+                b->pd[x].lane = b->pd[y].lane = 2;
+                q += 2;
+            } else {
+                ++q;
+            }
+        }
+        b->nwave_x2 = (int)(x2.size() / 2);
+        b->nwave -= (int)x2.size();
     }
 
     // ---- CHAIN mode (integer keys): single-stripe wave pairs run back to back, one chain per
@@ -397,7 +424,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
                    b->d_tasks.reserve(sizeof(int2) * std::max<size_t>(1, tasks.size())) &&
                    b->d_prog.reserve(4 * std::max<uint64_t>(1, progw)) &&
                    b->d_lane.reserve(4 * std::max<size_t>(1, lane_idx.size())) &&
-                   b->d_chain.reserve(4 * (chain_pairs.size() + chain_off.size() + 2));
+                   b->d_chain.reserve(4 * (chain_pairs.size() + chain_off.size() + 2)) &&
+                   b->d_x2.reserve(4 * std::max<size_t>(1, x2.size()));
     for (int i = 0; i < b->nbuf && okalloc; ++i)
         okalloc = b->d_res[i].reserve(sizeof(sed_result) * std::max(1, npairs)) &&
                   (!want_tb || b->d_tb[i].reserve(4 * std::max<uint64_t>(1, tbw)));
@@ -427,6 +455,9 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     if (!lane_idx.empty() && (e = hipMemcpyAsync(b->d_lane.p, lane_idx.data(), 4 * lane_idx.size(),
                                                  hipMemcpyHostToDevice, c->stream)) != hipSuccess)
         return c->hipfail(e, "upload lane list");
+    if (!x2.empty() && (e = hipMemcpyAsync(b->d_x2.p, x2.data(), 4 * x2.size(), hipMemcpyHostToDevice, c->stream)) !=
+                           hipSuccess)
+        return c->hipfail(e, "upload packed-wave list");
     for (int i = 0; i < b->nbuf; ++i)
         if ((e = hipMemsetAsync(b->d_res[i].p, 0, sizeof(sed_result) * std::max(1, npairs), c->stream)) != hipSuccess)
             return c->hipfail(e, "zero results");
@@ -506,6 +537,8 @@ int run_batch(sed_batch *b) {
         (e = hipMemsetAsync(b->d_prog.p, 0, 4 * b->prog_words, c->stream)) != hipSuccess)
         return c->hipfail(e, "memset progress");
     const bool len = want_tb || !(b->flags & SED_NO_LEN);
+    if (b->nwave_x2 > 0 && (e = sed_launch_i32x2(L, (const int32_t *)b->d_x2.p, b->nwave_x2, ip)) != hipSuccess)
+        return c->hipfail(e, "packed DP kernel launch");
     if (b->nwave > 0) {
         if (b->mode == SED_MODE_I32 && b->nchains) {
             L.chain_pairs = (const int32_t *)b->d_chain.p;
@@ -634,8 +667,12 @@ int sed_set_option(sed_ctx *c, int key, int value) {
         c->opt_split = value;
         return SED_OK;
     }
-    if (key == SED_OPT_LANE && value >= 0 && value <= 3) {
+    if (key == SED_OPT_LANE && value >= 0 && value <= 2) {
         c->opt_lane = value;
+        return SED_OK;
+    }
+    if (key == SED_OPT_PACK && (value == 0 || value == 2)) {
+        c->opt_pack = value;
         return SED_OK;
     }
     if (key == SED_OPT_CHAIN && value >= 0 && value <= 1024) {
@@ -703,7 +740,9 @@ int sed_batch_mode(const sed_batch *b) { return b ? b->mode : SED_E_ARG; }
 int sed_batch_rows_per_lane(const sed_batch *b) { return b ? b->R : SED_E_ARG; }
 int sed_batch_lane_pairs(const sed_batch *b) { return b ? b->nlane : SED_E_ARG; }
 int sed_batch_chains(const sed_batch *b) { return b ? b->nchains : SED_E_ARG; }
-int sed_batch_lane_x2(const sed_batch *b) { return b ? b->nlane_x2 : SED_E_ARG; }
+int sed_batch_packed_pairs(const sed_batch *b) {
+    return b ? (b->nlane_x2 > 0 ? b->nlane : 0) + 2 * b->nwave_x2 : SED_E_ARG;
+}
 
 int sed_batch_run(sed_batch *b) {
     if (!b) return SED_E_ARG;

@@ -19,6 +19,7 @@ SED_OPT_ROWS_PER_LANE = 2
 SED_OPT_SPLIT = 3
 SED_OPT_LANE = 4
 SED_OPT_CHAIN = 5
+SED_OPT_PACK = 6
 MODE_NAMES = {1: "i32", 2: "f64", 3: "f64-typed"}
 
 _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
@@ -44,7 +45,7 @@ SIGNATURES = [
     ("sed_batch_rows_per_lane", C.c_int, [C.c_void_p]),
     ("sed_batch_lane_pairs", C.c_int, [C.c_void_p]),
     ("sed_batch_chains", C.c_int, [C.c_void_p]),
-    ("sed_batch_lane_x2", C.c_int, [C.c_void_p]),
+    ("sed_batch_packed_pairs", C.c_int, [C.c_void_p]),
     ("sed_batch_run", C.c_int, [C.c_void_p]),
     ("sed_batch_sync", C.c_int, [C.c_void_p]),
     ("sed_batch_last_times", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
@@ -250,9 +251,9 @@ class Batch:
         return self._lib.sed_batch_chains(self.ptr)
 
     @property
-    def lane_x2(self):
-        """Lanes running two distance-only pairs each (packed 16-bit cells); 0 = one pair per lane."""
-        return self._lib.sed_batch_lane_x2(self.ptr)
+    def packed_pairs(self):
+        """Pairs computed two per lane / per wave in packed 16-bit cells (distance-only batches)."""
+        return self._lib.sed_batch_packed_pairs(self.ptr)
 
     def run(self):
         self.ctx._check(self._lib.sed_batch_run(self.ptr), "sed_batch_run")

@@ -20,7 +20,7 @@ OPCH = "idu"
 IUPAC = "AGCUYRWSKMDVHBN"
 
 
-def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len=False, chain=0):
+def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len=False, chain=0, pack=0):
     """Run (s1, s2) pairs through the engine; returns [(dist, is_int, len, opstr)]."""
     plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
     ctx.set_mode(mode)
@@ -28,6 +28,7 @@ def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len
     ctx.set_option(sedgpu.SED_OPT_SPLIT, split)
     ctx.set_option(sedgpu.SED_OPT_LANE, lane)
     ctx.set_option(sedgpu.SED_OPT_CHAIN, chain)
+    ctx.set_option(sedgpu.SED_OPT_PACK, pack)
     ctx.set_costs(plan)
     packed = sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs], [plan.encode(b) for _, b in pairs])
     dist, is_int, ln, ops = ctx.run(packed, script, no_len=no_len)
@@ -42,6 +43,7 @@ def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len
     ctx.set_option(sedgpu.SED_OPT_SPLIT, 0)
     ctx.set_option(sedgpu.SED_OPT_LANE, 0)
     ctx.set_option(sedgpu.SED_OPT_CHAIN, 0)
+    ctx.set_option(sedgpu.SED_OPT_PACK, 0)
     return out
 
 
@@ -294,8 +296,40 @@ def test_lane_x2_packed_distance_vs_oracle(gpu, tables, user):
     gpu.set_costs(plan)
     b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs],
                                              [plan.encode(y) for _, y in pairs]), False, no_len=True)
-    assert b.lane_pairs == len(pairs) and (len(pairs) + 1) // 2 <= b.lane_x2 < len(pairs)
+    assert b.lane_pairs == len(pairs) and b.packed_pairs == len(pairs)
     b.close()
     got = gpu_run(gpu, tables[user], pairs, script=False, no_len=True)
     _oracle_check(tables[user], pairs, got, no_len=True)
-    assert got == gpu_run(gpu, tables[user], pairs, script=False, no_len=True, lane=3)
+    assert got == gpu_run(gpu, tables[user], pairs, script=False, no_len=True, pack=2)
+
+
+@pytest.mark.parametrize("R", [0, 4, 8, 16])
+def test_wave_x2_packed_distance_vs_oracle(gpu, tables, R):
+    """Distance-only wave pairs of identical shape run two per wave in 16-bit halves; pairs without
+    a same-shape partner, lane pairs and empty pairs in the same batch take their usual kernels."""
+    rng = np.random.default_rng(808 + R)
+    shapes = [(40, 100), (300, 257), (700, 64), (1100, 90), (1, 40), (64, 33)]
+    pairs = []
+    for n, m in shapes:
+        for _ in range(int(rng.integers(2, 6))):
+            a = "".join(rng.choice(list("ACGU"), size=n))
+            b = "".join(rng.choice(list("ACGU"), size=m)) if rng.random() < 0.5 else \
+                "".join(c if rng.random() > 0.1 else rng.choice(list("ACGU")) for c in (a * 2)[:m])
+            pairs.append((a, b))
+    pairs += [("ACGU" * 10, "A" * 20), ("A" * 77, "C" * 91), ("", "ACG"), ("GG", "")]  # lane, single, empties
+    order = rng.permutation(len(pairs))
+    pairs = [pairs[i] for i in order]
+    user = bool(R & 8)
+    plan = sedcost.build_plan(tables[user], [a for a, _ in pairs], [b for _, b in pairs])
+    gpu.set_costs(plan)
+    gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, R)
+    gpu.set_option(sedgpu.SED_OPT_SPLIT, 2)  # a batch this small would otherwise run SPLIT (never packed)
+    b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs],
+                                             [plan.encode(y) for _, y in pairs]), False, no_len=True)
+    gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
+    gpu.set_option(sedgpu.SED_OPT_SPLIT, 0)
+    assert b.packed_pairs >= 12
+    b.close()
+    got = gpu_run(gpu, tables[user], pairs, R=R, split=2, script=False, no_len=True)
+    _oracle_check(tables[user], pairs, got, no_len=True)
+    assert got == gpu_run(gpu, tables[user], pairs, R=R, split=2, script=False, no_len=True, pack=2)
