@@ -352,13 +352,14 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
 }
 
 // ---------------------------------------------------------------------------
-// Distance only, two pairs per wave (SED_NO_LEN batches of equal-shape pairs): pair P in the low
+// Distance only, two pairs per wave (SED_NO_LEN batches, pairs of equal n): pair P in the low
 // 16 bits of every cell word, pair Q in the high 16 bits.  A distance key is D alone, below
 // 2^16 - 256 (the integer-mode bound), so the halves never wrap into each other and packed 16-bit
 // ops do two cells at once: perm + 3 v_pk_add_u16 + 2 v_pk_min_u16 = 6 VALU / 2 cells instead
 // of 5 VALU / cell.  The rest is the stripe kernel's schedule (virtual-column ramp, lane-0 LDS
-// chunk, in-place bottom rows in P's buffer); both pairs have the same n and m, so they share the
-// stripes, the steps and the sink cell.
+// chunk, in-place bottom rows in P's buffer, which the host makes the pair with the larger m); both
+// pairs have the same n, so they share stripes and rows, and the wave runs max(m) columns, the
+// shorter pair's extra columns being don't-care.  Each pair's sink is captured at its own step.
 // ---------------------------------------------------------------------------
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
@@ -375,7 +376,8 @@ __device__ __forceinline__ void x2_group(uint32_t (&V)[R], const uint32_t (&cP)[
                                          uint32_t &top_prev, uint32_t &bottom, uint32_t &selv,
                                          const uint2 *__restrict__ lch, uint32_t &outc, const int s0, const int lane,
                                          const uint32_t kins, const uint32_t kdel, const bool ramp,
-                                         const int cap_step, const int cap_lane, const int cap_row, uint32_t &cap) {
+                                         const int capP_step, const int capQ_step, const int cap_lane,
+                                         const int cap_row, uint32_t &capP, uint32_t &capQ) {
     constexpr int G = Grp<R>::G;
     uint32_t kin = kins, kde = kdel;
     asm volatile("" : "+v"(kin), "+v"(kde));  // see i32_group
@@ -404,9 +406,12 @@ __device__ __forceinline__ void x2_group(uint32_t (&V)[R], const uint32_t (&cP)[
         bottom = V[R - 1];
         outc = dpp_shl1(bottom, outc);
         if constexpr (SLOW) {
-            const bool hit = (s == cap_step) && (lane == cap_lane);
+            const bool hP = (s == capP_step) && (lane == cap_lane), hQ = (s == capQ_step) && (lane == cap_lane);
 #pragma unroll
-            for (int r = 0; r < R; ++r) cap = (hit && r == cap_row) ? V[r] : cap;
+            for (int r = 0; r < R; ++r) {
+                capP = (hP && r == cap_row) ? V[r] : capP;
+                capQ = (hQ && r == cap_row) ? V[r] : capQ;
+            }
         }
     }
 }
@@ -425,7 +430,7 @@ sed_wf_i32x2_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restr
     if (w >= nwaves) return;
     const int P = __builtin_amdgcn_readfirstlane(list[2 * w]), Q = __builtin_amdgcn_readfirstlane(list[2 * w + 1]);
     const sed_pair_desc dP = pd[P], dQ = pd[Q];
-    const int n = dP.n, m = dP.m;  // host: dQ has the same n, m >= 1
+    const int n = dP.n, m = dP.m, mQ = dQ.m;  // host: dQ.n == n, 1 <= mQ <= m
     const uint32_t kins = prm.ins * 0x10001u, kdel = prm.del * 0x10001u;
     const int nstripes = (n + ROWS - 1) / ROWS;
     const int SG = (m + 63 + G - 1) / G * G;
@@ -434,7 +439,7 @@ sed_wf_i32x2_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restr
     const uint32_t *pbP = seqb + dP.b_off, *pbQ = seqb + dQ.b_off;
     const int wsink = (n - 1) % ROWS;
     const int cap_lane = wsink / R, cap_row = wsink % R;
-    uint32_t cap = 0;
+    uint32_t capP = 0, capQ = 0;
     __shared__ uint2 lds_chunk[4][64];
     uint2 *lch = lds_chunk[threadIdx.x >> 6];
     uint32_t *bnd_io = bnd + dP.bnd_off;  // in place, as in the stripe kernel
@@ -460,25 +465,26 @@ sed_wf_i32x2_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restr
         };
         auto load_sel = [&](int c) -> uint32_t {
             const int ci = 64 * c + lane;
-            const uint32_t bp = (pbP[ci >> 4] >> ((ci & 15) * 2)) & 3u, bq = (pbQ[ci >> 4] >> ((ci & 15) * 2)) & 3u;
+            const uint32_t bp = (pbP[ci >> 4] >> ((ci & 15) * 2)) & 3u;
+            const uint32_t bq = ci < mQ ? (pbQ[ci >> 4] >> ((ci & 15) * 2)) & 3u : 0u;  // Q may be far shorter
             return 0x0C000C00u | bp | ((4u + bq) << 16);  // byte0 <- cP byte bP, byte2 <- cQ byte bQ
         };
         uint32_t tch = load_top(0), sch = load_sel(0);
         lch[lane] = make_uint2(tch, sch);
         const bool last = (k == nstripes - 1);
-        const int cap_step = last ? m - 1 + cap_lane : -1;
+        const int capP_step = last ? m - 1 + cap_lane : -1, capQ_step = last ? mQ - 1 + cap_lane : -1;
         int s = 0;
         for (int c = 0; c < nchunks; ++c) {
             uint32_t tnx = 0, snx = 0;
             if (c + 1 < nchunks) { tnx = load_top(c + 1); snx = load_sel(c + 1); }
             for (int g = 0; g < 64 / G && s < SG; ++g, s += G) {
-                const bool capg = cap_step >= s && cap_step < s + G;
+                const bool capg = (capP_step >= s && capP_step < s + G) || (capQ_step >= s && capQ_step < s + G);
                 if (s < 63 || capg)
                     x2_group<R, true>(V, cP, cQ, top_prev, bottom, selv, lch, outc, s, lane, kins, kdel, s < 63,
-                                      cap_step, cap_lane, cap_row, cap);
+                                      capP_step, capQ_step, cap_lane, cap_row, capP, capQ);
                 else
                     x2_group<R, false>(V, cP, cQ, top_prev, bottom, selv, lch, outc, s, lane, kins, kdel, false,
-                                       cap_step, cap_lane, cap_row, cap);
+                                       capP_step, capQ_step, cap_lane, cap_row, capP, capQ);
             }
             if (!last) bnd_io[s - 62 + lane] = outc;
             lch[lane] = make_uint2(tnx, snx);
@@ -490,7 +496,7 @@ sed_wf_i32x2_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restr
         r.len = -1;
         r.err = 0;
         r.pad[0] = r.pad[1] = 0;
-        const uint32_t DP = cap & 0xFFFFu, DQ = cap >> 16;
+        const uint32_t DP = capP & 0xFFFFu, DQ = capQ >> 16;
         r.dist = (double)DP;
         r.is_int = (DP == 0);
         res[P] = r;

@@ -328,8 +328,11 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         b->nlane_x2 = (int)(lane_idx.size() / 2);
     }
 
-    // distance-only integer wave pairs: two of identical shape per wave (sed_kernels.hip: i32x2). They are
-    // marked lane = 2 so that the other wave kernels (and CHAIN mode) skip them.
+    // distance-only integer wave pairs: two of equal n per wave (sed_kernels.hip: i32x2), the one with
+    // the larger m first (its bottom-row buffer serves both).  Partners come from a (n, m) sort and
+    // must have m within 4x of each other: the wave runs max(m) columns at 6 ops per 2 cells, which beats
+    // 5 ops per cell of each pair alone while min(m) > max(m) / 5.  Packed pairs are marked lane = 2,
+    // so the other wave kernels (and CHAIN mode) skip them.
     std::vector<int32_t> x2;
     b->nwave_x2 = 0;
     if (mode == SED_MODE_I32 && !split && !want_tb && (flags & SED_NO_LEN) && c->opt_pack != 2 && b->nwave > 1) {
@@ -340,10 +343,10 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
             return len_a[x] != len_a[y] ? len_a[x] < len_a[y] : len_b[x] < len_b[y];
         });
         for (size_t q = 0; q + 1 < w.size();) {
-            const int32_t x = w[q], y = w[q + 1];
-            if (len_a[x] == len_a[y] && len_b[x] == len_b[y]) {
-                x2.push_back(x);
+            const int32_t x = w[q], y = w[q + 1];  // len_b[x] <= len_b[y]
+            if (len_a[x] == len_a[y] && 4LL * len_b[x] >= len_b[y]) {
                 x2.push_back(y);
+                x2.push_back(x);
                 b->pd[x].lane = b->pd[y].lane = 2;
                 q += 2;
             } else {

@@ -305,10 +305,12 @@ def test_lane_x2_packed_distance_vs_oracle(gpu, tables, user):
 
 @pytest.mark.parametrize("R", [0, 4, 8, 16])
 def test_wave_x2_packed_distance_vs_oracle(gpu, tables, R):
-    """Distance-only wave pairs of identical shape run two per wave in 16-bit halves; pairs without
-    a same-shape partner, lane pairs and empty pairs in the same batch take their usual kernels."""
+    """Distance-only wave pairs of equal n run two per wave in 16-bit halves (m within 4x; the wave
+    runs the larger m); pairs without a partner, lane pairs and empty pairs in the same batch take
+    their usual kernels."""
     rng = np.random.default_rng(808 + R)
-    shapes = [(40, 100), (300, 257), (700, 64), (1100, 90), (1, 40), (64, 33)]
+    shapes = [(40, 100), (300, 257), (700, 64), (1100, 90), (1, 40), (64, 33), (300, 70), (300, 1000),
+              (700, 300), (1100, 400), (1100, 95)]
     pairs = []
     for n, m in shapes:
         for _ in range(int(rng.integers(2, 6))):
