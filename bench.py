@@ -34,16 +34,14 @@ import synth  # noqa: E402
 
 METRIC = "DP cells/sec (whole node) + edit-script bit-exact rate, 4k×4k RNA pairs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
-# VALU ceiling of the integer kernel, from tools/ubench/valu_rate.hip on MI355X:
-# wave64 v_add/v_and issue every ~2.5 cycles per SIMD, VOP3-only ops (v_min3, v_perm,
-# v_alignbit) every ~4.4.  A script-mode cell is 4 of the former + 3 of the latter.
 SIMDS, CLOCK = 1024, 2.4e9
 # VALU ceiling of the integer kernels: every op of the dependent DP cell issues at ~4 cycles per wave64
 # instruction on gfx950 whatever the op mix (tools/ubench/valu_mix.hip, valu_row.hip: 4.0-4.2 cycles/op,
 # the nominal 2-cycle ops do not pair when interleaved with the 4-cycle v_perm/v_min3/v_alignbit).
-# Ops per cell: perm + 3 add + min3 (+ and for the op-count field) (+ alignbit for the traceback).
+# Ops per cell in offset-key space (sed_kernels.hip): perm + add + min3 (+ delete op bit + and clearing the op for the
+# op-count field) (+ alignbit for the traceback); packed distance keys: perm + pk_add + 2 pk_min per 2 cells.
 VALU_CYCLES_PER_OP = 4.0
-CELL_OPS = {"script": 7, "len": 6, "nolen": 5, "nolen_x2": 3}  # x2: 6 packed 16-bit ops per 2 cells
+CELL_OPS = {"script": 6, "len": 5, "nolen": 3, "nolen_x2": 2}
 
 WORKLOADS = {
     # name: (pairs per GPU, n, m, cost table, description)

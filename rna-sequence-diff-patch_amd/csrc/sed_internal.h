@@ -27,10 +27,15 @@ struct sed_result {
     uint8_t pad[2];
 };
 
-// Integer kernel constants: costrow[a] byte b = cost(a -> b); kins = (insert << 16) + 4,
-// kdel = (delete << 16) + 5 (see the key layout in sed_kernels.hip).
+// Integer kernel constants (offset-key space, see sed_kernels.hip):
+//   costrow[a]   byte b = (cost(a -> b) - insert - delete - 1) & 0xFF  (32-bit keys)
+//   costrow16[a] byte b = (cost(a -> b) - insert - delete) & 0xFF      (16-bit packed distance keys)
+//   kins = (insert << 16) + 4, kdel = (delete << 16) + 5: the V-space insert / delete increments
+//   (op included); the offsets per column / row are kins and kdel - 1.
+#define SED_KB 0xFFFFFFFCu  // bias B of the 32-bit offset keys (B = 0 mod 4)
 struct sed_i32_params {
     uint32_t costrow[4];
+    uint32_t costrow16[4];
     uint32_t kins, kdel;
     uint32_t ins, del;
     uint32_t epoch;  // SPLIT hand-off counters: 1..32767 per run (sed_kernels.hip: wait_progress)

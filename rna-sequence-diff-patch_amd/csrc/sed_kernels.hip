@@ -23,10 +23,12 @@
 //    (distance, path length, op)   lexicographically minimal
 // is one unsigned min over packed keys
 //    V = D << 16 | L << 2 | op,   candidates V_pred + (cost << 16) + 4 + op
-// with op 0 insert, 1 delete, 2 update.  Cells are stored as Y = V >> 2
-// (= D << 14 | L); one v_perm_b32 looks the update cost up from a per-row byte
-// vector, so a cell is 7 VALU instructions: 3 v_lshl_add, v_perm, v_min3,
-// v_lshr and v_alignbit (which packs the 2-bit op for the traceback).
+// with op 0 insert, 1 delete, 2 update.  The kernels keep every cell in an
+// offset space, W = V - i*(kdel - 1) - j*kins + B, where the insert candidate
+// needs no add and the delete candidate only its op bit; one v_perm_b32 looks
+// the (offset) update constant up from a per-row byte vector, so a cell is 6
+// VALU instructions: v_perm, 2 v_add, v_min3, v_and (clears the op) and
+// v_alignbit (packs the 2-bit op for the traceback).
 //
 // fp64 kernel (the general path): fp64 candidates added exactly as the
 // reference does, equality ties, L tie-break on an integer key, and an
@@ -93,13 +95,35 @@ __device__ __forceinline__ void store_tb(uint32_t *p, const uint32_t (&w)[4]) {
 }
 
 // ---------------------------------------------------------------------------
-// Integer (packed-key) kernel.  Cells live in "V space":
-//     V = D << 16 | L << 2        (D < 2^16, L < 2^14)
-// candidate = V_pred + K, K = (cost << 16) + 4 + op, op 0 insert / 1 delete / 2 update;
-// mm = min3(candidates) carries the winning op in its low 2 bits and V_new = mm & ~3.
-// Lanes run unmasked all the time: a lane that has not reached column 1 yet is
-// reset to its column-0 state right before its first step, and a lane past
-// column m computes columns that nothing reads.
+// Integer (packed-key) kernels.  The reference's decision per cell is the
+// lexicographic minimum of (distance, path length, op) over its candidates, i.e.
+// one unsigned min over the keys
+//     V = D << 16 | L << 2 | op      (D < 2^16, L < 2^14; op 0 insert, 1 delete, 2 update)
+// with candidates V_left + kins, V_up + kdel, V_diag + (cost << 16) + 6, where
+// kins = (insert << 16) + 4 and kdel = (delete << 16) + 5 carry their op.
+//
+// Offset keys.  Subtracting the same amount from the three candidates of a cell
+// keeps their order, so cells are stored as
+//     W(i, j) = V(i, j) - i*Kd - j*kins + B    (Kd = kdel - 1, B = SED_KB = 2^32 - 4)
+// where i*Kd + j*kins bounds V from above (the all-delete-then-insert path) and
+// the host checks that it stays below B, so W never wraps.  In W space
+//     insert candidate = W_left,  delete candidate = W_up + 1 (its op),
+//     update candidate = W_diag + ((cost - delete - insert) << 16) - 2
+// and every border is the constant B.  The update constant is one v_perm_b32 of
+// a per-row byte vector (cost - delete - insert - 1, the bytes below it
+// 0xFF/0xFE; the host requires cost <= insert + delete), so a cell costs v_perm,
+// 2 v_add, v_min3, v_and, v_alignbit = 6 VALU.  Offsets are = 0 (mod 4), so
+// mm = min3 carries the winning op in its low 2 bits exactly as in V space.
+// (Folding the delete's op bit into the row offset as well would save the add,
+// but then the clean value's low bits rotate with the row and clearing the op
+// is no longer one instruction for every row.)
+// Distance only (!LEN): keys are D << 16 without the L/op field, W = V -
+// i*(delete << 16) - j*(insert << 16) + B, update constant ((cost - delete -
+// insert) << 16) - 1: an update also subtracts 1 from the low half, which never
+// borrows (fewer than 2^16 updates on any path), so D = (V + 0xFFFF) >> 16.
+// That is v_perm, v_add, v_min3 = 3 VALU per cell.
+// Lanes run unmasked all the time, and a lane past column m computes columns
+// that nothing reads.
 // ---------------------------------------------------------------------------
 // One column step of a lane's R rows.  tv = {top, sel} of this step's column
 // for lane 0 (the stripe's top row and str2 symbol): every lane reads the same
@@ -107,23 +131,23 @@ __device__ __forceinline__ void store_tb(uint32_t *p, const uint32_t (&w)[4]) {
 template <int R, bool TB, bool LEN>
 __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                          uint32_t &bottom, uint32_t &selv, const uint2 tv, uint32_t &outc,
-                                         uint32_t (&W)[4], const int u,
-                                         const uint32_t kins, const uint32_t kdel) {
+                                         uint32_t (&W)[4], const int u) {
     const uint32_t topv = dpp_shr1(tv.x, bottom);  // cell above the band, this column
     selv = dpp_shr1(tv.y, selv);                   // perm selector of this column's str2 symbol
     uint32_t up = topv, diag = top_prev;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const uint32_t left = V[r];
-        const uint32_t mm = umin3(left + kins,                                     // insert (op 0)
-                                  up + kdel,                                       // delete (op 1)
-                                  diag + __builtin_amdgcn_perm(cv[r], LEN ? 6u : 0u, selv));  // update (op 2)
+        // insert (op 0) = left, delete (op 1) = up + 1, update (op 2) = diag + the row's offset constant;
+        // perm bytes 1:0 come from the inline constant -2 (0xFFFE) or -1 (0xFFFF)
+        const uint32_t mm = umin3(left, LEN ? up + 1u : up,
+                                  diag + __builtin_amdgcn_perm(cv[r], LEN ? 0xFFFFFFFEu : 0xFFFFFFFFu, selv));
         if constexpr (TB) {
             const int c = u * R + r;  // compile-time after unrolling
             W[c >> 4] = __builtin_amdgcn_alignbit(mm, W[c >> 4], 2);
         }
         diag = left;
-        up = LEN ? (mm & ~3u) : mm;  // !LEN: distance only, keys carry no L/op field
+        up = LEN ? (mm & ~3u) : mm;
         V[r] = up;
     }
     top_prev = topv;
@@ -131,46 +155,45 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
     outc = dpp_shl1(bottom, outc);
 }
 
-__device__ __forceinline__ uint32_t i32_border(uint32_t i, uint32_t cost) { return ((i * cost) << 16) | (i << 2); }
-
+// Column-0 state of rows row0+1 .. row0+R (and of row0, the diagonal of the first column): every
+// border is the offset key B.
 template <int R>
-__device__ __forceinline__ void i32_reset(uint32_t (&V)[R], uint32_t &top_prev, int row0, uint32_t del) {
-    uint32_t v = i32_border((uint32_t)row0, del);
-    const uint32_t step = (del << 16) | 4u;
-    top_prev = v;
+__device__ __forceinline__ void i32_reset(uint32_t (&V)[R], uint32_t &top_prev) {
+    top_prev = SED_KB;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        v += step;
-        V[r] = v;
+    for (int r = 0; r < R; ++r) V[r] = SED_KB;
+}
+
+// The sink cell back to V space: V = W - B + n*Kd + m*kins; returns {D, L} (L = -1 without LEN).
+template <bool LEN>
+__device__ __forceinline__ int2 i32_decode(uint32_t w, int n, int m, const sed_i32_params &prm) {
+    if constexpr (LEN) {
+        const uint32_t v = w - SED_KB + (uint32_t)n * (prm.kdel - 1u) + (uint32_t)m * prm.kins;
+        return make_int2((int)(v >> 16), (int)((v >> 2) & 0x3FFFu));
+    } else {
+        const uint32_t v = w - SED_KB + (((uint32_t)n * prm.del + (uint32_t)m * prm.ins) << 16);
+        return make_int2((int)((v + 0xFFFFu) >> 16), -1);
     }
 }
 
-// Ramp without resets.  Every lane starts a stripe at its column-0 state (i32_reset) and lane
-// t begins real work at step t.  Before that it runs "virtual" negative columns that must leave
-// its state unchanged, which costs one per-lane select per step instead of per-row resets:
-//   * its str2 selector is the sentinel SED_SEL_SENT (perm byte 0x0D -> cost 0xFF), so the update
-//     candidate is far above the others;
-//   * its insert constant is 0, so the insert candidate is exactly the old value (op 0, L kept),
-//     one below the delete candidate border(row-1) + kdel = border(row) + 1.
-// The state (V, bottom, top_prev) therefore stays at the column-0 borders until the lane's
-// first real column, whose neighbours are then exactly D[row][0], D[row-1][0] and the cell above.
-#define SED_SEL_SENT 0x0C0D0100u
+// Ramp for free.  Every lane starts a stripe at its column-0 state and lane t begins real work
+// at step t.  Before that it runs "virtual" columns, which leave its state unchanged: their str2
+// selector is the sentinel SED_SEL_SENT (update constant 0), so with every neighbour at its
+// column-0 value B the candidates are B (insert), B + 1 (delete) and B + 0 (update), and the
+// minimum B keeps the border (op bits 0).  The lane's first real column then sees exactly
+// D[row][0], D[row-1][0] and the cell above.
+#define SED_SEL_SENT 0x0C0C0C0Cu
+// perm selector of str2 symbol b: byte3 <- 0xFF, byte2 <- cost byte b, bytes 1:0 <- the constant
+__device__ __forceinline__ uint32_t i32_sel(uint32_t b) { return 0x0D000100u | ((4u + b) << 16); }
 
-// SLOW groups: the ramp (steps < 63 of a stripe: per-lane insert constant) and the group that
-// produces the sink cell (captured on its lane).  One variant for both: every extra variant is
-// another merge point where the register allocator inserts copies of the whole state.
-template <int R, bool TB, bool LEN, bool SLOW>
+// CAP: the group that produces the sink cell (captured on its lane); every extra variant is
+// another merge point where the register allocator may insert copies of the whole state.
+template <int R, bool TB, bool LEN, bool CAP>
 __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                           uint32_t &bottom, uint32_t &selv, const uint2 *__restrict__ lch,
-                                          uint32_t &outc, uint32_t (&W)[4],
-                                          const int s0, const int lane, const uint32_t kins, const uint32_t kdel,
-                                          const bool ramp, const int cap_step, const int cap_lane, const int cap_row,
-                                          uint32_t &cap) {
+                                          uint32_t &outc, uint32_t (&W)[4], const int s0, const int lane,
+                                          const int cap_step, const int cap_lane, const int cap_row, uint32_t &cap) {
     constexpr int G = Grp<R>::G;
-    // opaque copies: the four group variants sit in sibling branches, and without this the
-    // compiler hoists the first step's V[r] + kins out of them (16 more live VGPRs -> spills)
-    uint32_t kin = kins, kde = kdel;
-    asm volatile("" : "+s"(kin), "+s"(kde));
     uint2 tv[G];
     const uint2 *lp = lch + (s0 & 63);  // G divides 64: a group never wraps the chunk
 #pragma unroll
@@ -178,10 +201,8 @@ __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         const int s = s0 + u;
-        uint32_t ki = kin;
-        if constexpr (SLOW) ki = ramp ? (kin & ~(uint32_t)((s - lane) >> 31)) : kin;  // virtual column: insert adds nothing
-        i32_step<R, TB, LEN>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u, ki, kde);
-        if constexpr (SLOW) {
+        i32_step<R, TB, LEN>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u);
+        if constexpr (CAP) {
             const bool hit = (s == cap_step) && (lane == cap_lane);
 #pragma unroll
             for (int r = 0; r < R; ++r) cap = (hit && r == cap_row) ? V[r] : cap;
@@ -259,7 +280,6 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
         }
         return;
     }
-    const uint32_t kins = LEN ? prm.kins : (prm.ins << 16), kdel = LEN ? prm.kdel : (prm.del << 16);
     const int nstripes = (n + ROWS - 1) / ROWS;
     const int klast = SPLIT ? kfirst : nstripes - 1;
     const int SG = (m + 63 + G - 1) / G * G;  // steps per stripe, rounded to whole groups
@@ -289,14 +309,14 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             cv[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
         }
         uint32_t top_prev;
-        i32_reset<R>(V, top_prev, row0, prm.del);
+        i32_reset<R>(V, top_prev);
         // column-0 state for every lane; virtual columns until the lane's first real one (see above)
         uint32_t bottom = V[R - 1], selv = SED_SEL_SENT, outc = 0;
         uint32_t W[4] = {0, 0, 0, 0};
 
         auto load_top = [&](int c) -> uint32_t {
             const int j = 64 * c + lane + 1;
-            if (k == 0) return i32_border((uint32_t)j, prm.ins);  // row 0: D = j*insert, L = j
+            if (k == 0) return SED_KB;  // row 0: D = j*insert, L = j (offset key B)
             if constexpr (SPLIT) {  // after one timeout stop waiting: the kernel must still drain quickly
                 if (ok) ok = wait_progress(prog + d.prog_off + k - 1, prm.epoch << 16, (uint32_t)min(m, 64 * c + 64));
             }
@@ -304,8 +324,7 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
         };
         auto load_sel = [&](int c) -> uint32_t {
             const int ci = 64 * c + lane;
-            const uint32_t b = (pb[ci >> 4] >> ((ci & 15) * 2)) & 3u;
-            return 0x0C000100u | ((4u + b) << 16);  // perm: byte2 <- cost byte b, bytes1:0 <- 6
+            return i32_sel((pb[ci >> 4] >> ((ci & 15) * 2)) & 3u);
         };
         uint32_t tch = load_top(0), sch = load_sel(0);
         lch[lane] = make_uint2(tch, sch);
@@ -318,12 +337,12 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             if (c + 1 < nchunks) { tnx = load_top(c + 1); snx = load_sel(c + 1); }
             for (int g = 0; g < 64 / G && s < SG; ++g, s += G) {
                 const bool capg = cap_step >= s && cap_step < s + G;
-                if (s < 63 || capg)
-                    i32_group<R, TB, LEN, true>(V, cv, top_prev, bottom, selv, lch, outc, W, s, lane, kins,
-                                                kdel, s < 63, cap_step, cap_lane, cap_row, cap);
+                if (capg)
+                    i32_group<R, TB, LEN, true>(V, cv, top_prev, bottom, selv, lch, outc, W, s, lane, cap_step,
+                                                cap_lane, cap_row, cap);
                 else
-                    i32_group<R, TB, LEN, false>(V, cv, top_prev, bottom, selv, lch, outc, W, s, lane, kins,
-                                                 kdel, false, cap_step, cap_lane, cap_row, cap);
+                    i32_group<R, TB, LEN, false>(V, cv, top_prev, bottom, selv, lch, outc, W, s, lane, cap_step,
+                                                 cap_lane, cap_row, cap);
                 if constexpr (TB) {
                     uint32_t *gp = tbk + (uint64_t)(s / G) * 256u;  // wave-uniform base, per-lane 16-byte offset
                     store_tb(gp + lane * 4, W);
@@ -343,23 +362,26 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
         if (!last) __builtin_amdgcn_s_waitcnt(0);  // own bottom-row stores done before the next stripe reads them
     }
     if (klast == nstripes - 1 && lane == cap_lane) {
-        const uint32_t D = cap >> 16;
-        res[pair].dist = (double)D;
-        res[pair].len = LEN ? (int32_t)((cap >> 2) & 0x3FFFu) : -1;
-        res[pair].is_int = (D == 0);
+        const int2 dl = i32_decode<LEN>(cap, n, m, prm);
+        res[pair].dist = (double)dl.x;
+        res[pair].len = dl.y;
+        res[pair].is_int = (dl.x == 0);
         res[pair].err = ok ? 0 : 1;  // SPLIT: a timed-out wait anywhere up the stripe chain poisons the pair
     }
 }
 
 // ---------------------------------------------------------------------------
 // Distance only, two pairs per wave (SED_NO_LEN batches, pairs of equal n): pair P in the low
-// 16 bits of every cell word, pair Q in the high 16 bits.  A distance key is D alone, below
-// 2^16 - 256 (the integer-mode bound), so the halves never wrap into each other and packed 16-bit
-// ops do two cells at once: perm + 3 v_pk_add_u16 + 2 v_pk_min_u16 = 6 VALU / 2 cells instead
-// of 5 VALU / cell.  The rest is the stripe kernel's schedule (virtual-column ramp, lane-0 LDS
-// chunk, in-place bottom rows in P's buffer, which the host makes the pair with the larger m); both
-// pairs have the same n, so they share stripes and rows, and the wave runs max(m) columns, the
-// shorter pair's extra columns being don't-care.  Each pair's sink is captured at its own step.
+// 16 bits of every cell word, pair Q in the high 16 bits.  Each half is a 16-bit offset key
+// W = D - i*delete - j*insert + 0xFFFF (the host checks i*delete + j*insert <= 0xFFFF over the
+// computed block, so no half wraps), with insert candidate W_left, delete candidate W_up and
+// update candidate W_diag + (cost - delete - insert), a 16-bit constant 0xFFxx since the host
+// packs only when every substitution is cheaper than delete + insert.  Packed 16-bit ops do two
+// cells at once: perm + v_pk_add_u16 + 2 v_pk_min_u16 = 4 VALU / 2 cells.  The rest is the stripe
+// kernel's schedule (virtual-column ramp, lane-0 LDS chunk, in-place bottom rows in P's buffer,
+// which the host makes the pair with the larger m); both pairs have the same n, so they share
+// stripes and rows, and the wave runs max(m) columns, the shorter pair's extra columns being
+// don't-care.  Each pair's sink is captured at its own step.
 // ---------------------------------------------------------------------------
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
@@ -369,18 +391,18 @@ __device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t,
                               __builtin_elementwise_min(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
 }
-#define SED_SEL_SENT_X2 0x0C0D0C0Du  // both halves: update cost 0xFF (virtual columns)
+// 16-bit offset key of the sink back to D: D = W - 0xFFFF + n*delete + m*insert (mod 2^16)
+__device__ __forceinline__ uint32_t x2_decode(uint32_t half, int n, int m, const sed_i32_params &prm) {
+    return (half + 1u + (uint32_t)n * prm.del + (uint32_t)m * prm.ins) & 0xFFFFu;
+}
 
-template <int R, bool SLOW>
+template <int R, bool CAP>
 __device__ __forceinline__ void x2_group(uint32_t (&V)[R], const uint32_t (&cP)[R], const uint32_t (&cQ)[R],
                                          uint32_t &top_prev, uint32_t &bottom, uint32_t &selv,
                                          const uint2 *__restrict__ lch, uint32_t &outc, const int s0, const int lane,
-                                         const uint32_t kins, const uint32_t kdel, const bool ramp,
                                          const int capP_step, const int capQ_step, const int cap_lane,
                                          const int cap_row, uint32_t &capP, uint32_t &capQ) {
     constexpr int G = Grp<R>::G;
-    uint32_t kin = kins, kde = kdel;
-    asm volatile("" : "+v"(kin), "+v"(kde));  // see i32_group
     uint2 tv[G];
     const uint2 *lp = lch + (s0 & 63);
 #pragma unroll
@@ -388,16 +410,14 @@ __device__ __forceinline__ void x2_group(uint32_t (&V)[R], const uint32_t (&cP)[
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         const int s = s0 + u;
-        uint32_t ki = kin;
-        if constexpr (SLOW) ki = ramp ? (kin & ~(uint32_t)((s - lane) >> 31)) : kin;
         const uint32_t topv = dpp_shr1(tv[u].x, bottom);
         selv = dpp_shr1(tv[u].y, selv);
         uint32_t up = topv, diag = top_prev;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const uint32_t left = V[r];
-            const uint32_t mm = pk_min(pk_min(pk_add(left, ki), pk_add(up, kde)),
-                                       pk_add(diag, __builtin_amdgcn_perm(cQ[r], cP[r], selv)));
+            // the row above (up) enters last: one dependent op per row on the column's chain
+            const uint32_t mm = pk_min(pk_min(left, pk_add(diag, __builtin_amdgcn_perm(cQ[r], cP[r], selv))), up);
             diag = left;
             up = mm;
             V[r] = mm;
@@ -405,7 +425,7 @@ __device__ __forceinline__ void x2_group(uint32_t (&V)[R], const uint32_t (&cP)[
         top_prev = topv;
         bottom = V[R - 1];
         outc = dpp_shl1(bottom, outc);
-        if constexpr (SLOW) {
+        if constexpr (CAP) {
             const bool hP = (s == capP_step) && (lane == cap_lane), hQ = (s == capQ_step) && (lane == cap_lane);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -431,7 +451,6 @@ sed_wf_i32x2_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restr
     const int P = __builtin_amdgcn_readfirstlane(list[2 * w]), Q = __builtin_amdgcn_readfirstlane(list[2 * w + 1]);
     const sed_pair_desc dP = pd[P], dQ = pd[Q];
     const int n = dP.n, m = dP.m, mQ = dQ.m;  // host: dQ.n == n, 1 <= mQ <= m
-    const uint32_t kins = prm.ins * 0x10001u, kdel = prm.del * 0x10001u;
     const int nstripes = (n + ROWS - 1) / ROWS;
     const int SG = (m + 63 + G - 1) / G * G;
     const int nchunks = (SG + 63) >> 6;
@@ -451,23 +470,23 @@ sed_wf_i32x2_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restr
         for (int r = 0; r < R; ++r) {
             const int ri = row0 + r;
             const uint32_t aP = (paP[ri >> 4] >> ((ri & 15) * 2)) & 3u, aQ = (paQ[ri >> 4] >> ((ri & 15) * 2)) & 3u;
-            cP[r] = aP == 0 ? prm.costrow[0] : aP == 1 ? prm.costrow[1] : aP == 2 ? prm.costrow[2] : prm.costrow[3];
-            cQ[r] = aQ == 0 ? prm.costrow[0] : aQ == 1 ? prm.costrow[1] : aQ == 2 ? prm.costrow[2] : prm.costrow[3];
+            cP[r] = aP == 0 ? prm.costrow16[0] : aP == 1 ? prm.costrow16[1] : aP == 2 ? prm.costrow16[2] : prm.costrow16[3];
+            cQ[r] = aQ == 0 ? prm.costrow16[0] : aQ == 1 ? prm.costrow16[1] : aQ == 2 ? prm.costrow16[2] : prm.costrow16[3];
         }
-        uint32_t top_prev = (uint32_t)row0 * kdel;  // column 0: i deletes, both halves
+        uint32_t top_prev = 0xFFFFFFFFu;  // column 0 and row 0 are the offset key 0xFFFF in both halves
 #pragma unroll
-        for (int r = 0; r < R; ++r) V[r] = (uint32_t)(row0 + r + 1) * kdel;
-        uint32_t bottom = V[R - 1], selv = SED_SEL_SENT_X2, outc = 0;
+        for (int r = 0; r < R; ++r) V[r] = 0xFFFFFFFFu;
+        uint32_t bottom = V[R - 1], selv = SED_SEL_SENT, outc = 0;
         auto load_top = [&](int c) -> uint32_t {
             const int j = 64 * c + lane + 1;
-            if (k == 0) return (uint32_t)j * kins;  // row 0: j inserts
+            if (k == 0) return 0xFFFFFFFFu;
             return load_sc1(bnd_io + j + 64);
         };
         auto load_sel = [&](int c) -> uint32_t {
             const int ci = 64 * c + lane;
             const uint32_t bp = (pbP[ci >> 4] >> ((ci & 15) * 2)) & 3u;
             const uint32_t bq = ci < mQ ? (pbQ[ci >> 4] >> ((ci & 15) * 2)) & 3u : 0u;  // Q may be far shorter
-            return 0x0C000C00u | bp | ((4u + bq) << 16);  // byte0 <- cP byte bP, byte2 <- cQ byte bQ
+            return 0x0D000D00u | bp | ((4u + bq) << 16);  // byte0 <- cP byte bP, byte2 <- cQ byte bQ, 1 and 3 <- 0xFF
         };
         uint32_t tch = load_top(0), sch = load_sel(0);
         lch[lane] = make_uint2(tch, sch);
@@ -479,12 +498,12 @@ sed_wf_i32x2_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restr
             if (c + 1 < nchunks) { tnx = load_top(c + 1); snx = load_sel(c + 1); }
             for (int g = 0; g < 64 / G && s < SG; ++g, s += G) {
                 const bool capg = (capP_step >= s && capP_step < s + G) || (capQ_step >= s && capQ_step < s + G);
-                if (s < 63 || capg)
-                    x2_group<R, true>(V, cP, cQ, top_prev, bottom, selv, lch, outc, s, lane, kins, kdel, s < 63,
-                                      capP_step, capQ_step, cap_lane, cap_row, capP, capQ);
+                if (capg)
+                    x2_group<R, true>(V, cP, cQ, top_prev, bottom, selv, lch, outc, s, lane, capP_step, capQ_step,
+                                      cap_lane, cap_row, capP, capQ);
                 else
-                    x2_group<R, false>(V, cP, cQ, top_prev, bottom, selv, lch, outc, s, lane, kins, kdel, false,
-                                       capP_step, capQ_step, cap_lane, cap_row, capP, capQ);
+                    x2_group<R, false>(V, cP, cQ, top_prev, bottom, selv, lch, outc, s, lane, capP_step, capQ_step,
+                                       cap_lane, cap_row, capP, capQ);
             }
             if (!last) bnd_io[s - 62 + lane] = outc;
             lch[lane] = make_uint2(tnx, snx);
@@ -496,7 +515,7 @@ sed_wf_i32x2_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restr
         r.len = -1;
         r.err = 0;
         r.pad[0] = r.pad[1] = 0;
-        const uint32_t DP = capP & 0xFFFFu, DQ = capQ >> 16;
+        const uint32_t DP = x2_decode(capP & 0xFFFFu, n, m, prm), DQ = x2_decode(capQ >> 16, n, mQ, prm);
         r.dist = (double)DP;
         r.is_int = (DP == 0);
         res[P] = r;
@@ -520,7 +539,7 @@ sed_wf_i32x2_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restr
 // exactly the stripe kernel's (one stripe), so the traceback kernel is shared.
 // ---------------------------------------------------------------------------
 struct chain_pair_state {
-    int pair, m, T, S, end;            // end: first global step after its last real column (T + m + 63)
+    int pair, n, m, T, S, end;         // end: first global step after its last real column (T + m + 63)
     int cap_step, cap_lane, cap_row;   // the sink cell (n, m)
     uint64_t tb_off;
     int sg;                            // traceback groups allocated per stripe
@@ -534,6 +553,7 @@ __device__ __forceinline__ chain_pair_state chain_load(const sed_pair_desc *__re
     const sed_pair_desc d = pd[pair];
     chain_pair_state c;
     c.pair = pair;
+    c.n = d.n;
     c.m = d.m;
     c.T = T;
     c.S = (d.m + 63) & ~63;
@@ -549,21 +569,17 @@ __device__ __forceinline__ chain_pair_state chain_load(const sed_pair_desc *__re
 }
 
 // One group of G steps.  SW: lanes switch from the previous pair to the pair starting at
-// `Tcur` after the step at which lane == s + 1 - Tcur.  GEN (rare groups: the first pair's
-// virtual-column ramp, sink captures of the previous (A) and current (B) pair, and any switch
-// in those groups) additionally masks the insert constant (ramp != 0) and captures.
+// `Tcur` after the step at which lane == s + 1 - Tcur.  GEN (rare groups: sink captures of the
+// previous (A) and current (B) pair, and any switch in those groups) additionally captures.
 template <int R, bool TB, bool LEN, bool SW, bool GEN>
 __device__ __forceinline__ void i32_chain_group(uint32_t (&V)[R], uint32_t (&cv)[R], const uint32_t (&cvn)[R],
                                                 const uint32_t (&Vb)[R], const uint32_t tpb, uint32_t &top_prev,
                                                 uint32_t &bottom, uint32_t &selv, const uint2 *__restrict__ lch,
                                                 uint32_t &outc, uint32_t (&W)[4], const int s0, const int lane,
-                                                const uint32_t kins, const uint32_t kdel, const int Tcur,
-                                                const bool ramp, const int csA, const int clA, const int crA,
+                                                const int Tcur, const int csA, const int clA, const int crA,
                                                 uint32_t &capA, const int csB, const int clB, const int crB,
                                                 uint32_t &capB) {
     constexpr int G = Grp<R>::G;
-    uint32_t kin = kins, kde = kdel;
-    asm volatile("" : "+s"(kin), "+s"(kde));  // see i32_group: keep sibling variants from hoisting V+kins
     uint2 tv[G];
     const uint2 *lp = lch + (s0 & 63);
 #pragma unroll
@@ -571,9 +587,7 @@ __device__ __forceinline__ void i32_chain_group(uint32_t (&V)[R], uint32_t (&cv)
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         const int s = s0 + u;
-        uint32_t ki = kin;
-        if constexpr (GEN) ki = ramp ? (kin & ~(uint32_t)((s - lane) >> 31)) : kin;
-        i32_step<R, TB, LEN>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u, ki, kde);
+        i32_step<R, TB, LEN>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u);
         if constexpr (GEN) {
             const bool hA = (s == csA) && (lane == clA), hB = (s == csB) && (lane == clB);
 #pragma unroll
@@ -595,11 +609,12 @@ __device__ __forceinline__ void i32_chain_group(uint32_t (&V)[R], uint32_t (&cv)
 }
 
 template <int R, bool TB, bool LEN>
-__device__ __forceinline__ void chain_store_result(sed_result *__restrict__ res, int pair, uint32_t cap) {
-    const uint32_t D = cap >> 16;
-    res[pair].dist = (double)D;
-    res[pair].len = LEN ? (int32_t)((cap >> 2) & 0x3FFFu) : -1;
-    res[pair].is_int = (D == 0);
+__device__ __forceinline__ void chain_store_result(sed_result *__restrict__ res, int pair, uint32_t cap, int n,
+                                                   int m, const sed_i32_params &prm) {
+    const int2 dl = i32_decode<LEN>(cap, n, m, prm);
+    res[pair].dist = (double)dl.x;
+    res[pair].len = dl.y;
+    res[pair].is_int = (dl.x == 0);
 }
 
 // the chain kernel also holds the next pair's cost rows and the column-0 constants
@@ -632,14 +647,13 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
         c0 = chain_off[chain];
         c1 = chain_off[chain + 1];
     }
-    const uint32_t kins = LEN ? prm.kins : (prm.ins << 16), kdel = LEN ? prm.kdel : (prm.del << 16);
     __shared__ uint2 lds_chunk[4][64];
     uint2 *lch = lds_chunk[threadIdx.x >> 6];
     const int row0 = lane * R;
 
     // per-lane constants: column-0 state of this lane's rows (the same for every pair)
     uint32_t Vb[R], tpb;
-    i32_reset<R>(Vb, tpb, row0, prm.del);
+    i32_reset<R>(Vb, tpb);
     auto rows_of = [&](int pair, uint32_t (&out)[R]) {
         const uint32_t *pa = seqa + pd[pair].a_off;
 #pragma unroll
@@ -652,7 +666,7 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
     auto chunk_of = [&](const chain_pair_state &c, int cl) -> uint2 {  // lane 0's inputs, local chunk cl
         const int j = 64 * cl + lane;
         const uint32_t b = (c.pb[j >> 4] >> ((j & 15) * 2)) & 3u;
-        return make_uint2(i32_border((uint32_t)(j + 1), prm.ins), 0x0C000100u | ((4u + b) << 16));
+        return make_uint2(SED_KB, i32_sel(b));  // row 0 (offset key B), str2 selector
     };
 
     chain_pair_state cur = chain_load<R>(pd, seqb, chain_pairs[c0], 0), prv = cur;
@@ -688,16 +702,15 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
         for (int g = 0; g < 64 / G; ++g) {
             const int s = s0 + g * G;
             const bool win = have_cur && have_prv && s < cur.T + 64;  // lanes switch from prv to cur
-            const bool ramp = have_cur && !have_prv && s < 63;       // first pair: virtual columns
             const bool capg = (have_prv && prv.cap_step >= s && prv.cap_step < s + G) ||
                               (have_cur && cur.cap_step >= s && cur.cap_step < s + G);
             // wave-uniform: which body; Tsw never matches a lane outside a switch window
             const int Tsw = win ? cur.T : -(1 << 30);
 #define SED_CGROUP(SW, GEN)                                                                               \
-    i32_chain_group<R, TB, LEN, SW, GEN>(V, cv, cvn, Vb, tpb, top_prev, bottom, selv, lch, outc, W, s, lane, kins, \
-                                         kdel, Tsw, ramp, prv.cap_step, prv.cap_lane, prv.cap_row, capA,          \
-                                         cur.cap_step, cur.cap_lane, cur.cap_row, capB)
-            if (capg || ramp) SED_CGROUP(false, true);
+    i32_chain_group<R, TB, LEN, SW, GEN>(V, cv, cvn, Vb, tpb, top_prev, bottom, selv, lch, outc, W, s, lane, Tsw, \
+                                         prv.cap_step, prv.cap_lane, prv.cap_row, capA, cur.cap_step,             \
+                                         cur.cap_lane, cur.cap_row, capB)
+            if (capg) SED_CGROUP(false, true);
             else if (win) SED_CGROUP(true, false);
             else SED_CGROUP(false, false);
 #undef SED_CGROUP
@@ -719,9 +732,9 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
             }
             if (capg) {
                 if (have_prv && prv.cap_step >= s && prv.cap_step < s + G && lane == prv.cap_lane)
-                    chain_store_result<R, TB, LEN>(res, prv.pair, capA);
+                    chain_store_result<R, TB, LEN>(res, prv.pair, capA, prv.n, prv.m, prm);
                 if (have_cur && cur.cap_step >= s && cur.cap_step < s + G && lane == cur.cap_lane)
-                    chain_store_result<R, TB, LEN>(res, cur.pair, capB);
+                    chain_store_result<R, TB, LEN>(res, cur.pair, capB, cur.n, cur.m, prm);
             }
         }
         lch[lane] = nx;  // after the chunk's last LDS read (in order)
@@ -1176,9 +1189,8 @@ __global__ void sed_selftest_kernel(uint32_t *out) {
     if (shl != (lane == 63 ? 9u : 1001u + lane)) fail |= 2;
     const uint32_t rol = dpp_rol1(v);
     if (rol != 1000u + ((lane + 1) & 63)) fail |= 4;
-    const uint32_t sel = 0x0C000100u | ((4u + (lane & 3)) << 16);
-    const uint32_t p = __builtin_amdgcn_perm(0x44332211u, 6u, sel);
-    if (p != ((((0x44332211u >> (8 * (lane & 3))) & 0xFFu) << 16) | 6u)) fail |= 8;
+    const uint32_t p = __builtin_amdgcn_perm(0x44332211u, 0xFFFFFFFEu, i32_sel(lane & 3));
+    if (p != (0xFF00FFFEu | (((0x44332211u >> (8 * (lane & 3))) & 0xFFu) << 16))) fail |= 8;
     const uint32_t ab = __builtin_amdgcn_alignbit(0x3u + (lane << 2), 0x80000000u, 2);
     if (ab != (0xE0000000u | 0x20000000u)) fail |= 16;
     atomicOr(out, fail);
@@ -1289,10 +1301,10 @@ hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops) {
     case RR:                                                                                                     \
         if (uni)                                                                                                 \
             hipLaunchKernelGGL((sed_traceback_window_kernel<RR>), dim3(grid), dim3(64), 0, L.stream, L.pd,       \
-                               L.npairs, L.tb, L.res, ops);                                                     \
+                               L.npairs, L.tb, L.res, ops);                                           \
         else                                                                                                     \
             hipLaunchKernelGGL((sed_traceback_kernel<RR>), dim3(grid), dim3(64), 0, L.stream, L.pd,              \
-                               L.npairs, L.tb, L.res, ops);                                                     \
+                               L.npairs, L.tb, L.res, ops);                                           \
         break;
         CASE(4) CASE(8) CASE(16) CASE(32)
 #undef CASE

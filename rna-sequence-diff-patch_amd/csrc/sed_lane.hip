@@ -7,10 +7,11 @@
 // row by row (StringEditDistance.py:185-222 order) with the whole DP row in VGPRs: no DPP, no
 // LDS, no inter-lane traffic; 64 pairs per wave, >= 4 waves per SIMD for 250k pairs.
 //
-// Cell keys are the packed-integer keys of sed_kernels.hip (D << 16 | L << 2 | op), so results
-// (distance, L = script length, canonical op) are identical to the wave kernel's:
-//   LEN:  candidates left+kins, up+kdel, diag+perm(costrow, 6, sel) -> v_min3 -> & ~3   (6 VALU)
-//   !LEN: distance only, no L/op field: +ins<<16, +del<<16, +cost<<16 -> v_min3         (5 VALU)
+// Cell keys are the offset keys of sed_kernels.hip (W = V - i*(kdel - 1) - j*kins + B over
+// V = D << 16 | L << 2 | op), so results (distance, L = script length, canonical op) are
+// identical to the wave kernel's:
+//   LEN:  candidates left, up + 1, diag + perm(costrow, -2, sel) -> v_min3 -> & ~3   (5 VALU)
+//   !LEN: distance only, no L/op field: left, up, diag + perm(costrow, -1, sel)      (3 VALU)
 // TB (implies LEN): the op of every cell (2 bits, 32 per row = one uint2) is stored per pair,
 // row-major, and the same lane walks it back from (n, m) to write the canonical script.
 #include "sed_internal.h"
@@ -20,7 +21,6 @@ namespace {
 __device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) {
     return min(min(a, b), c);  // folds to v_min3_u32
 }
-__device__ __forceinline__ uint32_t lane_border(uint32_t i, uint32_t cost) { return ((i * cost) << 16) | (i << 2); }
 
 template <bool LEN, bool TB>
 __global__ __launch_bounds__(256) void sed_lane_i32_kernel(const sed_pair_desc *__restrict__ pd,
@@ -37,9 +37,7 @@ __global__ __launch_bounds__(256) void sed_lane_i32_kernel(const sed_pair_desc *
     const int pair = idx[t];
     const sed_pair_desc d = pd[pair];
     const int n = d.n, m = d.m;  // host guarantees 1 <= n <= SED_LANE_MAXN, 1 <= m <= MM
-    const uint32_t kins = LEN ? prm.kins : (prm.ins << 16);
-    const uint32_t kdel = LEN ? prm.kdel : (prm.del << 16);
-    const uint32_t s1 = LEN ? 6u : 0u;  // perm bytes 1:0 of the update candidate (L+1, op 2)
+    const uint32_t s1 = LEN ? 0xFFFFFFFEu : 0xFFFFFFFFu;  // perm bytes 1:0 of the update constant
     // Transposed lookup: the lane keeps, per column j, the 4 costs cost(a -> b_j) as bytes of colw[j];
     // a row's symbol a_i becomes the perm selector, so a row costs 2 ops of setup instead of a
     // per-lane select of its cost row.  (Columns beyond m read the next pair's codes or padding:
@@ -62,28 +60,24 @@ __global__ __launch_bounds__(256) void sed_lane_i32_kernel(const sed_pair_desc *
         colw[j] = (b & 2u) ? hi : lo;
     }
 #pragma unroll
-    for (int j = 0; j <= MM; ++j) V[j] = lane_border((uint32_t)j, prm.ins);  // row 0: j inserts
+    for (int j = 0; j <= MM; ++j) V[j] = SED_KB;  // row 0: j inserts (offset key B)
     const uint32_t *pa = seqa + d.a_off;
-    const uint32_t cstep = (prm.del << 16) | 4u;  // column 0: i deletes
-    uint32_t wa = 0, colv = 0;
+    uint32_t wa = 0;  // column 0 (i deletes) is the offset key B in every row
     uint2 *tbp = reinterpret_cast<uint2 *>(tb) + (TB ? d.tb_off / 2 : 0);
     for (int i = 0; i < n; ++i) {
         if ((i & 15) == 0) wa = pa[i >> 4];
         const uint32_t a = (wa >> (2 * (i & 15))) & 3u;
-        const uint32_t sel = 0x0C000100u | ((4u + a) << 16);  // perm: byte2 <- cost byte a, bytes1:0 <- s1
+        const uint32_t sel = 0x0D000100u | ((4u + a) << 16);  // perm: byte3 <- 0xFF, byte2 <- cost byte a, 1:0 <- s1
         // update candidate of column j+1 is formed from the old V[j] before V[j] is overwritten,
         // so every V[j] is updated in place (no register rotation across the row loop)
         uint32_t dg = V[0] + __builtin_amdgcn_perm(colw[0], s1, sel);
-        colv += cstep;
-        V[0] = colv;
-        uint32_t left = colv;
+        uint32_t left = V[0];  // stays B
         uint32_t W0 = 0, W1 = 0;
 #pragma unroll
         for (int j = 1; j <= MM; ++j) {
             const uint32_t up = V[j];
-            const uint32_t cdel = up + kdel;                                              // delete (op 1)
             const uint32_t dnext = j < MM ? up + __builtin_amdgcn_perm(colw[j], s1, sel) : 0u;
-            const uint32_t mm = umin3(left + kins, cdel, dg);  // insert (op 0), update (op 2)
+            const uint32_t mm = umin3(left, LEN ? up + 1u : up, dg);  // insert (op 0), delete (op 1), update (op 2)
             dg = dnext;
             if constexpr (TB) {
                 if (j <= 16) W0 = __builtin_amdgcn_alignbit(mm, W0, 2);
@@ -98,8 +92,15 @@ __global__ __launch_bounds__(256) void sed_lane_i32_kernel(const sed_pair_desc *
     uint32_t cap = V[1];
 #pragma unroll
     for (int j = 2; j <= MM; ++j) cap = (j == m) ? V[j] : cap;
-    const uint32_t D = cap >> 16;
-    const int32_t L = LEN ? (int32_t)((cap >> 2) & 0x3FFFu) : -1;
+    uint32_t D;
+    int32_t L = -1;
+    if constexpr (LEN) {  // back to V space: V = W - B + n*(kdel - 1) + m*kins
+        const uint32_t v = cap - SED_KB + (uint32_t)n * (prm.kdel - 1u) + (uint32_t)m * prm.kins;
+        D = v >> 16;
+        L = (int32_t)((v >> 2) & 0x3FFFu);
+    } else {
+        D = (cap - SED_KB + (((uint32_t)n * prm.del + (uint32_t)m * prm.ins) << 16) + 0xFFFFu) >> 16;
+    }
     sed_result r;
     r.dist = (double)D;
     r.len = L;
@@ -134,10 +135,10 @@ __global__ __launch_bounds__(256) void sed_lane_i32_kernel(const sed_pair_desc *
 
 // Distance only, two pairs per lane (SED_NO_LEN batches: config 5, wfsearch).  Pair P lives in
 // the low 16 bits of every cell word and pair Q in the high 16 bits; both have the same n, so one
-// row loop serves both.  Distance keys need no L/op field, so a cell is D alone (< 2^16, the
-// integer-mode bound), and packed 16-bit ops do two cells at once:
-//   perm (P's and Q's update costs in one word) + 3 v_pk_add_u16 + 2 v_pk_min_u16 = 6 VALU / 2 cells
-// instead of 5 VALU / cell.  Both halves stay below 2^16 - 256, so no half ever wraps.
+// row loop serves both.  Each half is the 16-bit offset key of sed_kernels.hip's i32x2 kernel
+// (W = D - i*delete - j*insert + 0xFFFF; the host checks n*delete + 32*insert <= 0xFFFF and that
+// every substitution is cheaper than delete + insert), so packed 16-bit ops do two cells at once:
+//   perm (P's and Q's update constants in one word) + v_pk_add_u16 + 2 v_pk_min_u16 = 4 VALU / 2 cells.
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));  // v_pk_*_u16 operands
 __device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
@@ -159,13 +160,12 @@ __global__ __launch_bounds__(256) void sed_lane_i32x2_kernel(const sed_pair_desc
     const int P = idx[2 * t], Q = idx[2 * t + 1];
     const sed_pair_desc dP = pd[P], dQ = pd[Q];
     const int n = dP.n, mP = dP.m, mQ = dQ.m;  // host guarantees dQ.n == n, 1 <= n <= MAXN, 1 <= m <= MM
-    const uint32_t kins = prm.ins * 0x10001u, kdel = prm.del * 0x10001u;
     uint32_t colrow[4];  // transposed cost table, as in sed_lane_i32_kernel
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
         uint32_t w = 0;
 #pragma unroll
-        for (int a = 0; a < 4; ++a) w |= ((prm.costrow[a] >> (8 * b)) & 0xFFu) << (8 * a);
+        for (int a = 0; a < 4; ++a) w |= ((prm.costrow16[a] >> (8 * b)) & 0xFFu) << (8 * a);
         colrow[b] = w;
     }
     const uint32_t *pbP = seqb + dP.b_off, *pbQ = seqb + dQ.b_off;
@@ -179,27 +179,24 @@ __global__ __launch_bounds__(256) void sed_lane_i32x2_kernel(const sed_pair_desc
         colQ[j] = (bq & 2u) ? ((bq & 1u) ? colrow[3] : colrow[2]) : ((bq & 1u) ? colrow[1] : colrow[0]);
     }
 #pragma unroll
-    for (int j = 0; j <= MM; ++j) V[j] = (uint32_t)j * kins;  // row 0: j inserts, both halves
+    for (int j = 0; j <= MM; ++j) V[j] = 0xFFFFFFFFu;  // row 0 and column 0: offset key 0xFFFF, both halves
     const uint32_t *paP = seqa + dP.a_off, *paQ = seqa + dQ.a_off;
-    uint32_t waP = 0, waQ = 0, colv = 0;
+    uint32_t waP = 0, waQ = 0;
     for (int i = 0; i < n; ++i) {
         if ((i & 15) == 0) {
             waP = paP[i >> 4];
             waQ = paQ[i >> 4];
         }
         const uint32_t aP = (waP >> (2 * (i & 15))) & 3u, aQ = (waQ >> (2 * (i & 15))) & 3u;
-        // perm: byte0 <- colP byte aP (S1), byte2 <- colQ byte aQ (S0), bytes 1, 3 <- 0
-        const uint32_t sel = 0x0C000C00u | aP | ((4u + aQ) << 16);
+        // perm: byte0 <- colP byte aP (S1), byte2 <- colQ byte aQ (S0), bytes 1, 3 <- 0xFF
+        const uint32_t sel = 0x0D000D00u | aP | ((4u + aQ) << 16);
         uint32_t dg = pk_add(V[0], __builtin_amdgcn_perm(colQ[0], colP[0], sel));
-        colv += kdel;  // column 0: i deletes
-        V[0] = colv;
-        uint32_t left = colv;
+        uint32_t left = V[0];  // column 0 stays 0xFFFF
 #pragma unroll
         for (int j = 1; j <= MM; ++j) {
             const uint32_t up = V[j];
-            const uint32_t cdel = pk_add(up, kdel);
             const uint32_t dnext = j < MM ? pk_add(up, __builtin_amdgcn_perm(colQ[j], colP[j], sel)) : 0u;
-            const uint32_t v = pk_min(pk_min(pk_add(left, kins), cdel), dg);
+            const uint32_t v = pk_min(pk_min(up, dg), left);  // left (this row's chain) enters last
             dg = dnext;
             V[j] = v;
             left = v;
@@ -215,7 +212,9 @@ __global__ __launch_bounds__(256) void sed_lane_i32x2_kernel(const sed_pair_desc
     r.len = -1;
     r.err = 0;
     r.pad[0] = r.pad[1] = 0;
-    const uint32_t DP = capP & 0xFFFFu, DQ = capQ >> 16;
+    // 16-bit offset keys back to D: D = W - 0xFFFF + n*delete + m*insert (mod 2^16)
+    const uint32_t DP = ((capP & 0xFFFFu) + 1u + (uint32_t)n * prm.del + (uint32_t)mP * prm.ins) & 0xFFFFu;
+    const uint32_t DQ = ((capQ >> 16) + 1u + (uint32_t)n * prm.del + (uint32_t)mQ * prm.ins) & 0xFFFFu;
     r.dist = (double)DP;
     r.is_int = (DP == 0);
     res[P] = r;

@@ -143,14 +143,26 @@ bool i32_eligible(const sed_ctx *c) {
     if (c->K > 4) return false;
     if (c->ins_int || c->del_int) return false;
     if (!is_integral_small(c->ins, 256) || !is_integral_small(c->del, 256) || c->ins < 1 || c->del < 1) return false;
+    // offset keys (sed_kernels.hip): the update constant cost - insert - delete - 1 is one byte
+    // below 0xFF, i.e. 0 <= cost <= insert + delete <= 255
+    if (c->ins + c->del > 255) return false;
     for (int e = 0; e < c->K * c->K; ++e) {
         const double v = c->sub[e];
         if (c->sub_int[e]) {
             if (v != 0) return false;
-        } else if (!is_integral_small(v, 256) || v < 1) {
+        } else if (!is_integral_small(v, 256) || v < 1 || v > c->ins + c->del) {
             return false;
         }
     }
+    return true;
+}
+
+// 16-bit packed distance keys (i32x2 kernels) need every substitution strictly cheaper than
+// delete + insert: their update constant cost - delete - insert is a 16-bit 0xFFxx.
+bool x2_costs_ok(const sed_ctx *c) {
+    for (int a = 0; a < c->K; ++a)
+        for (int bb = 0; bb < c->K; ++bb)
+            if (a != bb && !(c->sub[a * c->K + bb] < c->ins + c->del)) return false;
     return true;
 }
 
@@ -226,10 +238,12 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         const int ROWS = 64 * R;
         bool fits = true;
         for (int p = 0; p < npairs && fits; ++p) {
+            // offset keys: i*delete + j*insert over every computed cell (padded rows, the columns
+            // the wave or the lane kernel runs past m) must stay below the bias, and L < 2^14
             const double npad = (double)((len_a[p] + ROWS - 1) / ROWS) * ROWS;
-            const double dmax = npad * c->del + (double)len_b[p] * c->ins;
-            // 256 of headroom: the ramp's sentinel update cost (0xFF << 16) is added to border values
-            if (dmax >= 65536.0 - 256.0 || npad + len_b[p] >= 16384.0) fits = false;
+            const double cols = (double)std::max(len_b[p] + 64 + 64 / R, SED_LANE_MAXM);
+            const double dsum = npad * c->del + cols * c->ins;
+            if (dsum > 65533.0 || npad + cols >= 16384.0) fits = false;
         }
         if (!fits) {
             if (c->opt_mode == 1) return c->fail(SED_E_RANGE, "integer key would overflow (D < 2^16, L < 2^14)");
@@ -313,7 +327,12 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // distance-only integer lane pairs: two pairs of equal n per lane (sed_lane.hip: i32x2). Stable
     // sort by n, pair neighbours of equal n; a pair without a partner shares its lane with itself.
     b->nlane_x2 = 0;
-    if (mode == SED_MODE_I32 && !want_tb && (flags & SED_NO_LEN) && c->opt_pack != 2 && !lane_idx.empty()) {
+    const bool x2_ok = mode == SED_MODE_I32 && x2_costs_ok(c);
+    // 16-bit offset keys: n*delete + 32*insert (the lane kernel's whole block) within 0xFFFF
+    bool lane_fit16 = true;
+    for (int32_t x : lane_idx)
+        if ((double)len_a[x] * c->del + SED_LANE_MAXM * c->ins > 65535.0) lane_fit16 = false;
+    if (x2_ok && lane_fit16 && !want_tb && (flags & SED_NO_LEN) && c->opt_pack != 2 && !lane_idx.empty()) {
         std::stable_sort(lane_idx.begin(), lane_idx.end(), [&](int32_t x, int32_t y) { return len_a[x] < len_a[y]; });
         std::vector<int32_t> two;
         two.reserve(lane_idx.size() + 1);
@@ -335,10 +354,14 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // so the other wave kernels (and CHAIN mode) skip them.
     std::vector<int32_t> x2;
     b->nwave_x2 = 0;
-    if (mode == SED_MODE_I32 && !split && !want_tb && (flags & SED_NO_LEN) && c->opt_pack != 2 && b->nwave > 1) {
+    if (x2_ok && !split && !want_tb && (flags & SED_NO_LEN) && c->opt_pack != 2 && b->nwave > 1) {
         std::vector<int32_t> w;
-        for (int p = 0; p < npairs; ++p)
-            if (!b->pd[p].lane && len_a[p] > 0 && len_b[p] > 0) w.push_back(p);
+        for (int p = 0; p < npairs; ++p) {
+            // 16-bit offset keys over the wave's block: padded rows x (m + 63 + G) columns within 0xFFFF
+            const double npad = (double)((len_a[p] + ROWS - 1) / ROWS) * ROWS;
+            const bool fit16 = npad * c->del + (double)(len_b[p] + 64 + 64 / R) * c->ins <= 65535.0;
+            if (!b->pd[p].lane && len_a[p] > 0 && len_b[p] > 0 && fit16) w.push_back(p);
+        }
         std::stable_sort(w.begin(), w.end(), [&](int32_t x, int32_t y) {
             return len_a[x] != len_a[y] ? len_a[x] < len_a[y] : len_b[x] < len_b[y];
         });
@@ -469,16 +492,19 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // ---- kernel parameters ----
     if (mode == SED_MODE_I32) {
         sed_i32_params ip{};
-        for (int a = 0; a < 4; ++a) {
-            uint32_t row = 0;
-            for (int bb = 0; bb < 4; ++bb) {
-                const double v = (a < c->K && bb < c->K) ? c->sub[a * c->K + bb] : 0.0;
-                row |= (uint32_t)v << (8 * bb);
-            }
-            ip.costrow[a] = row;
-        }
         ip.ins = (uint32_t)c->ins;
         ip.del = (uint32_t)c->del;
+        for (int a = 0; a < 4; ++a) {
+            uint32_t row = 0, row16 = 0;
+            for (int bb = 0; bb < 4; ++bb) {
+                // symbols outside the alphabet never occur in real cells: any cost <= ins + del will do
+                const uint32_t v = (a < c->K && bb < c->K) ? (uint32_t)c->sub[a * c->K + bb] : 0u;
+                row |= ((v - ip.ins - ip.del - 1u) & 0xFFu) << (8 * bb);
+                row16 |= ((v - ip.ins - ip.del) & 0xFFu) << (8 * bb);
+            }
+            ip.costrow[a] = row;
+            ip.costrow16[a] = row16;
+        }
         ip.kins = (ip.ins << 16) + 4u;
         ip.kdel = (ip.del << 16) + 5u;
         b->ip = ip;
