@@ -38,10 +38,11 @@ SIMDS, CLOCK = 1024, 2.4e9
 # VALU ceiling of the integer kernels: every op of the dependent DP cell issues at ~4 cycles per wave64
 # instruction on gfx950 whatever the op mix (tools/ubench/valu_mix.hip, valu_row.hip: 4.0-4.2 cycles/op,
 # the nominal 2-cycle ops do not pair when interleaved with the 4-cycle v_perm/v_min3/v_alignbit).
-# Ops per cell in offset-key space (sed_kernels.hip): perm + add + min3 (+ delete op bit + and clearing the op for the
-# op-count field) (+ alignbit for the traceback); packed distance keys: perm + pk_add + 2 pk_min per 2 cells.
+# Ops per cell in offset-key space (sed_kernels.hip): perm + add + min3 (+ and_or clearing the op for the
+# op-count field, + the ladder's delete add on 3 of 16 rows) (+ alignbit for the traceback); packed distance
+# keys: perm + pk_add + 2 pk_min per 2 cells.
 VALU_CYCLES_PER_OP = 4.0
-CELL_OPS = {"script": 6, "len": 5, "nolen": 3, "nolen_x2": 2}
+CELL_OPS = {"script": 5 + 3 / 16, "len": 4 + 3 / 16, "nolen": 3, "nolen_x2": 2}
 
 WORKLOADS = {
     # name: (pairs per GPU, n, m, cost table, description)
@@ -339,7 +340,7 @@ def main():
                      "kernel": kname,
                      "kernel_ms": dp_avg, "algo_bytes_per_launch": algo_bytes},
         "valu": None if valu_peak is None else {
-            "model": "%d VALU ops/cell x %.1f cycles/op per wave64 (tools/ubench/valu_row.hip), 1024 SIMDs, %.1f GHz"
+            "model": "%.4g VALU ops/cell x %.1f cycles/op per wave64 (tools/ubench/valu_row.hip), 1024 SIMDs, %.1f GHz"
                      % (ops_cell, VALU_CYCLES_PER_OP, CLOCK / 1e9),
             "achieved": rate, "peak": valu_peak, "unit": "cells/s", "frac": rate / valu_peak},
         "traceback_ms": float(np.mean(tb_ms)) if want_script else None,

@@ -51,7 +51,7 @@ enum {
  * run k overlaps the DP kernel of run k+1 (device memory for the traceback triples). */
 #define SED_PIPELINE 2u
 /* distance only (no SED_WANT_SCRIPT): out_len is not computed (-1), which lets the integer
- * kernels drop the op-count field of their keys (5 instead of 6 VALU ops per cell). */
+ * kernels drop the op-count field of their keys (3 instead of ~4.2 VALU ops per cell). */
 #define SED_NO_LEN 4u
 
 /* sed_set_option keys */

@@ -30,9 +30,9 @@ struct sed_result {
 // Integer kernel constants (offset-key space, see sed_kernels.hip):
 //   costrow[a]   byte b = (cost(a -> b) - insert - delete - 1) & 0xFF  (32-bit keys)
 //   costrow16[a] byte b = (cost(a -> b) - insert - delete) & 0xFF      (16-bit packed distance keys)
-//   kins = (insert << 16) + 4, kdel = (delete << 16) + 5: the V-space insert / delete increments
-//   (op included); the offsets per column / row are kins and kdel - 1.
-#define SED_KB 0xFFFFFFFCu  // bias B of the 32-bit offset keys (B = 0 mod 4)
+//   kins = (insert << 16) + 4, kdel = (delete << 16) + 5: the lane kernels' key increments (op included;
+//   their offsets per column / row are kins and kdel - 1).  The wave kernels derive their own from ins/del.
+#define SED_KB 0xFFFFFFFCu  // bias of the 32-bit distance-only offset keys (sed_kernels.hip)
 struct sed_i32_params {
     uint32_t costrow[4];
     uint32_t costrow16[4];
@@ -66,6 +66,7 @@ struct sed_launch {
     sed_result *res;
     int R;
     hipStream_t stream;
+    bool tb_ladder;     // traceback codes of the integer kernels carry the row's ladder rung (sed_kernels.hip)
     const int2 *tasks;  // SPLIT mode: (pair, stripe) per workgroup, else nullptr
     uint32_t *prog;     // SPLIT mode: per-stripe published-column counters (zeroed before each run)
     int ntasks;         // 0 -> one wave per pair
@@ -85,7 +86,7 @@ hipError_t sed_launch_f64(const sed_launch &L, const double *gtab, const sed_f64
 hipError_t sed_launch_f64_full(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed,
                                const sed_full_out &fo);
 // Lane-per-pair integer kernel (sed_lane.hip): pairs idx[0..nidx) with 1 <= m <= SED_LANE_MAXM.
-// len = false: distance only, no op-count field (5 VALU per cell).
+// len = false: distance only, no op-count field (3 VALU per cell).
 #define SED_LANE_MAXM 32
 #define SED_LANE_MAXN 512
 hipError_t sed_launch_lane_i32(const sed_launch &L, const int32_t *idx, int nidx, const sed_i32_params &prm, bool len);

@@ -98,56 +98,85 @@ __device__ __forceinline__ void store_tb(uint32_t *p, const uint32_t (&w)[4]) {
 // Integer (packed-key) kernels.  The reference's decision per cell is the
 // lexicographic minimum of (distance, path length, op) over its candidates, i.e.
 // one unsigned min over the keys
-//     V = D << 16 | L << 2 | op      (D < 2^16, L < 2^14; op 0 insert, 1 delete, 2 update)
-// with candidates V_left + kins, V_up + kdel, V_diag + (cost << 16) + 6, where
-// kins = (insert << 16) + 4 and kdel = (delete << 16) + 5 carry their op.
+//     V = D << 16 + L << 3 + op        (op 0 insert, 1 delete, 2 update)
+// with candidates V_left + Ki, V_up + Kd + 1, V_diag + (cost << 16) + 10, where
+// Ki = (insert << 16) + 8 and Kd = (delete << 16) + 8.  The L field may run past
+// its 13 bits: the three candidates of cell (i, j) have L in [max(i,j), i+j],
+// so 8 * |L difference| <= 8 * min(n, m) < 2^16 and any distance difference
+// still dominates (the host keeps min(n, m) < 8192); at the sink L is read
+// modulo 8192 inside that window.
 //
 // Offset keys.  Subtracting the same amount from the three candidates of a cell
 // keeps their order, so cells are stored as
-//     W(i, j) = V(i, j) - i*Kd - j*kins + B    (Kd = kdel - 1, B = SED_KB = 2^32 - 4)
-// where i*Kd + j*kins bounds V from above (the all-delete-then-insert path) and
-// the host checks that it stays below B, so W never wraps.  In W space
-//     insert candidate = W_left,  delete candidate = W_up + 1 (its op),
-//     update candidate = W_diag + ((cost - delete - insert) << 16) - 2
-// and every border is the constant B.  The update constant is one v_perm_b32 of
-// a per-row byte vector (cost - delete - insert - 1, the bytes below it
-// 0xFF/0xFE; the host requires cost <= insert + delete), so a cell costs v_perm,
-// 2 v_add, v_min3, v_and, v_alignbit = 6 VALU.  Offsets are = 0 (mod 4), so
-// mm = min3 carries the winning op in its low 2 bits exactly as in V space.
-// (Folding the delete's op bit into the row offset as well would save the add,
-// but then the clean value's low bits rotate with the row and clearing the op
-// is no longer one instruction for every row.)
+//     W(i, j) = V(i, j) - i*Kd - j*Ki + B + c(i)        (B = SED_KB3)
+// where i*Kd + j*Ki bounds V from above (the all-delete-then-insert path) and
+// the host checks that it stays below B, so W never wraps.  c(i) in 0..5 is a
+// per-row residue ("ladder") that steps down by one from row to row and jumps
+// back up on a few rows (Ladder<R> below, periodic in i with a period dividing
+// R, so every lane row has a compile-time rung).  With d = c(i) - c(i-1):
+//     insert candidate = W_left,
+//     delete candidate = W_up + (d + 1)          (no add on the d = -1 rows),
+//     update candidate = W_diag + ((cost - delete - insert) << 16) - 6 + d.
+// The update constant is one v_perm_b32 of a per-row byte vector (cost - delete
+// - insert - 1; the bytes below it 0xFF / (d - 6) from the inline constant d - 6;
+// the host requires cost <= insert + delete).  mm = min3 is a clean value (low 3
+// bits = c(i)) plus the winning op, which never leaves the 8-block because
+// c(i) + 2 <= 7, so clearing the op is one v_and_or: (mm & ~7) | c(i).  A cell
+// therefore costs v_perm, v_add, v_min3, v_and_or, v_alignbit = 5 VALU, plus the
+// delete add on 3 of 16 rows.  The traceback codes are mm's low 2 bits
+// (c(i) + op) & 3; the traceback kernels subtract the rung of the row they are on.
+// Every border is a constant: W(0, j) = B, W(i, 0) = B + c(i).
+//
 // Distance only (!LEN): keys are D << 16 without the L/op field, W = V -
-// i*(delete << 16) - j*(insert << 16) + B, update constant ((cost - delete -
+// i*(delete << 16) - j*(insert << 16) + SED_KB, update constant ((cost - delete -
 // insert) << 16) - 1: an update also subtracts 1 from the low half, which never
 // borrows (fewer than 2^16 updates on any path), so D = (V + 0xFFFF) >> 16.
-// That is v_perm, v_add, v_min3 = 3 VALU per cell.
+// That is v_perm, v_add, v_min3 = 3 VALU per cell; every border is SED_KB.
 // Lanes run unmasked all the time, and a lane past column m computes columns
 // that nothing reads.
 // ---------------------------------------------------------------------------
+#define SED_KB3 0xFFFFFE00u  // bias of the ladder keys (= 0 mod 8, 512 below 2^32 for the ramp sentinel)
+
+// The ladder: rung c(i) of row i by i mod P, 4 bits per rung; runs of 5,4,3,2,1,0 as long as the
+// period allows (P = 16: jumps at i = 1, 7, 11 (mod 16); P = 8: at 1, 7; P = 4: at 1).
+template <int R> struct Ladder {
+    static constexpr int P = R >= 16 ? 16 : R;
+    static constexpr uint64_t pat = P == 16 ? 0x1234501230123450ull : (P == 8 ? 0x10123450ull : 0x1230ull);
+    static constexpr int rung(int i) { return (int)((pat >> (4 * (i & (P - 1)))) & 0xF); }
+};
+
 // One column step of a lane's R rows.  tv = {top, sel} of this step's column
 // for lane 0 (the stripe's top row and str2 symbol): every lane reads the same
-// LDS word, only lane 0 keeps it (the DPP move's `old` operand).
+// LDS word, only lane 0 keeps it (the DPP move's `old` operand).  Lane rows are
+// i = (multiple of P) + r + 1, so row r sits on rung Ladder::rung(r + 1).
 template <int R, bool TB, bool LEN>
 __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                          uint32_t &bottom, uint32_t &selv, const uint2 tv, uint32_t &outc,
                                          uint32_t (&W)[4], const int u) {
+    using Lad = Ladder<R>;
     const uint32_t topv = dpp_shr1(tv.x, bottom);  // cell above the band, this column
     selv = dpp_shr1(tv.y, selv);                   // perm selector of this column's str2 symbol
     uint32_t up = topv, diag = top_prev;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const uint32_t left = V[r];
-        // insert (op 0) = left, delete (op 1) = up + 1, update (op 2) = diag + the row's offset constant;
-        // perm bytes 1:0 come from the inline constant -2 (0xFFFE) or -1 (0xFFFF)
-        const uint32_t mm = umin3(left, LEN ? up + 1u : up,
-                                  diag + __builtin_amdgcn_perm(cv[r], LEN ? 0xFFFFFFFEu : 0xFFFFFFFFu, selv));
-        if constexpr (TB) {
-            const int c = u * R + r;  // compile-time after unrolling
-            W[c >> 4] = __builtin_amdgcn_alignbit(mm, W[c >> 4], 2);
+        uint32_t mm;
+        if constexpr (LEN) {
+            const int c = Lad::rung(r + 1), d = c - Lad::rung(r);  // compile-time after unrolling
+            // insert (op 0) = left, delete (op 1) = up + d + 1, update (op 2) = diag + offset constant
+            // (perm bytes 1:0 from the inline constant d - 6)
+            mm = umin3(left, d == -1 ? up : up + (uint32_t)(d + 1),
+                       diag + __builtin_amdgcn_perm(cv[r], (uint32_t)(d - 6), selv));
+            if constexpr (TB) {
+                const int k = u * R + r;
+                W[k >> 4] = __builtin_amdgcn_alignbit(mm, W[k >> 4], 2);
+            }
+            up = (mm & ~7u) | (uint32_t)c;
+        } else {
+            mm = umin3(left, up, diag + __builtin_amdgcn_perm(cv[r], 0xFFFFFFFFu, selv));
+            up = mm;
         }
         diag = left;
-        up = LEN ? (mm & ~3u) : mm;
         V[r] = up;
     }
     top_prev = topv;
@@ -155,21 +184,26 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
     outc = dpp_shl1(bottom, outc);
 }
 
-// Column-0 state of rows row0+1 .. row0+R (and of row0, the diagonal of the first column): every
-// border is the offset key B.
-template <int R>
+// Column-0 state of rows row0+1 .. row0+R (row0 = multiple of P) and of row0, the diagonal of the
+// first column.
+template <int R, bool LEN>
 __device__ __forceinline__ void i32_reset(uint32_t (&V)[R], uint32_t &top_prev) {
-    top_prev = SED_KB;
+    top_prev = LEN ? SED_KB3 : SED_KB;
 #pragma unroll
-    for (int r = 0; r < R; ++r) V[r] = SED_KB;
+    for (int r = 0; r < R; ++r) V[r] = LEN ? SED_KB3 + (uint32_t)Ladder<R>::rung(r + 1) : SED_KB;
 }
+// row 0 (D = j*insert, L = j) in offset keys
+template <bool LEN> __device__ __forceinline__ uint32_t i32_row0() { return LEN ? SED_KB3 : SED_KB; }
 
-// The sink cell back to V space: V = W - B + n*Kd + m*kins; returns {D, L} (L = -1 without LEN).
-template <bool LEN>
+// The sink cell (n, m) back to V space; returns {D, L} (L = -1 without LEN).
+template <int R, bool LEN>
 __device__ __forceinline__ int2 i32_decode(uint32_t w, int n, int m, const sed_i32_params &prm) {
     if constexpr (LEN) {
-        const uint32_t v = w - SED_KB + (uint32_t)n * (prm.kdel - 1u) + (uint32_t)m * prm.kins;
-        return make_int2((int)(v >> 16), (int)((v >> 2) & 0x3FFFu));
+        const uint32_t v = w - SED_KB3 - (uint32_t)Ladder<R>::rung(n) + (uint32_t)n * ((prm.del << 16) + 8u) +
+                           (uint32_t)m * ((prm.ins << 16) + 8u);
+        const uint32_t lo = (uint32_t)max(n, m);
+        const uint32_t L = lo + ((((v >> 3) & 0x1FFFu) - lo) & 0x1FFFu);  // L in [max(n,m), n+m]
+        return make_int2((int)((v - 8u * L) >> 16), (int)L);
     } else {
         const uint32_t v = w - SED_KB + (((uint32_t)n * prm.del + (uint32_t)m * prm.ins) << 16);
         return make_int2((int)((v + 0xFFFFu) >> 16), -1);
@@ -178,11 +212,15 @@ __device__ __forceinline__ int2 i32_decode(uint32_t w, int n, int m, const sed_i
 
 // Ramp for free.  Every lane starts a stripe at its column-0 state and lane t begins real work
 // at step t.  Before that it runs "virtual" columns, which leave its state unchanged: their str2
-// selector is the sentinel SED_SEL_SENT (update constant 0), so with every neighbour at its
-// column-0 value B the candidates are B (insert), B + 1 (delete) and B + 0 (update), and the
-// minimum B keeps the border (op bits 0).  The lane's first real column then sees exactly
-// D[row][0], D[row-1][0] and the cell above.
+// selector is a sentinel, so with every neighbour at its column-0 value the insert candidate
+// (the border itself) is the minimum and keeps the border:
+//   ladder keys: insert B + c(i), delete B + c(i) + 1, update B + c(i-1) + 255 (SED_SEL_SENT3:
+//   update constant 0xFF >= any jump d);
+//   distance keys (and the 16-bit packed ones): insert = delete = border, update border + 0.
+// The lane's first real column then sees exactly D[row][0], D[row-1][0] and the cell above.
 #define SED_SEL_SENT 0x0C0C0C0Cu
+#define SED_SEL_SENT3 0x0C0C0C0Du
+template <bool LEN> __device__ __forceinline__ uint32_t i32_sent() { return LEN ? SED_SEL_SENT3 : SED_SEL_SENT; }
 // perm selector of str2 symbol b: byte3 <- 0xFF, byte2 <- cost byte b, bytes 1:0 <- the constant
 __device__ __forceinline__ uint32_t i32_sel(uint32_t b) { return 0x0D000100u | ((4u + b) << 16); }
 
@@ -210,9 +248,10 @@ __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)
     }
 }
 
-// Minimum waves per SIMD the register allocator must leave room for, per R
-// (R=16: 80 VGPRs / 6 waves measured fastest by tools/sweep.sh; R=32: 128 VGPRs / 4 waves).
-template <int R> struct I32Waves { static constexpr int value = R >= 32 ? 4 : (R == 16 ? 6 : 8); };
+// Minimum waves per SIMD the register allocator must leave room for, per R: the budget at which
+// the hot loop does not spill (R=16: 96 VGPRs / 5 waves; the 80-VGPR budget of 6 waves spills the
+// cost rows and ran 2.5x slower; R=4/8: 72 / 7; R=32: 128 / 4, which still spills: never chosen).
+template <int R> struct I32Waves { static constexpr int value = R >= 32 ? 4 : (R == 16 ? 5 : 7); };
 #ifdef SED_I32_WAVES_PER_EU
 #define SED_I32_WAVES(R) SED_I32_WAVES_PER_EU
 #else
@@ -309,14 +348,14 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             cv[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
         }
         uint32_t top_prev;
-        i32_reset<R>(V, top_prev);
+        i32_reset<R, LEN>(V, top_prev);
         // column-0 state for every lane; virtual columns until the lane's first real one (see above)
-        uint32_t bottom = V[R - 1], selv = SED_SEL_SENT, outc = 0;
+        uint32_t bottom = V[R - 1], selv = i32_sent<LEN>(), outc = 0;
         uint32_t W[4] = {0, 0, 0, 0};
 
         auto load_top = [&](int c) -> uint32_t {
             const int j = 64 * c + lane + 1;
-            if (k == 0) return SED_KB;  // row 0: D = j*insert, L = j (offset key B)
+            if (k == 0) return i32_row0<LEN>();
             if constexpr (SPLIT) {  // after one timeout stop waiting: the kernel must still drain quickly
                 if (ok) ok = wait_progress(prog + d.prog_off + k - 1, prm.epoch << 16, (uint32_t)min(m, 64 * c + 64));
             }
@@ -362,7 +401,7 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
         if (!last) __builtin_amdgcn_s_waitcnt(0);  // own bottom-row stores done before the next stripe reads them
     }
     if (klast == nstripes - 1 && lane == cap_lane) {
-        const int2 dl = i32_decode<LEN>(cap, n, m, prm);
+        const int2 dl = i32_decode<R, LEN>(cap, n, m, prm);
         res[pair].dist = (double)dl.x;
         res[pair].len = dl.y;
         res[pair].is_int = (dl.x == 0);
@@ -611,7 +650,7 @@ __device__ __forceinline__ void i32_chain_group(uint32_t (&V)[R], uint32_t (&cv)
 template <int R, bool TB, bool LEN>
 __device__ __forceinline__ void chain_store_result(sed_result *__restrict__ res, int pair, uint32_t cap, int n,
                                                    int m, const sed_i32_params &prm) {
-    const int2 dl = i32_decode<LEN>(cap, n, m, prm);
+    const int2 dl = i32_decode<R, LEN>(cap, n, m, prm);
     res[pair].dist = (double)dl.x;
     res[pair].len = dl.y;
     res[pair].is_int = (dl.x == 0);
@@ -653,7 +692,7 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
 
     // per-lane constants: column-0 state of this lane's rows (the same for every pair)
     uint32_t Vb[R], tpb;
-    i32_reset<R>(Vb, tpb);
+    i32_reset<R, LEN>(Vb, tpb);
     auto rows_of = [&](int pair, uint32_t (&out)[R]) {
         const uint32_t *pa = seqa + pd[pair].a_off;
 #pragma unroll
@@ -666,7 +705,7 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
     auto chunk_of = [&](const chain_pair_state &c, int cl) -> uint2 {  // lane 0's inputs, local chunk cl
         const int j = 64 * cl + lane;
         const uint32_t b = (c.pb[j >> 4] >> ((j & 15) * 2)) & 3u;
-        return make_uint2(SED_KB, i32_sel(b));  // row 0 (offset key B), str2 selector
+        return make_uint2(i32_row0<LEN>(), i32_sel(b));  // row 0, str2 selector
     };
 
     chain_pair_state cur = chain_load<R>(pd, seqb, chain_pairs[c0], 0), prv = cur;
@@ -679,7 +718,7 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
         V[r] = Vb[r];
         cvn[r] = cv[r];
     }
-    uint32_t top_prev = tpb, bottom = V[R - 1], selv = SED_SEL_SENT, outc = 0, capA = 0, capB = 0;
+    uint32_t top_prev = tpb, bottom = V[R - 1], selv = i32_sent<LEN>(), outc = 0, capA = 0, capB = 0;
     uint32_t W[4] = {0, 0, 0, 0};
     lch[lane] = chunk_of(cur, 0);
 
@@ -1028,8 +1067,8 @@ template <int R>
 __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
                                                            const uint32_t *__restrict__ tb,
                                                            const sed_result *__restrict__ res,
-                                                           uint32_t *__restrict__ ops) {
-    constexpr int G = Grp<R>::G;
+                                                           uint32_t *__restrict__ ops, const uint64_t pat) {
+    constexpr int G = Grp<R>::G, P = Ladder<R>::P;
     const int pair = blockIdx.x * blockDim.x + threadIdx.x;
     if (pair >= npairs) return;
     const sed_pair_desc d = pd[pair];
@@ -1067,7 +1106,8 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
             }
             const int wsel = c >> 4;
             const uint32_t wv = (wsel & 2) ? ((wsel & 1) ? cw.w : cw.z) : ((wsel & 1) ? cw.y : cw.x);
-            const uint32_t op = (wv >> (2 * (c & 15))) & 3u;
+            // integer codes are (rung(i) + op) & 3 (pat = the ladder), fp64 codes op (pat = 0)
+            const uint32_t op = ((wv >> (2 * (c & 15))) - (uint32_t)(pat >> (4 * (i & (P - 1))))) & 3u;
             emit(op);
             if (op != 1) --j;
             if (op != 0) {  // move up one row
@@ -1100,8 +1140,9 @@ template <int R>
 __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair_desc *__restrict__ pd,
                                                                   int npairs, const uint32_t *__restrict__ tb,
                                                                   const sed_result *__restrict__ res,
-                                                                  uint32_t *__restrict__ ops) {
+                                                                  uint32_t *__restrict__ ops, const uint64_t pat) {
     constexpr int G = Grp<R>::G, NT = G, NS = R;  // NT * NS = 64 blocks
+    constexpr int P = Ladder<R>::P;
     constexpr int LR = R == 4 ? 2 : R == 8 ? 3 : R == 16 ? 4 : 5, LG = 6 - LR;
     static_assert((1 << LR) == R, "R must be a power of two in 4..32");
     const int lane = threadIdx.x;
@@ -1150,7 +1191,8 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
                      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(wv.w, L) << 32);
             }
             const uint32_t c = ((uint32_t)(s & (G - 1)) << LR) | r;  // code index inside the block
-            const uint32_t op = (uint32_t)(((c & 32u) ? hi : lo) >> (2u * c & 63u)) & 3u;
+            const uint32_t op =  // minus the ladder rung of row i (sed_traceback_kernel)
+                ((uint32_t)(((c & 32u) ? hi : lo) >> (2u * c & 63u)) - (uint32_t)(pat >> (4 * (i & (P - 1))))) & 3u;
             emit(op);
             const uint32_t di = (op + 1u) >> 1, dj = (5u >> op) & 1u;  // row move (del, upd), column move (ins, upd)
             i -= (int)di;
@@ -1298,14 +1340,16 @@ hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops) {
     const int grid = uni ? L.npairs : (L.npairs + 63) / 64;
     switch (L.R) {
 #define CASE(RR)                                                                                                 \
-    case RR:                                                                                                     \
+    case RR: {                                                                                                   \
+        const uint64_t pat = L.tb_ladder ? Ladder<RR>::pat : 0ull;                                               \
         if (uni)                                                                                                 \
             hipLaunchKernelGGL((sed_traceback_window_kernel<RR>), dim3(grid), dim3(64), 0, L.stream, L.pd,       \
-                               L.npairs, L.tb, L.res, ops);                                           \
+                               L.npairs, L.tb, L.res, ops, pat);                                                \
         else                                                                                                     \
             hipLaunchKernelGGL((sed_traceback_kernel<RR>), dim3(grid), dim3(64), 0, L.stream, L.pd,              \
-                               L.npairs, L.tb, L.res, ops);                                           \
-        break;
+                               L.npairs, L.tb, L.res, ops, pat);                                                \
+        break;                                                                                                   \
+    }
         CASE(4) CASE(8) CASE(16) CASE(32)
 #undef CASE
     default: return hipErrorInvalidValue;

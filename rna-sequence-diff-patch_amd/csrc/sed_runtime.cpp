@@ -349,8 +349,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
 
     // distance-only integer wave pairs: two of equal n per wave (sed_kernels.hip: i32x2), the one with
     // the larger m first (its bottom-row buffer serves both).  Partners come from a (n, m) sort and
-    // must have m within 4x of each other: the wave runs max(m) columns at 6 ops per 2 cells, which beats
-    // 5 ops per cell of each pair alone while min(m) > max(m) / 5.  Packed pairs are marked lane = 2,
+    // must have 3 min(m) > max(m): the wave runs max(m) columns at 4 ops per 2 cells, which beats 3 ops
+    // per cell of each pair alone while 4 max(m) < 3 (m_P + m_Q).  Packed pairs are marked lane = 2,
     // so the other wave kernels (and CHAIN mode) skip them.
     std::vector<int32_t> x2;
     b->nwave_x2 = 0;
@@ -367,7 +367,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         });
         for (size_t q = 0; q + 1 < w.size();) {
             const int32_t x = w[q], y = w[q + 1];  // len_b[x] <= len_b[y]
-            if (len_a[x] == len_a[y] && 4LL * len_b[x] >= len_b[y]) {
+            if (len_a[x] == len_a[y] && 3LL * len_b[x] > len_b[y]) {
                 x2.push_back(y);
                 x2.push_back(x);
                 b->pd[x].lane = b->pd[y].lane = 2;
@@ -548,6 +548,7 @@ int run_batch(sed_batch *b) {
     L.res = (sed_result *)b->d_res[k].p;
     L.R = b->R;
     L.stream = c->stream;
+    L.tb_ladder = b->mode == SED_MODE_I32;
     L.tasks = b->split ? (const int2 *)b->d_tasks.p : nullptr;
     L.prog = (uint32_t *)b->d_prog.p;
     L.ntasks = b->split ? b->ntasks : 0;

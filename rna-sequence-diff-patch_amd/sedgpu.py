@@ -134,7 +134,7 @@ class Context:
 
     def run(self, packed, want_script, no_len=False):
         """packed: PackedPairs.  Returns (dist f64[], is_int u8[], len i32[], ops u32[] | None).
-        no_len (distance only): lengths are not computed (-1), the integer kernels run 5 ops/cell."""
+        no_len (distance only): lengths are not computed (-1), the integer kernels run 3 ops/cell."""
         np_ = packed.npairs
         dist = np.zeros(max(np_, 1), np.float64)
         is_int = np.zeros(max(np_, 1), np.uint8)
