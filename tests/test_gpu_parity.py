@@ -335,3 +335,53 @@ def test_wave_x2_packed_distance_vs_oracle(gpu, tables, R):
     got = gpu_run(gpu, tables[user], pairs, R=R, split=2, script=False, no_len=True)
     _oracle_check(tables[user], pairs, got, no_len=True)
     assert got == gpu_run(gpu, tables[user], pairs, R=R, split=2, script=False, no_len=True, pack=2)
+
+
+def _int_table(ins, dele, sub):
+    """An integer cost table over ACGU in the reference's format (sub(a, b) for a != b)."""
+    return {"insert": float(ins), "delete": float(dele),
+            "update": {a: {b: (0.0 if a == b else float(sub(a, b))) for b in "ACGU"} for a in "ACGU"}}
+
+
+@pytest.mark.parametrize("case", ["sum", "over", "wide", "tight"])
+def test_offset_key_eligibility_edges(gpu, case):
+    """The offset-key kernels need cost <= insert + delete <= 255 (sed_runtime.cpp: i32_eligible) and the
+    16-bit packed distance keys cost < insert + delete.  At the edges: substitutions costing exactly
+    insert + delete stay on the integer kernel (packing off), costlier ones or insert + delete > 255 fall
+    back to fp64; every route bit-exact against the oracle (script, length, distance-only packed/unpacked)."""
+    rng = np.random.default_rng(77)
+    tabs = {
+        "sum": (_int_table(1, 2, lambda a, b: 3), "i32"),
+        "over": (_int_table(1, 1, lambda a, b: 3 if (a, b) == ("A", "C") else 1), "f64"),
+        "wide": (_int_table(200, 100, lambda a, b: 7), "f64"),
+        "tight": (_int_table(2, 5, lambda a, b: int(rng.integers(1, 8))), "i32"),
+    }
+    table, mode = tabs[case]
+    pairs = _random_pairs(500 + len(case), 64, "ACGU", 0, 300, related=True)
+    pairs += _random_pairs(600 + len(case), 64, "ACGU", 1, 40)
+    plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
+    gpu.set_costs(plan)
+    b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(x) for x, _ in pairs],
+                                             [plan.encode(y) for _, y in pairs]), True)
+    assert b.mode == mode
+    b.close()
+    _oracle_check(table, pairs, gpu_run(gpu, table, pairs))
+    _oracle_check(table, pairs, gpu_run(gpu, table, pairs, script=False))
+    for pack in (0, 2):
+        _oracle_check(table, pairs, gpu_run(gpu, table, pairs, script=False, no_len=True, pack=pack), no_len=True)
+
+
+def test_ladder_rows_and_long_paths(gpu, tables):
+    """Ladder keys (sed_kernels.hip): every rung of the 16-row ladder at the sink (n = 1..48), stripes of
+    R = 4/8/16, and script lengths past 8192 (L read modulo 8192 inside [max(n,m), n+m])."""
+    rng = np.random.default_rng(4242)
+    pairs = [("".join(rng.choice(list("ACGU"), size=n)), "".join(rng.choice(list("ACGU"), size=int(m))))
+             for n in range(1, 49) for m in rng.integers(33, 90, size=2)]
+    for R in (4, 8, 16):
+        for user in (False, True):
+            _oracle_check(tables[user], pairs, gpu_run(gpu, tables[user], pairs, R=R))
+    a = "".join(rng.choice(list("ACGU"), size=9000))
+    b = "".join(rng.choice(list("ACGU"), size=300))  # L >= max(n, m) = 9000 > 8192
+    got = gpu_run(gpu, tables[True], [(a, b)])
+    assert got[0][2] > 8192
+    _oracle_check(tables[True], [(a, b)], got)
