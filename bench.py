@@ -152,6 +152,8 @@ def main():
     ap.add_argument("--no-pack", action="store_true",
                     help="distance-only pairs one per lane / wave (no packed 16-bit cells; A/B)")
     ap.add_argument("--split", type=int, default=0, help="SED_OPT_SPLIT: 0 auto, 1 force, 2 off (A/B)")
+    ap.add_argument("--tb", type=int, default=0,
+                    help="SED_OPT_TB: 0 auto, 1 per-cell traceback codes, 2 checkpoints + recompute (A/B)")
     ap.add_argument("--chain", type=int, default=0,
                     help="SED_OPT_CHAIN: 0 auto, 1 force, 2 off, L>=3 force with chains of L pairs (A/B)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -218,6 +220,8 @@ def main():
         ctx.set_option(sedgpu.SED_OPT_CHAIN, args.chain)
     if args.split:
         ctx.set_option(sedgpu.SED_OPT_SPLIT, args.split)
+    if args.tb:
+        ctx.set_option(sedgpu.SED_OPT_TB, args.tb)
     ctx.set_costs(plan)
     t0 = time.perf_counter()
     pipeline = want_script and not args.no_pipeline
@@ -334,6 +338,7 @@ def main():
                    "script": want_script, "pipeline": pipeline, "mode": batch.mode,
                    "rows_per_lane": batch.rows_per_lane, "lane_pairs": nl, "packed_pairs": npk,
                    "chains": batch.chains,
+                   "traceback": {0: None, 1: "per-cell codes", 2: "checkpoints + recompute"}[batch.traceback_mode],
                    "parallelism": "dp%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -63,6 +63,8 @@ enum {
 #define SED_OPT_CHAIN 5         /* integer kernel, single-stripe pairs run back to back in one wave (no
                                    per-pair ramp): 0 auto (large batches), 1 whenever eligible, 2 never,
                                    L >= 3 whenever eligible with chains of L pairs */
+#define SED_OPT_TB 7            /* script batches on the R = 16 integer wave kernel: 0 auto (checkpoints + recompute
+                                   for > 256 pairs), 1 per-cell traceback codes, 2 checkpoints whenever eligible */
 #define SED_OPT_PACK 6          /* distance-only integer batches (SED_NO_LEN): two pairs per lane (equal n) or per
                                    wave (equal n and m) in packed 16-bit cells: 0 auto (on), 2 never */
 
@@ -113,6 +115,7 @@ int sed_batch_rows_per_lane(const sed_batch *b);
 int sed_batch_lane_pairs(const sed_batch *b);         /* pairs on the lane-per-pair kernel (short str2) */
 int sed_batch_chains(const sed_batch *b);             /* CHAIN mode: number of chains (0 = not used) */
 int sed_batch_packed_pairs(const sed_batch *b);       /* pairs computed two per lane / wave (SED_OPT_PACK) */
+int sed_batch_traceback_mode(const sed_batch *b);     /* 0 no script, 1 per-cell codes, 2 checkpoints (SED_OPT_TB) */
 int sed_batch_run(sed_batch *b);                      /* enqueue on the context stream, returns at once */
 int sed_batch_sync(sed_batch *b);                     /* wait for the last run */
 /* device time of the last run, from HIP events on the launching stream (ms) */

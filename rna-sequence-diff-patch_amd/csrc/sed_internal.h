@@ -67,6 +67,7 @@ struct sed_launch {
     int R;
     hipStream_t stream;
     bool tb_ladder;     // traceback codes of the integer kernels carry the row's ladder rung (sed_kernels.hip)
+    bool ck;            // integer R = 16 wave kernel: tb holds checkpoints, the traceback recomputes tiles
     const int2 *tasks;  // SPLIT mode: (pair, stripe) per workgroup, else nullptr
     uint32_t *prog;     // SPLIT mode: per-stripe published-column counters (zeroed before each run)
     int ntasks;         // 0 -> one wave per pair
@@ -98,4 +99,6 @@ hipError_t sed_launch_lane_i32x2(const sed_launch &L, const int32_t *idx, int nl
 hipError_t sed_launch_lane_f64(const sed_launch &L, const int32_t *idx, int nidx, const double *gtab, double ins,
                                double del, int K);
 hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops);
+// CK batches (L.ck): the traceback that recomputes tiles from the forward kernel's checkpoints
+hipError_t sed_launch_traceback_ck(const sed_launch &L, uint32_t *ops, const sed_i32_params &prm);
 hipError_t sed_launch_selftest(uint32_t *d_out, hipStream_t stream);

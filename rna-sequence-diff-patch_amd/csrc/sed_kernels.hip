@@ -35,6 +35,7 @@
 // optional int/float typing bit.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "sed_internal.h"
 
 #define DPP_WAVE_SHL1 0x130  // lane i <- lane i+1, lane 63 keeps `old`
@@ -226,11 +227,12 @@ __device__ __forceinline__ uint32_t i32_sel(uint32_t b) { return 0x0D000100u | (
 
 // CAP: the group that produces the sink cell (captured on its lane); every extra variant is
 // another merge point where the register allocator may insert copies of the whole state.
-template <int R, bool TB, bool LEN, bool CAP>
+template <int R, bool TB, bool LEN, bool CAP, bool CK = false>
 __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                           uint32_t &bottom, uint32_t &selv, const uint2 *__restrict__ lch,
                                           uint32_t &outc, uint32_t (&W)[4], const int s0, const int lane,
-                                          const int cap_step, const int cap_lane, const int cap_row, uint32_t &cap) {
+                                          const int cap_step, const int cap_lane, const int cap_row, uint32_t &cap,
+                                          uint32_t (&rcv)[Grp<R>::G]) {
     constexpr int G = Grp<R>::G;
     uint2 tv[G];
     const uint2 *lp = lch + (s0 & 63);  // G divides 64: a group never wraps the chunk
@@ -240,6 +242,7 @@ __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)
     for (int u = 0; u < G; ++u) {
         const int s = s0 + u;
         i32_step<R, TB, LEN>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u);
+        if constexpr (CK) rcv[u] = V[R - 1];  // the band's bottom row, step s (row checkpoints)
         if constexpr (CAP) {
             const bool hit = (s == cap_step) && (lane == cap_lane);
 #pragma unroll
@@ -289,7 +292,12 @@ __device__ __forceinline__ bool wait_progress(const uint32_t *prog, uint32_t epo
 // SPLIT = true : one wave (one 64-thread workgroup) per stripe, all stripes of
 //                a pair run concurrently, each one 3 chunks (192 steps) behind the
 //                stripe above it (single long pairs: config 2, the GUI).
-template <int R, bool TB, bool SPLIT, bool LEN = true>
+// CK (R = 16, not SPLIT): instead of per-cell codes, tb receives checkpoints for the recompute
+// traceback (sed_traceback_ck_kernel): per stripe, at every chunk end each lane's 16 row values and its
+// top_prev ("column checkpoints", [chunk][17][64 lanes]), and every step the bottom row of the lanes
+// t = 3 (mod 4) ("row checkpoints", [group][16][4 steps]) -- 0.13 B per cell instead of 0.25, and no
+// v_alignbit per cell.
+template <int R, bool TB, bool SPLIT, bool LEN = true, bool CK = false>
 __global__ __launch_bounds__(SPLIT ? 64 : 256) __attribute__((amdgpu_waves_per_eu(SED_I32_WAVES(R)))) void
 sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *__restrict__ tasks,
                   uint32_t *__restrict__ prog, const uint32_t *__restrict__ seqa, const uint32_t *__restrict__ seqb,
@@ -297,6 +305,7 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
                   sed_i32_params prm) {
     constexpr int ROWS = 64 * R;
     constexpr int G = Grp<R>::G;
+    static_assert(!CK || (R == 16 && !SPLIT && !TB && LEN), "checkpoints: R = 16 script batches, one wave per pair");
     const int lane = threadIdx.x & 63;
     int pair, kfirst = 0;
     if constexpr (SPLIT) {
@@ -368,6 +377,12 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
         uint32_t tch = load_top(0), sch = load_sel(0);
         lch[lane] = make_uint2(tch, sch);
         uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * 256u;
+        // CK: column checkpoints of stripe k at ccb[(chunk * 17 + v) * 64 + lane], row checkpoints at
+        // rcb[(group * 16 + lane / 4) * 4 + step % 4] (the layout sed_traceback_ck_kernel reads)
+        uint32_t *ccb = tb + d.tb_off + (uint64_t)k * (uint64_t)nchunks * 1088u;
+        uint32_t *rcb = tb + d.tb_off + (uint64_t)nstripes * (uint64_t)nchunks * 1088u +
+                        (uint64_t)k * (uint64_t)(SG / G) * 64u;
+        uint32_t rcv[G];
         const bool last = (k == nstripes - 1);
         const int cap_step = last ? m - 1 + cap_lane : -1;
         int s = 0;
@@ -377,15 +392,25 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             for (int g = 0; g < 64 / G && s < SG; ++g, s += G) {
                 const bool capg = cap_step >= s && cap_step < s + G;
                 if (capg)
-                    i32_group<R, TB, LEN, true>(V, cv, top_prev, bottom, selv, lch, outc, W, s, lane, cap_step,
-                                                cap_lane, cap_row, cap);
+                    i32_group<R, TB, LEN, true, CK>(V, cv, top_prev, bottom, selv, lch, outc, W, s, lane, cap_step,
+                                                    cap_lane, cap_row, cap, rcv);
                 else
-                    i32_group<R, TB, LEN, false>(V, cv, top_prev, bottom, selv, lch, outc, W, s, lane, cap_step,
-                                                 cap_lane, cap_row, cap);
+                    i32_group<R, TB, LEN, false, CK>(V, cv, top_prev, bottom, selv, lch, outc, W, s, lane,
+                                                     cap_step, cap_lane, cap_row, cap, rcv);
                 if constexpr (TB) {
                     uint32_t *gp = tbk + (uint64_t)(s / G) * 256u;  // wave-uniform base, per-lane 16-byte offset
                     store_tb(gp + lane * 4, W);
                 }
+                if constexpr (CK) {
+                    if ((lane & 3) == 3)
+                        store_tb(rcb + (uint64_t)(s / G) * 64u + (uint32_t)(lane >> 2) * 4u, rcv);
+                }
+            }
+            if constexpr (CK) {  // column checkpoint: state after the chunk's last step
+                uint32_t *cp = ccb + (uint64_t)c * 1088u + lane;
+#pragma unroll
+                for (int r = 0; r < R; ++r) cp[r * 64] = V[r];
+                cp[16 * 64] = top_prev;
             }
             // lane i holds lane 63's bottom cell of step s-64+i, i.e. column s-126+i at bnd index col+64
             if (!last) {
@@ -1219,6 +1244,145 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
 }
 
 // ---------------------------------------------------------------------------
+// Traceback from checkpoints (CK, the R = 16 wave kernel's script batches).  One wave per pair walks
+// the canonical path back from (n, m) tile by tile.  A tile is 64 rows (forward lanes 4Q .. 4Q+3 of a
+// stripe) x the 64 columns those lanes processed in one chunk c, a staircase: band t = 4Q + b covers
+// columns 64c - t + 1 .. 64c - t + 64.  Entering a tile, the wave recomputes it from
+//   - the column checkpoints of chunk c-1 (each band's 16 row values at column 64c - t, and the value
+//     above the band at that column), or the column-0 borders for c = 0;
+//   - the row above the tile: the row checkpoints of lane 4Q-1 (or lane 63 of the stripe above, or
+//     row 0), read through LDS by lane 0;
+// with one lane per row (row r at sweep step sigma is at column J0 - 3 + sigma - r, J0 = 64c - 4Q + 1,
+// so that every lane's str2 selectors arrive through the DPP chain from lane 0), the same offset keys
+// and ladder rungs as the forward kernel, so every cell's key -- and its 2-bit choice -- is the forward
+// kernel's.  Lanes of band b hold their checkpoint until their first column (step r - b + 3); the first
+// row of bands 1..3 takes its first diagonal from the checkpoint; columns < 1 get the forward kernel's
+// sentinel selector, so they keep the column-0 borders exactly as its virtual columns do.  The sweep
+// stops at the entry cell's step: the path only goes up and left.  Codes stay in registers, 16 steps
+// per word, and the wave-uniform walk reads them with v_readlane until it leaves the tile.
+// The recompute costs ~1/5 of the per-cell v_alignbit it replaces.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
+                                                              const uint32_t *__restrict__ seqa,
+                                                              const uint32_t *__restrict__ seqb,
+                                                              const uint32_t *__restrict__ ck,
+                                                              const sed_result *__restrict__ res,
+                                                              uint32_t *__restrict__ ops, sed_i32_params prm) {
+    constexpr int R = 16, ROWS = 64 * R, G = Grp<R>::G;
+    using Lad = Ladder<R>;
+    const int lane = threadIdx.x;
+    const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x);
+    if (pair >= npairs) return;
+    const sed_pair_desc d = pd[pair];
+    if (d.lane) return;  // scripted by sed_lane.hip
+    const int n = d.n, m = d.m;
+    uint32_t *out = ops + d.ops_off;
+    uint32_t q = (uint32_t)__builtin_amdgcn_readfirstlane(res[pair].len);
+    uint32_t acc = 0;
+    auto emit = [&](uint32_t op) {  // sink -> origin, as sed_traceback_window_kernel
+        if (q == 0) return;         // never write below the pair's script (a bad path stops here)
+        acc = (acc << 2) | op;
+        if ((--q & 15u) == 0) out[q >> 4] = acc;
+    };
+    __shared__ uint32_t topb[132], selb[132];
+    int i = n, j = m;
+    if (i > 0 && j > 0) {
+        const int nstripes = (n + ROWS - 1) / ROWS;
+        const int SG = (m + 63 + G - 1) / G * G, nchunks = (SG + 63) >> 6, ngroups = SG / G;
+        const uint32_t *ccp = ck + d.tb_off;
+        const uint32_t *rcp = ccp + (uint64_t)nstripes * (uint64_t)nchunks * 1088u;
+        const uint32_t *pa = seqa + d.a_off, *pb = seqb + d.b_off;
+        // per-lane constants: tiles start at rows = 0 (mod 64), so lane r is always on rung(r + 1)
+        const int band = lane >> 4;
+        const uint32_t crung = (uint32_t)Lad::rung(lane + 1);
+        const int dd = Lad::rung(lane + 1) - Lad::rung(lane);
+        const uint32_t s1 = (uint32_t)(dd - 6), dadd = (uint32_t)(dd + 1);
+        const int sig0 = lane - band + 3;  // first real sweep step of this lane (<= 63)
+        int guard = 2 * (n + m) + 8;   // tiles visited; every visit makes progress
+        while (i > 0 && j > 0 && --guard > 0) {
+            const int k = (i - 1) / ROWS, t = ((i - 1) % ROWS) / R, Q = t >> 2;
+            const int c = (j - 1 + t) >> 6;
+            const int J0 = 64 * c - 4 * Q + 1, rowbase = k * ROWS + 64 * Q;
+            const int sig_end = (j - J0 + 3) + (i - rowbase - 1);  // the entry cell's sweep step (<= 126)
+            // ---- boundaries ----
+            const int ir = min(rowbase + lane, n - 1);  // 0-based str1 index of this lane's row (clamped)
+            const uint32_t a = (pa[ir >> 4] >> ((ir & 15) * 2)) & 3u;
+            const uint32_t cv = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
+            uint32_t V = SED_KB3 + crung, tp = SED_KB3;  // c = 0: the column-0 borders
+            if (c >= 1) {
+                const uint32_t *cp = ccp + ((uint64_t)k * (uint64_t)nchunks + (uint64_t)(c - 1)) * 1088u +
+                                     (uint32_t)(4 * Q + band);
+                V = cp[(lane & 15) * 64];
+                tp = cp[16 * 64];
+            }
+            for (int x = lane; x < 132; x += 64) {
+                // the row above the tile at column J0 - 4 + x: row checkpoints (steps clamped: past SG
+                // the columns are beyond m and never read by the walk; before step 0 the border B)
+                uint32_t v = SED_KB3;
+                if (Q >= 1) {
+                    const int st = 64 * c - 5 + x;
+                    if (st >= 0) {
+                        const int sc = min(st, SG - 1);
+                        v = rcp[((uint64_t)k * (uint64_t)ngroups + (uint64_t)(sc >> 2)) * 64u + (uint32_t)(Q - 1) * 4u +
+                                (uint32_t)(sc & 3)];
+                    }
+                } else if (k >= 1) {
+                    const int sc = min(64 * c + 59 + x, SG - 1);
+                    v = rcp[((uint64_t)(k - 1) * (uint64_t)ngroups + (uint64_t)(sc >> 2)) * 64u + 60u + (uint32_t)(sc & 3)];
+                }
+                topb[x] = v;
+                const int col = J0 - 3 + x;  // column of lane 0 at step x
+                const int ci = min(max(col - 1, 0), m - 1);
+                selb[x] = col < 1 ? SED_SEL_SENT3 : i32_sel((pb[ci >> 4] >> ((ci & 15) * 2)) & 3u);
+            }
+            __syncthreads();
+            // ---- sweep: lane r at step sigma computes (row rowbase + r + 1, column J0 + sigma - r) ----
+            uint32_t W[8];
+            uint32_t tprev = dpp_shr1(topb[0], V);  // diagonal of step 0: the lane above, or row above
+            uint32_t selv = SED_SEL_SENT3;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                if (w > 0 && 16 * w > sig_end) break;  // the path never needs later steps
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int sig = 16 * w + u;
+                    const uint32_t topv = dpp_shr1(topb[sig + 1], V);
+                    selv = dpp_shr1(selb[sig], selv);
+                    uint32_t diag = tprev;
+                    if (sig == 18 || sig == 33 || sig == 48) diag = lane == 16 * ((sig - 3) / 15) ? tp : diag;
+                    const uint32_t mm = umin3(V, topv + dadd, diag + __builtin_amdgcn_perm(cv, s1, selv));
+                    W[w] = __builtin_amdgcn_alignbit(mm, W[w], 2);
+                    const uint32_t vn = (mm & ~7u) | crung;
+                    V = (sig < 64 && sig < sig0) ? V : vn;  // left of the band's checkpoint: hold it
+                    tprev = topv;
+                }
+            }
+            // ---- walk inside the tile ----
+            int steps = 0;
+            while (true) {
+                const int r = i - rowbase - 1;
+                if (r < 0 || j < J0 - (r >> 4)) break;  // above the tile or left of the band's window
+                const int sg = (j - J0 + 3) + r;
+                uint32_t wv = W[0];
+#pragma unroll
+                for (int w = 1; w < 8; ++w) wv = (sg >> 4) == w ? W[w] : wv;
+                const uint32_t code = ((uint32_t)__builtin_amdgcn_readlane((int)wv, r) >> (2 * (sg & 15))) & 3u;
+                const uint32_t op = (code - (uint32_t)Lad::rung(i)) & 3u;
+                emit(op);
+                ++steps;
+                i -= (int)(op != 0);
+                j -= (int)(op != 1);
+                if (i == 0 || j == 0) break;
+            }
+            if (steps == 0) break;  // no progress: give up rather than spin (tests catch a bad script)
+            __syncthreads();        // topb / selb are rewritten for the next tile
+        }
+    }
+    while (j > 0) { emit(0u); --j; }
+    while (i > 0) { emit(1u); --i; }
+}
+
+// ---------------------------------------------------------------------------
 // Self-test of the cross-lane primitives the kernels rely on.
 // ---------------------------------------------------------------------------
 __global__ void sed_selftest_kernel(uint32_t *out) {
@@ -1241,7 +1405,7 @@ __global__ void sed_selftest_kernel(uint32_t *out) {
 // ---------------------------------------------------------------------------
 // Launchers (host side, called from sed_runtime.cpp)
 // ---------------------------------------------------------------------------
-template <int R, bool TB, bool LEN = true>
+template <int R, bool TB, bool LEN = true, bool CK = false>
 static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
     if (L.ntasks > 0) {  // SPLIT: one 64-thread workgroup per (pair, stripe)
         hipLaunchKernelGGL((sed_wf_i32_kernel<R, TB, true, LEN>), dim3(L.ntasks), dim3(64), 0, L.stream, L.pd, L.npairs,
@@ -1249,7 +1413,9 @@ static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
                            prm);
     } else {
         const int grid = (L.npairs + 3) / 4;
-        hipLaunchKernelGGL((sed_wf_i32_kernel<R, TB, false, LEN>), dim3(grid), dim3(256), 0, L.stream, L.pd, L.npairs,
+        // SED_OCC_LDS (tuning/A-B only): dynamic LDS bytes per workgroup, which caps the resident waves
+        static const int occ_lds = [] { const char *e = getenv("SED_OCC_LDS"); return e ? atoi(e) : 0; }();
+        hipLaunchKernelGGL((sed_wf_i32_kernel<R, TB, false, LEN, CK>), dim3(grid), dim3(256), occ_lds, L.stream, L.pd, L.npairs,
                            L.tasks, L.prog, (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res,
                            prm);
     }
@@ -1293,6 +1459,10 @@ hipError_t sed_launch_i32x2(const sed_launch &L, const int32_t *list, int nwaves
 
 hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm, bool len) {
     const bool tb = L.tb != nullptr;
+    if (tb && L.ck) {
+        if (L.R != 16 || L.ntasks > 0) return hipErrorInvalidValue;
+        return launch_i32_R<16, false, true, true>(L, prm);
+    }
     switch (L.R) {
 #define CASE(RR)                                                                                     \
     case RR:                                                                                         \
@@ -1332,6 +1502,12 @@ hipError_t sed_launch_f64(const sed_launch &L, const double *gtab, const sed_f64
 #undef CASE
     default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t sed_launch_traceback_ck(const sed_launch &L, uint32_t *ops, const sed_i32_params &prm) {
+    hipLaunchKernelGGL(sed_traceback_ck_kernel, dim3(L.npairs), dim3(64), 0, L.stream, L.pd, L.npairs,
+                       (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.res, ops, prm);
+    return hipGetLastError();
 }
 
 hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops) {

@@ -58,7 +58,7 @@ struct sed_ctx {
     int ins_int = 0, del_int = 0;
     DevBuf gtab;  // fp64 kernel table: per entry {value bits, is-int flag}
     // options
-    int opt_mode = 0, opt_R = 0, opt_split = 0, opt_lane = 0, opt_chain = 0, opt_pack = 0;
+    int opt_mode = 0, opt_R = 0, opt_split = 0, opt_lane = 0, opt_chain = 0, opt_pack = 0, opt_tb = 0;
     DevBuf selftest;
     sed_batch *scratch = nullptr;
 
@@ -87,6 +87,7 @@ struct sed_batch {
     double cells = 0, algo_bytes = 0;
     DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops, d_tasks, d_prog, d_lane, d_chain, d_x2;
     bool split = false;
+    bool ck = false;           // traceback from checkpoints + recompute (sed_kernels.hip: CK) instead of codes
     int nlane = 0, nwave = 0;  // pairs on the lane-per-pair kernel / on the wave kernels
     int nlane_x2 = 0;          // > 0: lane pairs run two per lane (distance only), in this many lanes
     int nwave_x2 = 0;          // distance-only wave pairs of equal shape run two per wave, in this many waves
@@ -268,6 +269,10 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     b->R = R;
     const int ROWS = 64 * R;
     const bool want_tb = (flags & SED_WANT_SCRIPT) != 0;
+    // CK traceback (R = 16 wave kernel, not SPLIT; CHAIN mode needs R <= 8): checkpoints + recompute,
+    // by default for batches past the window kernel's 256 pairs
+    b->ck = want_tb && mode == SED_MODE_I32 && !split && R == 16 && c->opt_tb != 1 &&
+            (c->opt_tb == 2 || npairs > 256);
 
     // ---- layout ----
     b->pd.assign(npairs, sed_pair_desc{});
@@ -278,7 +283,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
                           (mode == SED_MODE_I32 || (mode == SED_MODE_F64 && !want_tb && (flags & SED_NO_LEN)));
     uint64_t aw = 0, bw = 0, tbw = 0, bndw = 0, opw = 0, progw = 0;
     const bool packed = (mode == SED_MODE_I32);
-    double cells = 0, in_bytes = 0, tb_bytes = 0;
+    double cells = 0, in_bytes = 0, tb_bytes = 0, ck_bytes = 0;
     for (int p = 0; p < npairs; ++p) {
         const int nn = len_a[p], mm = len_b[p];
         sed_pair_desc &d = b->pd[p];
@@ -306,7 +311,11 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
             const uint64_t nstripes = (nn + ROWS - 1) / ROWS;
             const uint64_t SG = (mm + 63 + G - 1) / G * G;
             const uint64_t nchunks = (SG + 63) / 64;
-            if (want_tb) tbw += nstripes * (SG / G) * 64 * 4;
+            if (want_tb) {  // CK: per stripe nchunks x 17 x 64 column checkpoints + (SG/G) x 64 row checkpoints
+                const uint64_t w = b->ck ? nstripes * (nchunks * 17 * 64 + (SG / G) * 64) : nstripes * (SG / G) * 64 * 4;
+                tbw += w;
+                ck_bytes += 4.0 * (double)w;
+            }
             if (nstripes > 1) bndw += (nchunks + 2) * 64 * (packed ? 1 : 4) * (split ? nstripes : 1);
             if (split) {
                 for (uint64_t k = 0; k < nstripes; ++k) tasks.push_back(make_int2(p, (int)k));
@@ -319,7 +328,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         cells += (double)nn * mm;
         in_bytes += packed ? (nn + mm) / 4.0 : (double)(nn + mm);
     }
-    tb_bytes = cells * 0.25;
+    // algorithmic traceback bytes: the 2-bit choice of every cell, or (CK) the checkpoints written
+    tb_bytes = b->ck ? ck_bytes : cells * 0.25;
     b->tb_words = tbw;
     b->bnd_words = bndw;
     b->nlane = (int)lane_idx.size();
@@ -549,6 +559,7 @@ int run_batch(sed_batch *b) {
     L.R = b->R;
     L.stream = c->stream;
     L.tb_ladder = b->mode == SED_MODE_I32;
+    L.ck = b->ck;
     L.tasks = b->split ? (const int2 *)b->d_tasks.p : nullptr;
     L.prog = (uint32_t *)b->d_prog.p;
     L.ntasks = b->split ? b->ntasks : 0;
@@ -604,7 +615,8 @@ int run_batch(sed_batch *b) {
         if ((e = hipEventRecord(lg[2], ts)) != hipSuccess) return c->hipfail(e, "event record");
         if (b->nwave > 0) {
             L.stream = ts;
-            if ((e = sed_launch_traceback(L, (uint32_t *)b->d_ops.p)) != hipSuccess)
+            if ((e = b->ck ? sed_launch_traceback_ck(L, (uint32_t *)b->d_ops.p, ip)
+                           : sed_launch_traceback(L, (uint32_t *)b->d_ops.p)) != hipSuccess)
                 return c->hipfail(e, "traceback kernel launch");
         }
         if ((e = hipEventRecord(lg[3], ts)) != hipSuccess) return c->hipfail(e, "event record");
@@ -701,6 +713,10 @@ int sed_set_option(sed_ctx *c, int key, int value) {
         c->opt_lane = value;
         return SED_OK;
     }
+    if (key == SED_OPT_TB && value >= 0 && value <= 2) {
+        c->opt_tb = value;
+        return SED_OK;
+    }
     if (key == SED_OPT_PACK && (value == 0 || value == 2)) {
         c->opt_pack = value;
         return SED_OK;
@@ -770,6 +786,11 @@ int sed_batch_mode(const sed_batch *b) { return b ? b->mode : SED_E_ARG; }
 int sed_batch_rows_per_lane(const sed_batch *b) { return b ? b->R : SED_E_ARG; }
 int sed_batch_lane_pairs(const sed_batch *b) { return b ? b->nlane : SED_E_ARG; }
 int sed_batch_chains(const sed_batch *b) { return b ? b->nchains : SED_E_ARG; }
+int sed_batch_traceback_mode(const sed_batch *b) {
+    if (!b || !(b->flags & SED_WANT_SCRIPT)) return 0;
+    return b->ck ? 2 : 1;
+}
+
 int sed_batch_packed_pairs(const sed_batch *b) {
     return b ? (b->nlane_x2 > 0 ? b->nlane : 0) + 2 * b->nwave_x2 : SED_E_ARG;
 }

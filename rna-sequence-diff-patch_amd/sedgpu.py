@@ -20,6 +20,7 @@ SED_OPT_SPLIT = 3
 SED_OPT_LANE = 4
 SED_OPT_CHAIN = 5
 SED_OPT_PACK = 6
+SED_OPT_TB = 7
 MODE_NAMES = {1: "i32", 2: "f64", 3: "f64-typed"}
 
 _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
@@ -46,6 +47,7 @@ SIGNATURES = [
     ("sed_batch_lane_pairs", C.c_int, [C.c_void_p]),
     ("sed_batch_chains", C.c_int, [C.c_void_p]),
     ("sed_batch_packed_pairs", C.c_int, [C.c_void_p]),
+    ("sed_batch_traceback_mode", C.c_int, [C.c_void_p]),
     ("sed_batch_run", C.c_int, [C.c_void_p]),
     ("sed_batch_sync", C.c_int, [C.c_void_p]),
     ("sed_batch_last_times", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
@@ -249,6 +251,11 @@ class Batch:
     @property
     def chains(self):
         return self._lib.sed_batch_chains(self.ptr)
+
+    @property
+    def traceback_mode(self):
+        """0 distance only, 1 per-cell traceback codes, 2 checkpoints + recompute (SED_OPT_TB)."""
+        return self._lib.sed_batch_traceback_mode(self.ptr)
 
     @property
     def packed_pairs(self):

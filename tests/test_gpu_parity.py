@@ -20,7 +20,7 @@ OPCH = "idu"
 IUPAC = "AGCUYRWSKMDVHBN"
 
 
-def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len=False, chain=0, pack=0):
+def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len=False, chain=0, pack=0, tb=0):
     """Run (s1, s2) pairs through the engine; returns [(dist, is_int, len, opstr)]."""
     plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
     ctx.set_mode(mode)
@@ -29,6 +29,7 @@ def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len
     ctx.set_option(sedgpu.SED_OPT_LANE, lane)
     ctx.set_option(sedgpu.SED_OPT_CHAIN, chain)
     ctx.set_option(sedgpu.SED_OPT_PACK, pack)
+    ctx.set_option(sedgpu.SED_OPT_TB, tb)
     ctx.set_costs(plan)
     packed = sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs], [plan.encode(b) for _, b in pairs])
     dist, is_int, ln, ops = ctx.run(packed, script, no_len=no_len)
@@ -44,6 +45,7 @@ def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len
     ctx.set_option(sedgpu.SED_OPT_LANE, 0)
     ctx.set_option(sedgpu.SED_OPT_CHAIN, 0)
     ctx.set_option(sedgpu.SED_OPT_PACK, 0)
+    ctx.set_option(sedgpu.SED_OPT_TB, 0)
     return out
 
 
@@ -385,3 +387,42 @@ def test_ladder_rows_and_long_paths(gpu, tables):
     got = gpu_run(gpu, tables[True], [(a, b)])
     assert got[0][2] > 8192
     _oracle_check(tables[True], [(a, b)], got)
+
+
+@pytest.mark.parametrize("user", [False, True])
+def test_checkpoint_traceback_vs_oracle(gpu, tables, user):
+    """CK traceback (SED_OPT_TB = 2): the R = 16 kernel stores column / row checkpoints instead of per-cell
+    codes and the traceback recomputes 64-row tiles.  Ragged multi-stripe batches (lengths 1..2600, related
+    and unrelated, border lengths around tiles, chunks and stripes) give the oracle's scripts, and the same
+    as the per-cell codes (SED_OPT_TB = 1)."""
+    pairs = _random_pairs(900 + user, 24, "ACGU", 1, 2600, related=True)
+    pairs += _random_pairs(910 + user, 16, "ACGU", 1, 1500)
+    rng = np.random.default_rng(920 + user)
+    for n, m in ((64, 64), (65, 63), (1024, 64), (1025, 129), (2048, 1), (1, 2048), (1088, 1090), (63, 4000)):
+        a = "".join(rng.choice(list("ACGU"), size=n))
+        pairs.append((a, "".join(c if rng.random() > 0.2 else rng.choice(list("ACGU")) for c in a)[:m].ljust(m, "G")))
+    plan = sedcost.build_plan(tables[user], [a for a, _ in pairs], [b for _, b in pairs])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs([plan.encode(x) for x, _ in pairs], [plan.encode(y) for _, y in pairs])
+    for tb, want in ((2, 2), (1, 1), (0, 1)):  # auto: codes below 257 pairs
+        gpu.set_option(sedgpu.SED_OPT_TB, tb)
+        gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 16)
+        gpu.set_option(sedgpu.SED_OPT_SPLIT, 2)
+        b = sedgpu.Batch(gpu, packed, True)
+        assert b.traceback_mode == want
+        b.close()
+    gpu.set_option(sedgpu.SED_OPT_TB, 0)
+    gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
+    gpu.set_option(sedgpu.SED_OPT_SPLIT, 0)
+    got = gpu_run(gpu, tables[user], pairs, R=16, split=2, lane=2, tb=2)
+    _oracle_check(tables[user], pairs, got)
+    assert got == gpu_run(gpu, tables[user], pairs, R=16, split=2, lane=2, tb=1)
+
+
+def test_checkpoint_traceback_config2_pair(gpu, tables):
+    """The G3 pair (4096 x 4096, user_costs) through the CK traceback."""
+    g3 = load_golden("g3_config2.json")
+    s1, s2 = synth.pair_strings(g3["pair_id"], g3["n"], g3["m"], g3["base_seed"])
+    (d, ii, ln, s), = gpu_run(gpu, tables[True], [(s1, s2)], R=16, split=2, tb=2)
+    assert (d, ii) == (float.fromhex(g3["dist"][0]), g3["dist"][1])
+    assert ln == len(g3["canon"]) and s == g3["canon"]
