@@ -40,7 +40,7 @@ SIMDS, CLOCK = 1024, 2.4e9
 # the nominal 2-cycle ops do not pair when interleaved with the 4-cycle v_perm/v_min3/v_alignbit).
 # Ops per cell in offset-key space (sed_kernels.hip): perm + add + min3 (+ and_or clearing the op for the
 # op-count field, + the ladder's delete add on 3 of 16 rows) (+ alignbit for the traceback); packed distance
-# keys: perm + pk_add + 2 pk_min per 2 cells.
+# keys: perm + pk_add + 2 pk_min per 2 cells.  Checkpoint script batches (traceback mode 2) use "len".
 VALU_CYCLES_PER_OP = 4.0
 CELL_OPS = {"script": 5 + 3 / 16, "len": 4 + 3 / 16, "nolen": 3, "nolen_x2": 2}
 
@@ -320,7 +320,10 @@ def main():
     wave_x2 = npk - (nl if lane_x2 else 0)  # wave pairs computed two per wave
     ops_cell = None
     if batch.mode == "i32":
-        ops_cell = CELL_OPS["script" if want_script else ("nolen_x2" if npk == P else "nolen")]
+        # checkpoint batches (SED_OPT_TB 2) drop the per-cell alignbit: the forward cell is the "len" cell,
+        # and the traceback's recompute runs concurrently on the same SIMDs (it is not in this model)
+        ops_cell = CELL_OPS[("len" if batch.traceback_mode == 2 else "script") if want_script
+                            else ("nolen_x2" if npk == P else "nolen")]
     valu_peak = SIMDS * CLOCK * 64 / (VALU_CYCLES_PER_OP * ops_cell) if ops_cell else None
     rate = cells / (dp_avg * 1e-3)
     if batch.mode != "i32":
