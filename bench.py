@@ -338,7 +338,7 @@ def main():
         "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u32" if batch.mode == "i32" else "f64", "data": "synthetic",
         "config": {"workload": desc, "pairs_per_gpu": P, "n": n, "m": m, "costs": costs_file,
-                   "script": want_script, "pipeline": pipeline, "mode": batch.mode,
+                   "script": want_script, "pipeline": pipeline and batch.traceback_mode != 2, "mode": batch.mode,
                    "rows_per_lane": batch.rows_per_lane, "lane_pairs": nl, "packed_pairs": npk,
                    "chains": batch.chains,
                    "traceback": {0: None, 1: "per-cell codes", 2: "checkpoints + recompute"}[batch.traceback_mode],

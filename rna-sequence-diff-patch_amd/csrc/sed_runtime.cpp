@@ -273,6 +273,10 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // by default for batches past the window kernel's 256 pairs
     b->ck = want_tb && mode == SED_MODE_I32 && !split && R == 16 && c->opt_tb != 1 &&
             (c->opt_tb == 2 || npairs > 256);
+    // SED_PIPELINE is a hint: checkpoint batches run their traceback after the DP on one stream.  Both
+    // kernels are issue-bound, so overlap only adds contention (config 4: 20.33 ms sequential against
+    // 20.5-20.8 ms pipelined, profiles/r01_ck/ab_pipeline.jsonl) and saves two traceback buffers.
+    if (b->ck) b->nbuf = 1;
 
     // ---- layout ----
     b->pd.assign(npairs, sed_pair_desc{});
