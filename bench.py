@@ -40,7 +40,8 @@ SIMDS, CLOCK = 1024, 2.4e9
 # the nominal 2-cycle ops do not pair when interleaved with the 4-cycle v_perm/v_min3/v_alignbit).
 # Ops per cell in offset-key space (sed_kernels.hip): perm + add + min3 (+ and_or clearing the op for the
 # op-count field, + the ladder's delete add on 3 of 16 rows) (+ alignbit for the traceback); packed distance
-# keys: perm + pk_add + 2 pk_min per 2 cells.  Checkpoint script batches (traceback mode 2) use "len".
+# keys: perm + pk_add + 2 pk_min per 2 cells.  Checkpoint script batches (traceback mode 2) run the distance
+# keys (D << 16 - U carries the path length; the traceback recomputes the op tie-break): "nolen".
 VALU_CYCLES_PER_OP = 4.0
 CELL_OPS = {"script": 5 + 3 / 16, "len": 4 + 3 / 16, "nolen": 3, "nolen_x2": 2}
 
@@ -140,7 +141,7 @@ def cpu_baseline(plan, packed, seconds, threads, want_ops):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)  # the last traceback is not overlapped: amortise it
+    ap.add_argument("--steps", type=int, default=20)  # per-cell-code batches: the last traceback is not overlapped
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     ap.add_argument("--pairs", type=int, default=0, help="override pairs per GPU")
@@ -237,7 +238,7 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        batch.run()  # DP(k) on the DP stream; traceback(k) on a second stream overlaps DP(k+1)
+        batch.run()  # DP then traceback; per-cell-code batches overlap traceback(k) with DP(k+1) (SED_PIPELINE)
     batch.sync()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -320,9 +321,9 @@ def main():
     wave_x2 = npk - (nl if lane_x2 else 0)  # wave pairs computed two per wave
     ops_cell = None
     if batch.mode == "i32":
-        # checkpoint batches (SED_OPT_TB 2) drop the per-cell alignbit: the forward cell is the "len" cell,
-        # and the traceback's recompute runs concurrently on the same SIMDs (it is not in this model)
-        ops_cell = CELL_OPS[("len" if batch.traceback_mode == 2 else "script") if want_script
+        # checkpoint batches (SED_OPT_TB 2): the forward kernel runs distance keys (3 ops/cell); the
+        # traceback's recompute runs after it on the same SIMDs and is not in this model (kernel_ms is the DP)
+        ops_cell = CELL_OPS[("nolen" if batch.traceback_mode == 2 else "script") if want_script
                             else ("nolen_x2" if npk == P else "nolen")]
     valu_peak = SIMDS * CLOCK * 64 / (VALU_CYCLES_PER_OP * ops_cell) if ops_cell else None
     rate = cells / (dp_avg * 1e-3)

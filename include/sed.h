@@ -47,8 +47,10 @@ enum {
 
 /* flags for sed_run_batch / sed_batch_create */
 #define SED_WANT_SCRIPT 1u
-/* sed_batch only: three traceback/result buffers and a second stream, so the traceback of
- * run k overlaps the DP kernel of run k+1 (device memory for the traceback triples). */
+/* sed_batch only, a hint: batches with per-cell traceback codes get three traceback/result buffers
+ * and a second stream, so the traceback of run k overlaps the DP kernel of run k+1 (device memory
+ * for the traceback triples).  Checkpoint batches (sed_batch_traceback_mode 2, the default for
+ * script batches of > 256 pairs) ignore it and run DP then traceback on one stream. */
 #define SED_PIPELINE 2u
 /* distance only (no SED_WANT_SCRIPT): out_len is not computed (-1), which lets the integer
  * kernels drop the op-count field of their keys (3 instead of ~4.2 VALU ops per cell). */
@@ -67,6 +69,10 @@ enum {
                                    for > 256 pairs), 1 per-cell traceback codes, 2 checkpoints whenever eligible */
 #define SED_OPT_PACK 6          /* distance-only integer batches (SED_NO_LEN): two pairs per lane (equal n) or per
                                    wave (equal n and m) in packed 16-bit cells: 0 auto (on), 2 never */
+#define SED_OPT_CHAIN_WAVES 8   /* dynamic CHAIN mode: persistent waves, 0 auto (every SIMD's resident waves), else a
+                                   cap (tests: several counter-fetched pairs per wave) */
+#define SED_OPT_DEBUG_CORRUPT 9 /* testing only: p + 1 overwrites one checkpoint word of pair p before its traceback,
+                                   which must then fail with SED_E_DEVICE naming the pair; 0 off */
 
 /* modes reported by sed_batch_mode */
 #define SED_MODE_I32 1
@@ -116,6 +122,9 @@ int sed_batch_lane_pairs(const sed_batch *b);         /* pairs on the lane-per-p
 int sed_batch_chains(const sed_batch *b);             /* CHAIN mode: number of chains (0 = not used) */
 int sed_batch_packed_pairs(const sed_batch *b);       /* pairs computed two per lane / wave (SED_OPT_PACK) */
 int sed_batch_traceback_mode(const sed_batch *b);     /* 0 no script, 1 per-cell codes, 2 checkpoints (SED_OPT_TB) */
+/* CHAIN diagnostics of the last run (waits for it): pairs handed out by the dynamic-CHAIN device counter, and
+ * the most pairs one wave computed back to back (0 when CHAIN mode is off). */
+int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave);
 int sed_batch_run(sed_batch *b);                      /* enqueue on the context stream, returns at once */
 int sed_batch_sync(sed_batch *b);                     /* wait for the last run */
 /* device time of the last run, from HIP events on the launching stream (ms) */

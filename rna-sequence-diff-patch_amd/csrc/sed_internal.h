@@ -23,9 +23,16 @@ struct sed_result {
     double dist;     // dp[n][m].value
     int32_t len;     // ops in the canonical script (L at the sink)
     uint8_t is_int;  // 1 when the reference's value is a Python int
-    uint8_t err;     // 1 when a SPLIT-mode wait timed out (results invalid)
-    uint8_t pad[2];
+    uint8_t err;     // SED_ERR_* (0 = ok); nonzero: the pair's results are invalid
+    uint16_t seq;    // CHAIN mode: ordinal of the pair within the wave that computed it (diagnostics)
 };
+
+// sed_result.err codes (sed_runtime.cpp: fetch_results maps them to SED_E_DEVICE with the pair index)
+#define SED_ERR_SPLIT_TIMEOUT 1  // SPLIT: an inter-workgroup hand-off wait timed out
+#define SED_ERR_TB_CHECK 2       // CK traceback: a recomputed tile disagrees with the path length (bad checkpoint)
+#define SED_ERR_TB_STALL 3       // traceback: a tile visit made no progress
+#define SED_ERR_TB_GUARD 4       // traceback: more tile visits than any path can need
+#define SED_ERR_TB_LENGTH 5      // traceback: the walk's op count differs from the sink's L
 
 // Integer kernel constants (offset-key space, see sed_kernels.hip):
 //   costrow[a]   byte b = (cost(a -> b) - insert - delete - 1) & 0xFF  (32-bit keys)
@@ -99,6 +106,11 @@ hipError_t sed_launch_lane_i32x2(const sed_launch &L, const int32_t *idx, int nl
 hipError_t sed_launch_lane_f64(const sed_launch &L, const int32_t *idx, int nidx, const double *gtab, double ins,
                                double del, int K);
 hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops);
+// checkpoint layout of the CK forward kernel (R = 16): per stripe nchunks x 17 x 64 column checkpoints, then
+// for all stripes (SG/G) x 64 row checkpoints; word offset of forward lane t's row r at the end of chunk c
+__host__ __device__ inline uint64_t sed_ck_col_word(int stripe, int nchunks, int c, int r, int t) {
+    return ((uint64_t)stripe * (uint64_t)nchunks + (uint64_t)c) * 1088u + (uint64_t)r * 64u + (uint64_t)t;
+}
 // CK batches (L.ck): the traceback that recomputes tiles from the forward kernel's checkpoints
 hipError_t sed_launch_traceback_ck(const sed_launch &L, uint32_t *ops, const sed_i32_params &prm);
 hipError_t sed_launch_selftest(uint32_t *d_out, hipStream_t stream);

@@ -17,18 +17,21 @@
 // step; lane 63's bottom row is collected the same way (wave_shl:1) and written
 // once per 64 steps as the next stripe's top row.
 //
-// Integer kernel (the exact fast path).  When every cost is
+// Integer kernels (the exact fast path).  When every cost is
 // an integral positive Python float (or the int 0 of a match), the reference's
 // fp64 values are exact integers and the per-cell decision
 //    (distance, path length, op)   lexicographically minimal
-// is one unsigned min over packed keys
-//    V = D << 16 | L << 2 | op,   candidates V_pred + (cost << 16) + 4 + op
-// with op 0 insert, 1 delete, 2 update.  The kernels keep every cell in an
-// offset space, W = V - i*(kdel - 1) - j*kins + B, where the insert candidate
-// needs no add and the delete candidate only its op bit; one v_perm_b32 looks
-// the (offset) update constant up from a per-row byte vector, so a cell is 6
-// VALU instructions: v_perm, 2 v_add, v_min3, v_and (clears the op) and
-// v_alignbit (packs the 2-bit op for the traceback).
+// is one unsigned v_min3_u32 over packed keys.  Three key formats, all kept in
+// an offset space where the insert candidate needs no add and every border is a
+// constant (details at "Integer (packed-key) kernels" below):
+//  - ladder keys V = D << 16 + L << 3 + op (per-cell traceback codes): v_perm,
+//    v_add, v_min3, v_and_or (clears the op), v_alignbit (packs the 2-bit op)
+//    = 5 VALU per cell, plus a delete add on 3 of 16 rows;
+//  - distance keys D << 16 - U (U = updates on the path, so at a fixed cell the
+//    low half orders by the path length L = i + j - U): v_perm, v_add, v_min3
+//    = 3 VALU.  Distance-only batches and the checkpoint forward kernel (CK),
+//    whose traceback recomputes tiles in ladder keys converted from them;
+//  - 16-bit packed distance keys, two pairs per word (distance only).
 //
 // fp64 kernel (the general path): fp64 candidates added exactly as the
 // reference does, equality ties, L tie-break on an integer key, and an
@@ -128,11 +131,14 @@ __device__ __forceinline__ void store_tb(uint32_t *p, const uint32_t (&w)[4]) {
 // (c(i) + op) & 3; the traceback kernels subtract the rung of the row they are on.
 // Every border is a constant: W(0, j) = B, W(i, 0) = B + c(i).
 //
-// Distance only (!LEN): keys are D << 16 without the L/op field, W = V -
+// Distance keys (!LEN): V = D << 16 - U without an op field, W = V -
 // i*(delete << 16) - j*(insert << 16) + SED_KB, update constant ((cost - delete -
 // insert) << 16) - 1: an update also subtracts 1 from the low half, which never
-// borrows (fewer than 2^16 updates on any path), so D = (V + 0xFFFF) >> 16.
-// That is v_perm, v_add, v_min3 = 3 VALU per cell; every border is SED_KB.
+// borrows (fewer than 2^16 updates on any path), so D = (V + 0xFFFF) >> 16 and
+// U = (D << 16) - V.  At equal D the smaller key has more updates, i.e. the
+// shorter path (L = i + j - U), so the min is the (D, L) minimum; only the op
+// tie-break is missing, which the CK traceback recomputes.  That is v_perm,
+// v_add, v_min3 = 3 VALU per cell; every border is SED_KB.
 // Lanes run unmasked all the time, and a lane past column m computes columns
 // that nothing reads.
 // ---------------------------------------------------------------------------
@@ -196,8 +202,8 @@ __device__ __forceinline__ void i32_reset(uint32_t (&V)[R], uint32_t &top_prev) 
 // row 0 (D = j*insert, L = j) in offset keys
 template <bool LEN> __device__ __forceinline__ uint32_t i32_row0() { return LEN ? SED_KB3 : SED_KB; }
 
-// The sink cell (n, m) back to V space; returns {D, L} (L = -1 without LEN).
-template <int R, bool LEN>
+// The sink cell (n, m) back to V space; returns {D, L} (without LEN, L = n + m - U when WANT_L, else -1).
+template <int R, bool LEN, bool WANT_L = false>
 __device__ __forceinline__ int2 i32_decode(uint32_t w, int n, int m, const sed_i32_params &prm) {
     if constexpr (LEN) {
         const uint32_t v = w - SED_KB3 - (uint32_t)Ladder<R>::rung(n) + (uint32_t)n * ((prm.del << 16) + 8u) +
@@ -207,8 +213,17 @@ __device__ __forceinline__ int2 i32_decode(uint32_t w, int n, int m, const sed_i
         return make_int2((int)((v - 8u * L) >> 16), (int)L);
     } else {
         const uint32_t v = w - SED_KB + (((uint32_t)n * prm.del + (uint32_t)m * prm.ins) << 16);
-        return make_int2((int)((v + 0xFFFFu) >> 16), -1);
+        const uint32_t D = (v + 0xFFFFu) >> 16;
+        return make_int2((int)D, WANT_L ? n + m - (int)((D << 16) - v) : -1);
     }
+}
+
+// Distance key (!LEN) of a cell in row i -> the ladder key of the same (D, L) (clean, op 0).  With
+// U = (SED_KB - w) & 0xFFFF (updates on the path) both keys share D<<16 - (i*del + j*ins)<<16, and the
+// ladder key is w - SED_KB + SED_KB3 + c(i) - 7U; independent of the column (sed_traceback_ck_kernel).
+__device__ __forceinline__ uint32_t i32_dist_to_ladder(uint32_t w, uint32_t rung) {
+    const uint32_t U = (SED_KB - w) & 0xFFFFu;
+    return w + (SED_KB3 - SED_KB) + rung - 7u * U;
 }
 
 // Ramp for free.  Every lane starts a stripe at its column-0 state and lane t begins real work
@@ -295,8 +310,9 @@ __device__ __forceinline__ bool wait_progress(const uint32_t *prog, uint32_t epo
 // CK (R = 16, not SPLIT): instead of per-cell codes, tb receives checkpoints for the recompute
 // traceback (sed_traceback_ck_kernel): per stripe, at every chunk end each lane's 16 row values and its
 // top_prev ("column checkpoints", [chunk][17][64 lanes]), and every step the bottom row of the lanes
-// t = 3 (mod 4) ("row checkpoints", [group][16][4 steps]) -- 0.13 B per cell instead of 0.25, and no
-// v_alignbit per cell.
+// t = 3 (mod 4) ("row checkpoints", [group][16][4 steps]) -- 0.13 B per cell instead of 0.25.  The CK
+// kernel runs distance keys (LEN = false, 3 VALU per cell instead of the ladder keys' 5.19): they carry
+// (D, L), which is all the checkpoints need; the traceback recomputes the op tie-break.
 template <int R, bool TB, bool SPLIT, bool LEN = true, bool CK = false>
 __global__ __launch_bounds__(SPLIT ? 64 : 256) __attribute__((amdgpu_waves_per_eu(SED_I32_WAVES(R)))) void
 sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *__restrict__ tasks,
@@ -305,7 +321,7 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
                   sed_i32_params prm) {
     constexpr int ROWS = 64 * R;
     constexpr int G = Grp<R>::G;
-    static_assert(!CK || (R == 16 && !SPLIT && !TB && LEN), "checkpoints: R = 16 script batches, one wave per pair");
+    static_assert(!CK || (R == 16 && !SPLIT && !TB && !LEN), "checkpoints: R = 16 distance keys, one wave per pair");
     const int lane = threadIdx.x & 63;
     int pair, kfirst = 0;
     if constexpr (SPLIT) {
@@ -325,6 +341,7 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             res[pair].dist = (double)D;
             res[pair].len = n + m;
             res[pair].is_int = (D == 0);
+            res[pair].err = 0;
         }
         return;
     }
@@ -426,11 +443,11 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
         if (!last) __builtin_amdgcn_s_waitcnt(0);  // own bottom-row stores done before the next stripe reads them
     }
     if (klast == nstripes - 1 && lane == cap_lane) {
-        const int2 dl = i32_decode<R, LEN>(cap, n, m, prm);
+        const int2 dl = i32_decode<R, LEN, CK>(cap, n, m, prm);
         res[pair].dist = (double)dl.x;
         res[pair].len = dl.y;
         res[pair].is_int = (dl.x == 0);
-        res[pair].err = ok ? 0 : 1;  // SPLIT: a timed-out wait anywhere up the stripe chain poisons the pair
+        res[pair].err = ok ? 0 : SED_ERR_SPLIT_TIMEOUT;  // SPLIT: a timed-out wait anywhere up the stripe chain poisons the pair
     }
 }
 
@@ -578,7 +595,7 @@ sed_wf_i32x2_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restr
         sed_result r;
         r.len = -1;
         r.err = 0;
-        r.pad[0] = r.pad[1] = 0;
+        r.seq = 0;
         const uint32_t DP = x2_decode(capP & 0xFFFFu, n, m, prm), DQ = x2_decode(capQ >> 16, n, mQ, prm);
         r.dist = (double)DP;
         r.is_int = (DP == 0);
@@ -674,11 +691,13 @@ __device__ __forceinline__ void i32_chain_group(uint32_t (&V)[R], uint32_t (&cv)
 
 template <int R, bool TB, bool LEN>
 __device__ __forceinline__ void chain_store_result(sed_result *__restrict__ res, int pair, uint32_t cap, int n,
-                                                   int m, const sed_i32_params &prm) {
+                                                   int m, int seq, const sed_i32_params &prm) {
     const int2 dl = i32_decode<R, LEN>(cap, n, m, prm);
     res[pair].dist = (double)dl.x;
     res[pair].len = dl.y;
     res[pair].is_int = (dl.x == 0);
+    res[pair].err = 0;
+    res[pair].seq = (uint16_t)min(seq, 65535);  // the pair's ordinal in its wave (dynamic-CHAIN diagnostics)
 }
 
 // the chain kernel also holds the next pair's cost rows and the column-0 constants
@@ -736,6 +755,7 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
     chain_pair_state cur = chain_load<R>(pd, seqb, chain_pairs[c0], 0), prv = cur;
     bool have_cur = true, have_prv = false;
     int q = c0;
+    int ord = 0, ord_prv = 0;  // ordinals of cur and prv among this wave's pairs
     uint32_t cv[R], cvn[R], V[R];
     rows_of(cur.pair, cv);
 #pragma unroll
@@ -796,20 +816,22 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
             }
             if (capg) {
                 if (have_prv && prv.cap_step >= s && prv.cap_step < s + G && lane == prv.cap_lane)
-                    chain_store_result<R, TB, LEN>(res, prv.pair, capA, prv.n, prv.m, prm);
+                    chain_store_result<R, TB, LEN>(res, prv.pair, capA, prv.n, prv.m, ord_prv, prm);
                 if (have_cur && cur.cap_step >= s && cur.cap_step < s + G && lane == cur.cap_lane)
-                    chain_store_result<R, TB, LEN>(res, cur.pair, capB, cur.n, cur.m, prm);
+                    chain_store_result<R, TB, LEN>(res, cur.pair, capB, cur.n, cur.m, ord, prm);
             }
         }
         lch[lane] = nx;  // after the chunk's last LDS read (in order)
         const int s1 = s0 + 64;
         if (have_cur && s1 == cur.T + cur.S) {  // lane 0 is done with cur: it becomes the draining pair
             prv = cur;
+            ord_prv = ord;
             have_prv = true;
             capA = capB;
             if (have_nxt) {
                 cur = nxt;
                 ++q;
+                ++ord;
                 rows_of(cur.pair, cvn);
                 // lane 0 switches before the next pair's first step
 #pragma unroll
@@ -964,6 +986,7 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
             res[pair].dist = (n == 0) ? (double)m * prm.ins : (double)n * prm.del;
             res[pair].len = n + m;
             res[pair].is_int = (n == 0 && m == 0) ? 1 : (n == 0 ? prm.ins_int : prm.del_int);
+            res[pair].err = 0;
         }
         return;
     }
@@ -1076,6 +1099,7 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
                 res[pair].dist = dv;
                 res[pair].len = (int32_t)(lv >> 2);
                 res[pair].is_int = TYPED ? (uint8_t)tv : (uint8_t)(dv == 0.0);
+                res[pair].err = 0;
             }
         }
     }
@@ -1091,7 +1115,7 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
 template <int R>
 __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
                                                            const uint32_t *__restrict__ tb,
-                                                           const sed_result *__restrict__ res,
+                                                           sed_result *__restrict__ res,
                                                            uint32_t *__restrict__ ops, const uint64_t pat) {
     constexpr int G = Grp<R>::G, P = Ladder<R>::P;
     const int pair = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1104,8 +1128,12 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
     uint32_t *out = ops + d.ops_off;
     int q = res[pair].len;  // ops in the script; written from position q-1 down to 0
     int i = n, j = m;
-    uint32_t acc = 0;
+    uint32_t acc = 0, bad = 0;
     auto emit = [&](uint32_t op) {
+        if (q <= 0) {  // the walk is longer than the sink's L: never write below the pair's script
+            bad = 1;
+            return;
+        }
         --q;
         acc |= op << (2 * (q & 15));
         if ((q & 15) == 0) {
@@ -1152,6 +1180,7 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
     }
     while (j > 0) { emit(0u); --j; }
     while (i > 0) { emit(1u); --i; }
+    if (bad || q != 0) res[pair].err = SED_ERR_TB_LENGTH;
 }
 
 
@@ -1164,7 +1193,7 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
 template <int R>
 __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair_desc *__restrict__ pd,
                                                                   int npairs, const uint32_t *__restrict__ tb,
-                                                                  const sed_result *__restrict__ res,
+                                                                  sed_result *__restrict__ res,
                                                                   uint32_t *__restrict__ ops, const uint64_t pat) {
     constexpr int G = Grp<R>::G, NT = G, NS = R;  // NT * NS = 64 blocks
     constexpr int P = Ladder<R>::P;
@@ -1182,8 +1211,12 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
     // ops are emitted sink -> origin, i.e. from position q-1 down; acc = acc<<2 | op leaves the op of
     // position q in bits 1:0 and position q+p in bits 2p+1:2p when a word [q, q+16) completes
     uint32_t q = (uint32_t)__builtin_amdgcn_readfirstlane(res[pair].len);
-    uint32_t acc = 0;
+    uint32_t acc = 0, bad = 0;
     auto emit = [&](uint32_t op) {
+        if (q == 0) {  // longer than the sink's L (integer flag: a wave-uniform walk)
+            bad = 1;
+            return;
+        }
         acc = (acc << 2) | op;
         if ((--q & 15u) == 0) out[q >> 4] = acc;  // every lane stores the same word (no exec switching)
     };
@@ -1241,6 +1274,7 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
     }
     while (j > 0) { emit(0u); --j; }
     while (i > 0) { emit(1u); --i; }
+    if ((bad | q) && lane == 0) res[pair].err = SED_ERR_TB_LENGTH;
 }
 
 // ---------------------------------------------------------------------------
@@ -1253,20 +1287,24 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
 //   - the row above the tile: the row checkpoints of lane 4Q-1 (or lane 63 of the stripe above, or
 //     row 0), read through LDS by lane 0;
 // with one lane per row (row r at sweep step sigma is at column J0 - 3 + sigma - r, J0 = 64c - 4Q + 1,
-// so that every lane's str2 selectors arrive through the DPP chain from lane 0), the same offset keys
-// and ladder rungs as the forward kernel, so every cell's key -- and its 2-bit choice -- is the forward
-// kernel's.  Lanes of band b hold their checkpoint until their first column (step r - b + 3); the first
-// row of bands 1..3 takes its first diagonal from the checkpoint; columns < 1 get the forward kernel's
-// sentinel selector, so they keep the column-0 borders exactly as its virtual columns do.  The sweep
-// stops at the entry cell's step: the path only goes up and left.  Codes stay in registers, 16 steps
-// per word, and the wave-uniform walk reads them with v_readlane until it leaves the tile.
-// The recompute costs ~1/5 of the per-cell v_alignbit it replaces.
+// so that every lane's str2 selectors arrive through the DPP chain from lane 0).  The forward kernel
+// stores distance keys (D, L without the op); every checkpoint value is converted to the ladder key of
+// the same (D, L) on load (i32_dist_to_ladder), so the recompute runs the ladder recurrence and each
+// cell's key carries the canonical op.  Lanes of band b hold their checkpoint until their first column
+// (step r - b + 3); the first row of bands 1..3 takes its first diagonal from the checkpoint; columns
+// < 1 get the forward kernel's sentinel selector, so they keep the column-0 borders exactly as its
+// virtual columns do.  The sweep stops after the 16-step word holding the entry cell's step (the path
+// only goes up and left), and the entry cell's recomputed key must carry the path length still to
+// emit: a mismatch (a corrupted checkpoint, SED_OPT_DEBUG_CORRUPT) sets res.err instead of writing a
+// wrong script.
+// Codes stay in registers, 16 steps per word; the wave-uniform walk reads them with v_readlane, one
+// unrolled copy of the walk per word, since the step index only decreases along the path.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
                                                               const uint32_t *__restrict__ seqa,
                                                               const uint32_t *__restrict__ seqb,
                                                               const uint32_t *__restrict__ ck,
-                                                              const sed_result *__restrict__ res,
+                                                              sed_result *__restrict__ res,
                                                               uint32_t *__restrict__ ops, sed_i32_params prm) {
     constexpr int R = 16, ROWS = 64 * R, G = Grp<R>::G;
     using Lad = Ladder<R>;
@@ -1278,9 +1316,12 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
     const int n = d.n, m = d.m;
     uint32_t *out = ops + d.ops_off;
     uint32_t q = (uint32_t)__builtin_amdgcn_readfirstlane(res[pair].len);
-    uint32_t acc = 0;
+    uint32_t acc = 0, err = 0;
     auto emit = [&](uint32_t op) {  // sink -> origin, as sed_traceback_window_kernel
-        if (q == 0) return;         // never write below the pair's script (a bad path stops here)
+        if (q == 0) {               // never write below the pair's script
+            err = SED_ERR_TB_LENGTH;
+            return;
+        }
         acc = (acc << 2) | op;
         if ((--q & 15u) == 0) out[q >> 4] = acc;
     };
@@ -1298,22 +1339,26 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
         const int dd = Lad::rung(lane + 1) - Lad::rung(lane);
         const uint32_t s1 = (uint32_t)(dd - 6), dadd = (uint32_t)(dd + 1);
         const int sig0 = lane - band + 3;  // first real sweep step of this lane (<= 63)
-        int guard = 2 * (n + m) + 8;   // tiles visited; every visit makes progress
-        while (i > 0 && j > 0 && --guard > 0) {
+        int guard = 2 * (n + m) + 8;       // tiles visited; every visit makes progress
+        while (i > 0 && j > 0) {
+            if (--guard <= 0) {
+                err = SED_ERR_TB_GUARD;
+                break;
+            }
             const int k = (i - 1) / ROWS, t = ((i - 1) % ROWS) / R, Q = t >> 2;
             const int c = (j - 1 + t) >> 6;
             const int J0 = 64 * c - 4 * Q + 1, rowbase = k * ROWS + 64 * Q;
-            const int sig_end = (j - J0 + 3) + (i - rowbase - 1);  // the entry cell's sweep step (<= 126)
-            // ---- boundaries ----
+            const int re = i - rowbase - 1;              // the entry cell's tile row
+            const int sig_end = (j - J0 + 3) + re;       // the entry cell's sweep step (<= 126)
+            // ---- boundaries (distance keys -> ladder keys; rows rowbase + 16b are on rung 0) ----
             const int ir = min(rowbase + lane, n - 1);  // 0-based str1 index of this lane's row (clamped)
             const uint32_t a = (pa[ir >> 4] >> ((ir & 15) * 2)) & 3u;
             const uint32_t cv = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
             uint32_t V = SED_KB3 + crung, tp = SED_KB3;  // c = 0: the column-0 borders
             if (c >= 1) {
-                const uint32_t *cp = ccp + ((uint64_t)k * (uint64_t)nchunks + (uint64_t)(c - 1)) * 1088u +
-                                     (uint32_t)(4 * Q + band);
-                V = cp[(lane & 15) * 64];
-                tp = cp[16 * 64];
+                const uint32_t *cp = ccp + sed_ck_col_word(k, nchunks, c - 1, lane & 15, 4 * Q + band);
+                V = i32_dist_to_ladder(cp[0], crung);
+                tp = i32_dist_to_ladder(cp[(16 - (lane & 15)) * 64], 0u);
             }
             for (int x = lane; x < 132; x += 64) {
                 // the row above the tile at column J0 - 4 + x: row checkpoints (steps clamped: past SG
@@ -1323,12 +1368,13 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
                     const int st = 64 * c - 5 + x;
                     if (st >= 0) {
                         const int sc = min(st, SG - 1);
-                        v = rcp[((uint64_t)k * (uint64_t)ngroups + (uint64_t)(sc >> 2)) * 64u + (uint32_t)(Q - 1) * 4u +
-                                (uint32_t)(sc & 3)];
+                        v = i32_dist_to_ladder(rcp[((uint64_t)k * (uint64_t)ngroups + (uint64_t)(sc >> 2)) * 64u +
+                                                   (uint32_t)(Q - 1) * 4u + (uint32_t)(sc & 3)], 0u);
                     }
                 } else if (k >= 1) {
                     const int sc = min(64 * c + 59 + x, SG - 1);
-                    v = rcp[((uint64_t)(k - 1) * (uint64_t)ngroups + (uint64_t)(sc >> 2)) * 64u + 60u + (uint32_t)(sc & 3)];
+                    v = i32_dist_to_ladder(rcp[((uint64_t)(k - 1) * (uint64_t)ngroups + (uint64_t)(sc >> 2)) * 64u +
+                                               60u + (uint32_t)(sc & 3)], 0u);
                 }
                 topb[x] = v;
                 const int col = J0 - 3 + x;  // column of lane 0 at step x
@@ -1336,50 +1382,77 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
                 selb[x] = col < 1 ? SED_SEL_SENT3 : i32_sel((pb[ci >> 4] >> ((ci & 15) * 2)) & 3u);
             }
             __syncthreads();
-            // ---- sweep: lane r at step sigma computes (row rowbase + r + 1, column J0 + sigma - r) ----
+            // ---- sweep: lane r at step sigma computes (row rowbase + r + 1, column J0 - 3 + sigma - r) ----
+            // Whole 16-step words (a branch per step would keep the LDS reads from running ahead); the block
+            // holding the entry step also captures each lane's key at that step.
             uint32_t W[8];
             uint32_t tprev = dpp_shr1(topb[0], V);  // diagonal of step 0: the lane above, or row above
-            uint32_t selv = SED_SEL_SENT3;
+            uint32_t selv = SED_SEL_SENT3, ent = 0;
+            const int w_end = sig_end >> 4;
+            auto step = [&](const int sig, uint32_t &wv, const bool capture) {
+                const uint32_t topv = dpp_shr1(topb[sig + 1], V);
+                selv = dpp_shr1(selb[sig], selv);
+                uint32_t diag = tprev;
+                if (sig == 18 || sig == 33 || sig == 48) diag = lane == 16 * ((sig - 3) / 15) ? tp : diag;
+                const uint32_t mm = umin3(V, topv + dadd, diag + __builtin_amdgcn_perm(cv, s1, selv));
+                wv = __builtin_amdgcn_alignbit(mm, wv, 2);
+                const uint32_t vn = (mm & ~7u) | crung;
+                V = (sig < 64 && sig < sig0) ? V : vn;  // left of the band's checkpoint: hold it
+                if (capture) ent = sig == sig_end ? vn : ent;
+                tprev = topv;
+            };
 #pragma unroll
             for (int w = 0; w < 8; ++w) {
-                if (w > 0 && 16 * w > sig_end) break;  // the path never needs later steps
+                if (w > w_end) break;  // the path never needs later steps
+                if (w == w_end) {
 #pragma unroll
-                for (int u = 0; u < 16; ++u) {
-                    const int sig = 16 * w + u;
-                    const uint32_t topv = dpp_shr1(topb[sig + 1], V);
-                    selv = dpp_shr1(selb[sig], selv);
-                    uint32_t diag = tprev;
-                    if (sig == 18 || sig == 33 || sig == 48) diag = lane == 16 * ((sig - 3) / 15) ? tp : diag;
-                    const uint32_t mm = umin3(V, topv + dadd, diag + __builtin_amdgcn_perm(cv, s1, selv));
-                    W[w] = __builtin_amdgcn_alignbit(mm, W[w], 2);
-                    const uint32_t vn = (mm & ~7u) | crung;
-                    V = (sig < 64 && sig < sig0) ? V : vn;  // left of the band's checkpoint: hold it
-                    tprev = topv;
+                    for (int u = 0; u < 16; ++u) step(16 * w + u, W[w], true);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) step(16 * w + u, W[w], false);
                 }
             }
-            // ---- walk inside the tile ----
-            int steps = 0;
-            while (true) {
-                const int r = i - rowbase - 1;
-                if (r < 0 || j < J0 - (r >> 4)) break;  // above the tile or left of the band's window
-                const int sg = (j - J0 + 3) + r;
-                uint32_t wv = W[0];
-#pragma unroll
-                for (int w = 1; w < 8; ++w) wv = (sg >> 4) == w ? W[w] : wv;
-                const uint32_t code = ((uint32_t)__builtin_amdgcn_readlane((int)wv, r) >> (2 * (sg & 15))) & 3u;
-                const uint32_t op = (code - (uint32_t)Lad::rung(i)) & 3u;
-                emit(op);
-                ++steps;
-                i -= (int)(op != 0);
-                j -= (int)(op != 1);
-                if (i == 0 || j == 0) break;
+            // ---- the entry cell's key must carry the ops still to emit (L of a canonical-path cell) ----
+            if ((uint32_t)i32_decode<R, true>((uint32_t)__builtin_amdgcn_readlane((int)ent, re), i, j, prm).y != q) {
+                err = SED_ERR_TB_CHECK;
+                break;
             }
-            if (steps == 0) break;  // no progress: give up rather than spin (tests catch a bad script)
-            __syncthreads();        // topb / selb are rewritten for the next tile
+            // ---- walk inside the tile; one copy per code word ----
+            int steps = 0;
+            uint32_t going = 1;
+#pragma unroll
+            for (int w = 7; w >= 0; --w) {
+                while (going) {
+                    const int r = i - rowbase - 1;
+                    if (r < 0 || j < J0 - (r >> 4)) {  // above the tile or left of the band's window
+                        going = 0;
+                        break;
+                    }
+                    const int sg = (j - J0 + 3) + r;
+                    if ((sg >> 4) != w) break;  // in a lower word: the next copy
+                    const uint32_t code = ((uint32_t)__builtin_amdgcn_readlane((int)W[w], r) >> (2 * (sg & 15))) & 3u;
+                    const uint32_t op = (code - (uint32_t)Lad::rung(i)) & 3u;
+                    emit(op);
+                    ++steps;
+                    i -= (int)(op != 0);
+                    j -= (int)(op != 1);
+                    if (i == 0 || j == 0 || err) going = 0;
+                }
+            }
+            if (err) break;
+            if (steps == 0) {  // no progress: give up rather than spin
+                err = SED_ERR_TB_STALL;
+                break;
+            }
+            __syncthreads();  // topb / selb are rewritten for the next tile
         }
     }
-    while (j > 0) { emit(0u); --j; }
-    while (i > 0) { emit(1u); --i; }
+    if (!err) {
+        while (j > 0) { emit(0u); --j; }
+        while (i > 0) { emit(1u); --i; }
+        if (q != 0) err = SED_ERR_TB_LENGTH;
+    }
+    if (err && lane == 0) res[pair].err = (uint8_t)err;
 }
 
 // ---------------------------------------------------------------------------
@@ -1461,7 +1534,7 @@ hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm, bool l
     const bool tb = L.tb != nullptr;
     if (tb && L.ck) {
         if (L.R != 16 || L.ntasks > 0) return hipErrorInvalidValue;
-        return launch_i32_R<16, false, true, true>(L, prm);
+        return launch_i32_R<16, false, false, true>(L, prm);  // distance keys + checkpoints
     }
     switch (L.R) {
 #define CASE(RR)                                                                                     \

@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void sed_lane_i32_kernel(const sed_pair_desc *
     r.len = L;
     r.is_int = (D == 0);
     r.err = 0;
-    r.pad[0] = r.pad[1] = 0;
+    r.seq = 0;
     res[pair] = r;
     if constexpr (TB) {
         // canonical path, sink -> origin; op k of the script (origin -> sink) at bits 2(k&15) of word k>>4
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(256) void sed_lane_i32x2_kernel(const sed_pair_desc
     sed_result r;
     r.len = -1;
     r.err = 0;
-    r.pad[0] = r.pad[1] = 0;
+    r.seq = 0;
     // 16-bit offset keys back to D: D = W - 0xFFFF + n*delete + m*insert (mod 2^16)
     const uint32_t DP = ((capP & 0xFFFFu) + 1u + (uint32_t)n * prm.del + (uint32_t)mP * prm.ins) & 0xFFFFu;
     const uint32_t DQ = ((capQ >> 16) + 1u + (uint32_t)n * prm.del + (uint32_t)mQ * prm.ins) & 0xFFFFu;
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(256) void sed_lane_f64_kernel(const sed_pair_desc *
     r.len = -1;
     r.is_int = (D == 0.0);
     r.err = 0;
-    r.pad[0] = r.pad[1] = 0;
+    r.seq = 0;
     res[pair] = r;
 }
 

@@ -59,6 +59,8 @@ struct sed_ctx {
     DevBuf gtab;  // fp64 kernel table: per entry {value bits, is-int flag}
     // options
     int opt_mode = 0, opt_R = 0, opt_split = 0, opt_lane = 0, opt_chain = 0, opt_pack = 0, opt_tb = 0;
+    int opt_chain_waves = 0;    // SED_OPT_CHAIN_WAVES: cap on the persistent waves of dynamic CHAIN mode
+    int opt_debug_corrupt = 0;  // SED_OPT_DEBUG_CORRUPT: pair + 1 whose sink-tile checkpoint is overwritten
     DevBuf selftest;
     sed_batch *scratch = nullptr;
 
@@ -400,7 +402,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     b->nchains = 0;
     b->chain_dyn = false;
     if (mode == SED_MODE_I32 && !split && c->opt_chain != 2 && (R == 4 || R == 8) && b->nwave > 0) {
-        const int resident = 1024 * 5;  // SIMDs x the chain kernel's waves per SIMD
+        // SIMDs x the chain kernel's waves per SIMD, unless capped (tests: several fetched pairs per wave)
+        const int resident = c->opt_chain_waves > 0 ? c->opt_chain_waves : 1024 * 5;
         bool ok = true;
         for (int p = 0; p < npairs && ok; ++p)
             if (!b->pd[p].lane && (len_a[p] < 1 || len_a[p] > ROWS || len_b[p] < 1)) ok = false;
@@ -531,7 +534,11 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         fp.K = c->K;
         b->fp = fp;
     }
-    if ((e = grow_log(b, 64)) != hipSuccess) return c->hipfail(e, "event create");
+    // the event log is reused across refills (sed_run_batch's scratch batch): entries are created
+    // only up to 64 ahead of the runs, and run_batch grows it on demand past that
+    b->nlog = 0;
+    if (b->log.size() < 64 && (e = grow_log(b, 64 - b->log.size())) != hipSuccess)
+        return c->hipfail(e, "event create");
     if (b->nbuf > 1 && !b->tb_stream &&
         (e = hipStreamCreateWithFlags(&b->tb_stream, hipStreamNonBlocking)) != hipSuccess)
         return c->hipfail(e, "traceback stream");
@@ -614,6 +621,23 @@ int run_batch(sed_batch *b) {
         if (e != hipSuccess) return c->hipfail(e, "lane kernel launch");
     }
     if ((e = hipEventRecord(lg[1], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
+    if (want_tb && b->ck && c->opt_debug_corrupt > 0 && c->opt_debug_corrupt <= b->npairs) {
+        // SED_OPT_DEBUG_CORRUPT: overwrite the column checkpoint of the sink's row in the chunk before the
+        // sink's tile with the smallest distance key (D offset 0, no updates), which the recompute then
+        // spreads to the sink (test of the traceback's error path: the pair must come back SED_E_DEVICE)
+        const int p = c->opt_debug_corrupt - 1;
+        const sed_pair_desc &d = b->pd[p];
+        const int ROWS = 16 * 64, G = 4;
+        if (!d.lane && d.n > 0 && d.m > 0) {
+            const int nstripes = (d.n + ROWS - 1) / ROWS, SG = (d.m + 63 + G - 1) / G * G, nchunks = (SG + 63) >> 6;
+            const int t = ((d.n - 1) % ROWS) / 16, r = (d.n - 1) % 16, cs = (d.m - 1 + t) >> 6;
+            if (cs >= 1) {
+                uint32_t *w = (uint32_t *)b->d_tb[k].p + d.tb_off + sed_ck_col_word(nstripes - 1, nchunks, cs - 1, r, t);
+                if ((e = hipMemsetD32Async((hipDeviceptr_t)w, 0x0000FFFCu, 1, c->stream)) != hipSuccess)
+                    return c->hipfail(e, "debug corrupt");
+            }
+        }
+    }
     if (want_tb) {
         if (ts != c->stream && (e = hipStreamWaitEvent(ts, lg[1], 0)) != hipSuccess) return c->hipfail(e, "stream wait");
         if ((e = hipEventRecord(lg[2], ts)) != hipSuccess) return c->hipfail(e, "event record");
@@ -651,8 +675,20 @@ int fetch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32_t *
                              hipMemcpyDeviceToHost)) !=
                   hipSuccess)
         return c->hipfail(e, "download results");
-    for (int p = 0; p < np; ++p)
-        if (b->h_res[p].err) return c->fail(SED_E_DEVICE, "pair %d: inter-workgroup hand-off timed out", p);
+    for (int p = 0; p < np; ++p) {
+        switch (b->h_res[p].err) {
+        case 0: break;
+        case SED_ERR_SPLIT_TIMEOUT: return c->fail(SED_E_DEVICE, "pair %d: inter-workgroup hand-off timed out", p);
+        case SED_ERR_TB_CHECK:
+            return c->fail(SED_E_DEVICE, "pair %d: traceback failed: a recomputed tile contradicts the path length "
+                                         "(corrupt checkpoint)", p);
+        case SED_ERR_TB_STALL: return c->fail(SED_E_DEVICE, "pair %d: traceback failed: a tile made no progress", p);
+        case SED_ERR_TB_GUARD: return c->fail(SED_E_DEVICE, "pair %d: traceback failed: too many tile visits", p);
+        case SED_ERR_TB_LENGTH:
+            return c->fail(SED_E_DEVICE, "pair %d: traceback failed: script length differs from the sink's", p);
+        default: return c->fail(SED_E_DEVICE, "pair %d: device error code %d", p, (int)b->h_res[p].err);
+        }
+    }
     for (int p = 0; p < np; ++p) {
         if (out_dist) out_dist[p] = b->h_res[p].dist;
         if (out_is_int) out_is_int[p] = b->h_res[p].is_int;
@@ -725,6 +761,14 @@ int sed_set_option(sed_ctx *c, int key, int value) {
         c->opt_pack = value;
         return SED_OK;
     }
+    if (key == SED_OPT_CHAIN_WAVES && value >= 0) {
+        c->opt_chain_waves = value;
+        return SED_OK;
+    }
+    if (key == SED_OPT_DEBUG_CORRUPT && value >= 0) {
+        c->opt_debug_corrupt = value;
+        return SED_OK;
+    }
     if (key == SED_OPT_CHAIN && value >= 0 && value <= 1024) {
         c->opt_chain = value;
         return SED_OK;
@@ -793,6 +837,35 @@ int sed_batch_chains(const sed_batch *b) { return b ? b->nchains : SED_E_ARG; }
 int sed_batch_traceback_mode(const sed_batch *b) {
     if (!b || !(b->flags & SED_WANT_SCRIPT)) return 0;
     return b->ck ? 2 : 1;
+}
+
+int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave) {
+    if (!b) return SED_E_ARG;
+    sed_ctx *c = b->ctx;
+    (void)hipSetDevice(c->device);
+    if (!b->ran) return c->fail(SED_E_STATE, "batch has not been run");
+    int rc = sync_batch(b);
+    if (rc != SED_OK) return rc;
+    int32_t f = 0, mx = 0;
+    if (b->nchains > 0 && b->npairs > 0) {
+        hipError_t e;
+        if (b->chain_dyn) {  // every persistent wave ends with one failed grab: counter = list + waves
+            uint32_t cnt = 0;
+            if ((e = hipMemcpy(&cnt, (uint32_t *)b->d_chain.p + b->chain_npairs + 1, 4, hipMemcpyDeviceToHost)) !=
+                hipSuccess)
+                return c->hipfail(e, "download chain counter");
+            f = (int32_t)cnt - b->nchains;
+        }
+        std::vector<sed_result> h(b->npairs);
+        if ((e = hipMemcpy(h.data(), b->d_res[b->cur()].p, sizeof(sed_result) * b->npairs, hipMemcpyDeviceToHost)) !=
+            hipSuccess)
+            return c->hipfail(e, "download results");
+        for (int p = 0; p < b->npairs; ++p)
+            if (!b->pd[p].lane && b->n[p] > 0 && b->m[p] > 0) mx = std::max(mx, (int32_t)h[p].seq + 1);
+    }
+    if (fetched) *fetched = f;
+    if (max_per_wave) *max_per_wave = mx;
+    return SED_OK;
 }
 
 int sed_batch_packed_pairs(const sed_batch *b) {

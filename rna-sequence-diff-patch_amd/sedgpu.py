@@ -21,6 +21,8 @@ SED_OPT_LANE = 4
 SED_OPT_CHAIN = 5
 SED_OPT_PACK = 6
 SED_OPT_TB = 7
+SED_OPT_CHAIN_WAVES = 8
+SED_OPT_DEBUG_CORRUPT = 9
 MODE_NAMES = {1: "i32", 2: "f64", 3: "f64-typed"}
 
 _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
@@ -48,6 +50,7 @@ SIGNATURES = [
     ("sed_batch_chains", C.c_int, [C.c_void_p]),
     ("sed_batch_packed_pairs", C.c_int, [C.c_void_p]),
     ("sed_batch_traceback_mode", C.c_int, [C.c_void_p]),
+    ("sed_batch_chain_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("sed_batch_run", C.c_int, [C.c_void_p]),
     ("sed_batch_sync", C.c_int, [C.c_void_p]),
     ("sed_batch_last_times", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
@@ -256,6 +259,12 @@ class Batch:
     def traceback_mode(self):
         """0 distance only, 1 per-cell traceback codes, 2 checkpoints + recompute (SED_OPT_TB)."""
         return self._lib.sed_batch_traceback_mode(self.ptr)
+
+    def chain_stats(self):
+        """(pairs handed out by the dynamic-CHAIN counter, most pairs one wave computed) of the last run."""
+        f, mx = C.c_int32(), C.c_int32()
+        self.ctx._check(self._lib.sed_batch_chain_stats(self.ptr, C.byref(f), C.byref(mx)), "sed_batch_chain_stats")
+        return f.value, mx.value
 
     @property
     def packed_pairs(self):

@@ -23,7 +23,17 @@ Fixture sets:
       over a list-backed collection of the test_input.xml sequences.
 
     python -B tests/golden/make_golden.py --g7       # G7 only
+    python -B tests/golden/make_golden.py --g8       # G8 only
+
+  G8  cost tables the GUI (gui.py:193-252) and hand-edited JSON can produce, each
+      installed as the reference's user_costs global (what reload_user_costs does):
+      fractional insert/delete (border products j*ins, i*del), zero and negative
+      substitutions (int/float typing), substitutions dearer than insert + delete,
+      int literals, a zero insert, and an integer table the packed kernel takes.
+      Per table: G1-style small pairs (every path, full matrix) and G2-style
+      medium pairs (canonical ES, length, matrix digest).
 """
+import copy
 import hashlib
 import io
 import json
@@ -311,6 +321,95 @@ def gen_g7(IR, IX):
     return {"test_input": seqs, "cases": IX.import_xml(cases_path), "searches": searches}
 
 
+def g8_tables():
+    """Cost tables reachable through the GUI's editors (float(val) writes, gui.py:193-252) or a
+    hand-edited user_costs.json, derived from the shipped tables."""
+    with open(os.path.join(REF, "user_costs.json")) as f:
+        user = json.load(f)
+    with open(os.path.join(REF, "costs.json")) as f:
+        dflt = json.load(f)
+    T = {}
+    t = copy.deepcopy(user)
+    t["insert"], t["delete"] = 0.66, 0.83
+    T["frac_indel"] = t
+    t = copy.deepcopy(user)
+    t["update"]["A"]["C"] = 0.0
+    t["update"]["G"]["U"] = 0.0
+    t["update"]["Y"]["N"] = 0.0
+    T["zero_sub"] = t
+    t = copy.deepcopy(dflt)
+    t["insert"], t["delete"] = 1.0, 2.0
+    t["update"]["A"]["G"] = 7.0
+    t["update"]["C"]["U"] = 3.5
+    t["update"]["R"]["A"] = 4.0
+    T["sub_over"] = t
+
+    def ints(x):
+        if isinstance(x, dict):
+            return {k: ints(v) for k, v in x.items()}
+        return int(x) if float(x).is_integer() else x
+    T["int_literals"] = ints(copy.deepcopy(user))
+    t = copy.deepcopy(user)
+    t["insert"], t["delete"] = 3.0, 1.0
+    for a, row in zip("ACGU", ((0, 2, 1, 4), (3, 0, 4, 1), (1, 4, 0, 2), (4, 1, 3, 0))):
+        for b, v in zip("ACGU", row):
+            t["update"][a][b] = float(v)
+    T["gui_int"] = t
+    t = copy.deepcopy(dflt)
+    t["insert"] = 0.0
+    T["zero_insert"] = t
+    t = copy.deepcopy(user)
+    t["update"]["A"]["G"] = -1.0
+    t["update"]["U"]["C"] = -0.5
+    T["negative_sub"] = t
+    return T
+
+
+def gen_g8(S):
+    tables = g8_tables()
+    rng = random.Random(8008)
+    saved = S.user_costs
+    out = {"tables": tables, "small": [], "medium": []}
+    try:
+        for name, table in tables.items():
+            S.user_costs = table  # what reload_user_costs() does after the GUI rewrote user_costs.json
+            for alpha in ("ACGU", IUPAC):
+                for _ in range(24):
+                    s1, s2 = rand_str(rng, alpha, 0, 6), rand_str(rng, alpha, 0, 6)
+                    dp = S.wagnerFisher(s1, s2, True)
+                    rec = {"table": name, "s1": s1, "s2": s2, "dist": vrec(dp[-1][-1].value),
+                           "cells": [[*vrec(n.value), cell_mask(n)] for row in dp for n in row]}
+                    cpath, clen = canonical_from_graph(dp)
+                    rec["canon"] = path_ops(cpath)
+                    paths = create_paths_or_deadlock(S, dp)
+                    if paths is None:
+                        rec["paths"] = "deadlock"
+                    else:
+                        ops = [path_ops(p) for p in paths]
+                        assert ops[0] == rec["canon"], (name, s1, s2)
+                        rec["npaths"] = len(ops)
+                        rec["paths"] = ops[:200]
+                    out["small"].append(rec)
+            for kind, alpha, n, m in (("rand", "ACGU", 256, 256), ("related", "ACGU", 512, 512),
+                                      ("rand", IUPAC, 300, 280), ("related", "ACGU", 1024, 1000)):
+                s1 = "".join(rng.choice(alpha) for _ in range(n))
+                if kind == "related":
+                    s2 = "".join(c if rng.random() >= 0.1 else rng.choice(alpha) for c in s1)[:m]
+                else:
+                    s2 = "".join(rng.choice(alpha) for _ in range(m))
+                dp = S.wagnerFisher(s1, s2, True)
+                cpath, clen = canonical_from_graph(dp)
+                es = S.generate_es(cpath, s1, s2)
+                out["medium"].append({"table": name, "s1": s1, "s2": s2, "kind": kind,
+                                      "dist": vrec(dp[-1][-1].value), "canon": path_ops(cpath), "len": clen,
+                                      "es_sha256": hashlib.sha256(json.dumps(es_compact(es)).encode()).hexdigest(),
+                                      "digest": matrix_digest(dp)})
+                print("G8", name, kind, len(alpha), n, m, out["medium"][-1]["dist"], file=sys.stderr)
+    finally:
+        S.user_costs = saved
+    return out
+
+
 def dump(name, obj):
     path = os.path.join(HERE, name)
     with open(path, "w") as f:
@@ -326,12 +425,16 @@ def main():
     if "--g7" in sys.argv:
         dump("g7_ingest_search.json", gen_g7(IR, IX))
         return
+    if "--g8" in sys.argv:
+        dump("g8_cost_tables.json", gen_g8(S))
+        return
     dump("g1_small.json", gen_g1(S))
     dump("g6_errors.json", gen_g6(S))
     dump("g5_patching.json", gen_g5(S))
     dump("g4_wf_score.json", gen_g4(IR, IX))
     dump("g2_medium.json", gen_g2(S))
     dump("g7_ingest_search.json", gen_g7(IR, IX))
+    dump("g8_cost_tables.json", gen_g8(S))
 
 
 if __name__ == "__main__":

@@ -54,3 +54,22 @@ def test_lex_order_from_sink():
     assert len(paths) == copaths.count_paths(M) == 63  # Delannoy D(3,3)
     key = [(len(p), p[::-1].translate(str.maketrans("idu", "012"))) for p in paths]
     assert key == sorted(key)
+
+
+def test_g8_path_order_on_gui_cost_tables():
+    """Ordered enumeration and counts on the G8 tables (zero/negative costs give many co-optimal paths)."""
+    g8 = load_golden("g8_cost_tables.json")
+    n = 0
+    for r in g8["small"]:
+        if r["paths"] == "deadlock":
+            continue
+        M = np.array([mk for _, _, mk in r["cells"]], np.uint8).reshape(len(r["s1"]) + 1, len(r["s2"]) + 1)
+        got = []
+        for p in copaths.iter_paths(M):
+            got.append("".join("idu"[c] for c in p))
+            if len(got) == len(r["paths"]):
+                break
+        assert got == r["paths"], (r["table"], r["s1"], r["s2"])
+        assert copaths.count_paths(M) == r["npaths"]
+        n += 1
+    assert n > 300

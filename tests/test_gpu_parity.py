@@ -426,3 +426,70 @@ def test_checkpoint_traceback_config2_pair(gpu, tables):
     (d, ii, ln, s), = gpu_run(gpu, tables[True], [(s1, s2)], R=16, split=2, tb=2)
     assert (d, ii) == (float.fromhex(g3["dist"][0]), g3["dist"][1])
     assert ln == len(g3["canon"]) and s == g3["canon"]
+
+
+@pytest.mark.parametrize("mode", [0, 2, 3])
+def test_g8_gui_cost_tables_small(gpu, mode):
+    """G8 (reference-generated): cost tables the GUI can write, in every kernel mode; the auto mode
+    routes the integer table to the packed kernel and the rest to fp64 / fp64-typed."""
+    g8 = load_golden("g8_cost_tables.json")
+    for name, table in g8["tables"].items():
+        recs = [r for r in g8["small"] if r["table"] == name]
+        if mode == 0 and name == "gui_int":
+            acgu = [(r["s1"], r["s2"]) for r in recs if set(r["s1"] + r["s2"]) <= set("ACGU")]
+            plan = sedcost.build_plan(table, [a for a, _ in acgu], [b for _, b in acgu])
+            gpu.set_costs(plan)
+            b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(a) for a, _ in acgu],
+                                                     [plan.encode(y) for _, y in acgu]), True)
+            assert b.mode == "i32"
+            b.close()
+        got = gpu_run(gpu, table, [(r["s1"], r["s2"]) for r in recs], mode=mode)
+        for r, (d, ii, ln, s) in zip(recs, got):
+            assert (d, ii) == (float.fromhex(r["dist"][0]), r["dist"][1]), (name, r["s1"], r["s2"], mode)
+            assert s == r["canon"] and ln == len(r["canon"]), (name, r["s1"], r["s2"], mode)
+
+
+def test_g8_gui_cost_tables_full_matrix(gpu):
+    g8 = load_golden("g8_cost_tables.json")
+    for r in g8["small"][::2]:
+        table = g8["tables"][r["table"]]
+        plan = sedcost.build_plan(table, [r["s1"]], [r["s2"]])
+        gpu.set_costs(plan)
+        D, M = gpu.full_matrix(plan.encode(r["s1"]), plan.encode(r["s2"]))
+        want = [[float.fromhex(h), bool(ii), mk] for h, ii, mk in r["cells"]]
+        have = [[float(d), bool(mm >> 3), int(mm & 7)] for d, mm in zip(D.ravel(), M.ravel())]
+        assert want == have, (r["table"], r["s1"], r["s2"])
+
+
+def test_g8_gui_cost_tables_medium(gpu):
+    """G8 medium pairs (256..1024): distance bits, typing, length and canonical script in auto mode, forced
+    fp64-typed mode, and (integer table) at every R with per-cell codes and with checkpoints."""
+    g8 = load_golden("g8_cost_tables.json")
+    for r in g8["medium"]:
+        table = g8["tables"][r["table"]]
+        runs = [dict(mode=0), dict(mode=3)]
+        if r["table"] == "gui_int" and set(r["s1"] + r["s2"]) <= set("ACGU"):
+            runs += [dict(R=4, split=2), dict(R=8, split=2), dict(R=16, split=2, tb=1), dict(R=16, split=2, tb=2),
+                     dict(split=1)]
+        for kw in runs:
+            (d, ii, ln, s), = gpu_run(gpu, table, [(r["s1"], r["s2"])], **kw)
+            assert (d, ii) == (float.fromhex(r["dist"][0]), r["dist"][1]), (r["table"], r["kind"], kw)
+            assert ln == r["len"] and s == r["canon"], (r["table"], r["kind"], kw)
+        # distance only: the fp64 lane kernel / packed integer kernels where the table allows them
+        (d, ii, ln, s), = gpu_run(gpu, table, [(r["s1"], r["s2"])], script=False, no_len=True)
+        assert (d, ii) == (float.fromhex(r["dist"][0]), r["dist"][1]), (r["table"], r["kind"], "distance")
+
+
+@pytest.mark.parametrize("name", ["frac_indel", "zero_sub", "sub_over", "int_literals", "gui_int",
+                                  "zero_insert", "negative_sub"])
+def test_g8_tables_random_batches_vs_oracle(gpu, name):
+    """The G8 tables on ragged random batches (lane and wave pairs, ACGU and IUPAC) vs the oracle, which
+    test_oracle_golden.py pins to the same tables; scripts, lengths and distance-only routes."""
+    table = load_golden("g8_cost_tables.json")["tables"][name]
+    pairs = _random_pairs(1300 + len(name), 80, "ACGU", 0, 600, related=True)
+    pairs += _random_pairs(1400 + len(name), 80, IUPAC, 1, 300, related=True)
+    pairs += _random_pairs(1500 + len(name), 120, "ACGUN", 1, 40)
+    _oracle_check(table, pairs, gpu_run(gpu, table, pairs))
+    _oracle_check(table, pairs, gpu_run(gpu, table, pairs, script=False))
+    _oracle_check(table, pairs, gpu_run(gpu, table, pairs, script=False, no_len=True), no_len=True)
+    _oracle_check(table, pairs, gpu_run(gpu, table, pairs, mode=3))

@@ -1,0 +1,166 @@
+"""GPU parity of the production routes large batches take (config 3's dynamic CHAIN mode, the default
+checkpoint traceback with lane-kernel pairs in the same batch, pipelined batches) and the traceback's
+error path.  Every pair is checked against the C oracle (multithreaded), op by op."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import sedcost
+import sedgpu
+
+pytestmark = pytest.mark.gpu
+THREADS = min(16, len(os.sched_getaffinity(0)))
+
+
+def _ragged(seed, count, nlo, nhi, mlo, mhi, related=0.5):
+    rng = np.random.default_rng(seed)
+    A, B = [], []
+    for _ in range(count):
+        n, m = int(rng.integers(nlo, nhi + 1)), int(rng.integers(mlo, mhi + 1))
+        a = rng.integers(0, 4, size=n).astype(np.uint8)
+        if rng.random() < related:
+            src = np.resize(a, m) if n else rng.integers(0, 4, size=m).astype(np.uint8)
+            mut = rng.random(m) < 0.12
+            b = np.where(mut, rng.integers(0, 4, size=m), src).astype(np.uint8)
+        else:
+            b = rng.integers(0, 4, size=m).astype(np.uint8)
+        A.append(a)
+        B.append(b)
+    return A, B
+
+
+def _plan(table):
+    return sedcost.build_plan(table, ["ACGU"], ["ACGU"])
+
+
+def _check_all(plan, packed, dist, is_int, ln, ops, script=True, no_len=False):
+    """Every pair vs the oracle: distance bits, typing, length and (script) every op."""
+    cs = oracle.Costs.from_plan(plan)
+    P = packed.npairs
+    od, oi, ol, oops, ooff = oracle.batch(cs, packed.codes_a, packed.off_a, packed.len_a, packed.codes_b,
+                                          packed.off_b, packed.len_b, P, want_ops=script, nthreads=THREADS)
+    assert np.array_equal(dist, od), np.flatnonzero(dist != od)[:10]
+    assert np.array_equal(is_int.astype(bool), oi.astype(bool))
+    if no_len:
+        assert np.all((ln == -1) | (ln == ol))
+    else:
+        assert np.array_equal(ln, ol), np.flatnonzero(ln != ol)[:10]
+    if script:
+        bad = [p for p in range(P)
+               if not np.array_equal(sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln[p])),
+                                     oops[ooff[p]:ooff[p] + ol[p]])]
+        assert not bad, bad[:10]
+
+
+def _batch_run(ctx, packed, script, no_len=False, pipeline=False, runs=1):
+    b = sedgpu.Batch(ctx, packed, script, pipeline=pipeline, no_len=no_len)
+    try:
+        for _ in range(runs):
+            b.run()
+        out = b.results()
+        return b, out
+    except Exception:
+        b.close()
+        raise
+
+
+@pytest.mark.parametrize("user", [False, True])
+def test_dynamic_chain_config3_route(gpu, tables, user):
+    """12 000 ragged single-stripe pairs (n 1..512, m 1..700): more than twice the 5120 resident waves, so
+    the automatic route is dynamic CHAIN (persistent waves fetching pairs from the device counter) at R = 8.
+    Every pair is checked; the counter handed out every wave pair and waves ran several pairs back to back."""
+    A, B = _ragged(3000 + user, 12000, 1, 512, 1, 700)
+    plan = _plan(tables[user])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs(A, B)
+    for script, no_len in ((True, False), (False, False), (False, True)):
+        b, (d, ii, ln, ops) = _batch_run(gpu, packed, script, no_len=no_len)
+        try:
+            nwave = packed.npairs - b.lane_pairs
+            if not no_len:  # distance-only batches pack pairs two per wave instead (SED_OPT_PACK)
+                assert b.rows_per_lane == 8 and b.chains == 5120
+                fetched, per_wave = b.chain_stats()
+                assert fetched == nwave and per_wave >= 2, (fetched, nwave, per_wave)
+        finally:
+            b.close()
+        _check_all(plan, packed, d, ii, ln, ops, script=script, no_len=no_len)
+
+
+def test_dynamic_chain_capped_waves(gpu, tables):
+    """The same route with the persistent waves capped (SED_OPT_CHAIN_WAVES = 300): ~30 fetched pairs per
+    wave, so every wave crosses many pair switches; scripts and lengths vs the oracle."""
+    A, B = _ragged(3100, 9000, 1, 512, 33, 700)
+    plan = _plan(tables[True])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs(A, B)
+    gpu.set_option(sedgpu.SED_OPT_CHAIN, 1)
+    gpu.set_option(sedgpu.SED_OPT_CHAIN_WAVES, 300)
+    try:
+        b, (d, ii, ln, ops) = _batch_run(gpu, packed, True)
+        try:
+            assert b.chains == 300
+            fetched, per_wave = b.chain_stats()
+            assert fetched == packed.npairs - b.lane_pairs and per_wave >= 25, (fetched, per_wave)
+        finally:
+            b.close()
+    finally:
+        gpu.set_option(sedgpu.SED_OPT_CHAIN, 0)
+        gpu.set_option(sedgpu.SED_OPT_CHAIN_WAVES, 0)
+    _check_all(plan, packed, d, ii, ln, ops)
+
+
+def test_checkpoint_default_route_with_lane_pairs_and_pipeline(gpu, tables):
+    """> 256 mixed pairs under automatic options: short str2 (m <= 32) on the lane kernel with per-cell
+    codes, long pairs (n up to 2600) on the R = 16 checkpoint route, in one batch.  Every pair vs the
+    oracle, then the same batch pipelined (SED_PIPELINE, ignored by checkpoint batches) run 3 times."""
+    A1, B1 = _ragged(3200, 200, 1, 512, 1, 32)
+    A2, B2 = _ragged(3201, 120, 513, 2600, 33, 2600)
+    A, B = A1 + A2, B1 + B2
+    order = np.random.default_rng(3202).permutation(len(A))
+    A, B = [A[i] for i in order], [B[i] for i in order]
+    plan = _plan(tables[True])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs(A, B)
+    b, (d, ii, ln, ops) = _batch_run(gpu, packed, True)
+    try:
+        assert b.traceback_mode == 2 and b.rows_per_lane == 16 and b.lane_pairs >= 150
+    finally:
+        b.close()
+    _check_all(plan, packed, d, ii, ln, ops)
+    b, (d2, ii2, ln2, ops2) = _batch_run(gpu, packed, True, pipeline=True, runs=3)
+    b.close()
+    assert np.array_equal(d2, d) and np.array_equal(ln2, ln) and np.array_equal(ops2, ops)
+
+
+def test_checkpoint_traceback_reports_a_corrupt_checkpoint(gpu, tables):
+    """SED_OPT_DEBUG_CORRUPT overwrites one column-checkpoint word (the sink row's, in the chunk before the
+    sink's tile) of one pair with the smallest key between the DP and the traceback: the recomputed tile then contradicts the path
+    length, and the run fails with SedError naming that pair instead of returning a wrong script."""
+    A, B = _ragged(3300, 300, 200, 1500, 100, 1500)
+    plan = _plan(tables[True])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs(A, B)
+    victim = 123
+    gpu.set_option(sedgpu.SED_OPT_DEBUG_CORRUPT, victim + 1)
+    try:
+        with pytest.raises(sedgpu.SedError, match="pair %d: traceback failed" % victim):
+            gpu.run(packed, True)
+    finally:
+        gpu.set_option(sedgpu.SED_OPT_DEBUG_CORRUPT, 0)
+    d, ii, ln, ops = gpu.run(packed, True)  # the same context recovers
+    _check_all(plan, packed, d, ii, ln, ops)
+
+
+def test_repeated_runs_reuse_the_context(gpu, tables):
+    """sed_run_batch refills one scratch batch per call (event log reused, not grown): many small calls in
+    a row stay correct."""
+    A, B = _ragged(3400, 40, 1, 300, 1, 300)
+    plan = _plan(tables[False])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs(A, B)
+    first = gpu.run(packed, True)
+    for _ in range(300):
+        d, ii, ln, ops = gpu.run(packed, True)
+    assert np.array_equal(d, first[0]) and np.array_equal(ops, first[3])

@@ -5,7 +5,7 @@ TAG=${1:-chk}
 O=gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1
 shift || true
 for w in ${@:-c4 c3 c2 c5 c5n iupac}; do
   timeout -k 10 200 python3 bench.py --workload $w --steps 20 --warmup 2 --no-cpu-baseline >> $O/bench.jsonl 2>> $O/bench.log
