@@ -156,7 +156,7 @@ template <int R> struct Ladder {
 // for lane 0 (the stripe's top row and str2 symbol): every lane reads the same
 // LDS word, only lane 0 keeps it (the DPP move's `old` operand).  Lane rows are
 // i = (multiple of P) + r + 1, so row r sits on rung Ladder::rung(r + 1).
-template <int R, bool TB, bool LEN>
+template <int R, bool TB, bool LEN, bool COLLECT = true>
 __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                          uint32_t &bottom, uint32_t &selv, const uint2 tv, uint32_t &outc,
                                          uint32_t (&W)[4], const int u) {
@@ -188,7 +188,7 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
     }
     top_prev = topv;
     bottom = V[R - 1];
-    outc = dpp_shl1(bottom, outc);
+    if constexpr (COLLECT) outc = dpp_shl1(bottom, outc);  // lane 63's bottom row (CK: the row checkpoints)
 }
 
 // Column-0 state of rows row0+1 .. row0+R (row0 = multiple of P) and of row0, the diagonal of the
@@ -218,12 +218,15 @@ __device__ __forceinline__ int2 i32_decode(uint32_t w, int n, int m, const sed_i
     }
 }
 
-// Distance key (!LEN) of a cell in row i -> the ladder key of the same (D, L) (clean, op 0).  With
-// U = (SED_KB - w) & 0xFFFF (updates on the path) both keys share D<<16 - (i*del + j*ins)<<16, and the
-// ladder key is w - SED_KB + SED_KB3 + c(i) - 7U; independent of the column (sed_traceback_ck_kernel).
-__device__ __forceinline__ uint32_t i32_dist_to_ladder(uint32_t w, uint32_t rung) {
+// Distance key (!LEN) of a cell -> the traceback key of the same (D, L) (clean, op 0).  Traceback keys
+// (sed_traceback_ck_kernel) are T = V - i*((delete << 16) + 4) - j*((insert << 16) + 4) + SED_KB over
+// V = D << 16 | L << 2 | op: the insert candidate is the left cell, the delete candidate the cell above
+// + 1, the update candidate the diagonal + ((cost - delete - insert) << 16) - 2, and the winner's low 2
+// bits are the op itself.  With U = (SED_KB - w) & 0xFFFF (updates on the path) both keys share
+// (D - i*delete - j*insert) << 16, and T = w - 3U; independent of the cell's position.
+__device__ __forceinline__ uint32_t i32_dist_to_tb(uint32_t w) {
     const uint32_t U = (SED_KB - w) & 0xFFFFu;
-    return w + (SED_KB3 - SED_KB) + rung - 7u * U;
+    return w - 3u * U;
 }
 
 // Ramp for free.  Every lane starts a stripe at its column-0 state and lane t begins real work
@@ -256,7 +259,7 @@ __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         const int s = s0 + u;
-        i32_step<R, TB, LEN>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u);
+        i32_step<R, TB, LEN, !CK>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u);
         if constexpr (CK) rcv[u] = V[R - 1];  // the band's bottom row, step s (row checkpoints)
         if constexpr (CAP) {
             const bool hit = (s == cap_step) && (lane == cap_lane);
@@ -379,9 +382,17 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
         uint32_t bottom = V[R - 1], selv = i32_sent<LEN>(), outc = 0;
         uint32_t W[4] = {0, 0, 0, 0};
 
+        // CK: the previous stripe's lane 63 stored its bottom row as row checkpoints (column j at step
+        // j + 62, clamped: past SG the columns are beyond m and never read)
+        const uint32_t *rck_prev = tb + d.tb_off + (uint64_t)nstripes * (uint64_t)nchunks * 1088u +
+                                   (uint64_t)(k - 1) * (uint64_t)(SG / G) * 64u + 60u;
         auto load_top = [&](int c) -> uint32_t {
             const int j = 64 * c + lane + 1;
             if (k == 0) return i32_row0<LEN>();
+            if constexpr (CK) {
+                const int st = min(j + 62, SG - 1);
+                return load_sc1(rck_prev + (uint32_t)(st >> 2) * 64u + (uint32_t)(st & 3));
+            }
             if constexpr (SPLIT) {  // after one timeout stop waiting: the kernel must still drain quickly
                 if (ok) ok = wait_progress(prog + d.prog_off + k - 1, prm.epoch << 16, (uint32_t)min(m, 64 * c + 64));
             }
@@ -430,7 +441,7 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
                 cp[16 * 64] = top_prev;
             }
             // lane i holds lane 63's bottom cell of step s-64+i, i.e. column s-126+i at bnd index col+64
-            if (!last) {
+            if (!CK && !last) {
                 bnd_out[s - 62 + lane] = outc;
                 if constexpr (SPLIT)
                     publish_progress(prog + d.prog_off + k, (prm.epoch << 16) | (ok ? 0u : SED_PROG_POISON),
@@ -1288,18 +1299,51 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
 //     row 0), read through LDS by lane 0;
 // with one lane per row (row r at sweep step sigma is at column J0 - 3 + sigma - r, J0 = 64c - 4Q + 1,
 // so that every lane's str2 selectors arrive through the DPP chain from lane 0).  The forward kernel
-// stores distance keys (D, L without the op); every checkpoint value is converted to the ladder key of
-// the same (D, L) on load (i32_dist_to_ladder), so the recompute runs the ladder recurrence and each
-// cell's key carries the canonical op.  Lanes of band b hold their checkpoint until their first column
-// (step r - b + 3); the first row of bands 1..3 takes its first diagonal from the checkpoint; columns
-// < 1 get the forward kernel's sentinel selector, so they keep the column-0 borders exactly as its
-// virtual columns do.  The sweep stops after the 16-step word holding the entry cell's step (the path
-// only goes up and left), and the entry cell's recomputed key must carry the path length still to
-// emit: a mismatch (a corrupted checkpoint, SED_OPT_DEBUG_CORRUPT) sets res.err instead of writing a
-// wrong script.
-// Codes stay in registers, 16 steps per word; the wave-uniform walk reads them with v_readlane, one
-// unrolled copy of the walk per word, since the step index only decreases along the path.
+// stores distance keys (D, L without the op); every checkpoint value is converted on load to the
+// traceback key of the same (D, L) (i32_dist_to_tb), whose min carries the canonical op in its low two
+// bits: 6 VALU per cell (perm, 2 adds, min3, and, alignbit).  Lanes of band b hold their checkpoint
+// until their first column (step r - b + 3) and store code 3 there (outside the band's window); the
+// first row of bands 1..3 takes its first diagonal from the checkpoint; columns < 1 get the sentinel
+// selector, so they keep the column-0 border.  The sweep stops after the 16-step word holding the
+// entry cell's step (the path only goes up and left), and the entry cell's key must carry the path
+// length still to emit: a mismatch (a corrupted checkpoint, SED_OPT_DEBUG_CORRUPT) sets res.err
+// instead of writing a wrong script.  Codes stay in registers, 16 steps per word.  The walk is scalar:
+// one v_readlane per step and the state packed as S = row + (step << 7), so a step is ~16 SALU
+// (a step moves S by 128 / 129 / 257 for insert / delete / update; bit 6 set = above the tile; code
+// 3 = left of the window), one unrolled copy per code word since the step only decreases.
 // ---------------------------------------------------------------------------
+#define SED_TB_MOVES (128ull | (129ull << 16) | (257ull << 32))  // S decrement per op (insert, delete, update)
+template <bool C0>  // C0: chunk-0 tile, whose window reaches the column-0 border: stop at j = 0
+__device__ __forceinline__ uint32_t ck_walk(const uint32_t (&W)[8], uint32_t S, uint32_t &q, uint32_t &acc,
+                                            uint32_t &err, uint32_t *__restrict__ out, const uint32_t q0, int jcol) {
+#pragma unroll
+    for (int w = 7; w >= 0; --w) {
+        if (S >= ((uint32_t)(16 * w) << 7) && S < ((uint32_t)(16 * w + 16) << 7)) {
+            for (;;) {
+                const uint32_t code =
+                    ((uint32_t)__builtin_amdgcn_readlane((int)W[w], (int)(S & 63u)) >> ((S >> 6) & 31u)) & 3u;
+                if (code == 3u) return S;  // left of the band's window
+                if constexpr (C0) {
+                    if (jcol == 0) return S;
+                    jcol -= (int)((5u >> code) & 1u);
+                }
+                acc = (acc << 2) | code;
+                if ((--q & 15u) == 0) {
+                    if (q >= q0) {  // ran past the sink's L
+                        err = SED_ERR_TB_LENGTH;
+                        return S;
+                    }
+                    out[q >> 4] = acc;
+                }
+                S -= (uint32_t)(SED_TB_MOVES >> (code << 4)) & 0xFFFFu;
+                if (S & 64u) return S;  // above the tile
+                if (S < ((uint32_t)(16 * w) << 7)) break;
+            }
+        }
+    }
+    return S;
+}
+
 __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
                                                               const uint32_t *__restrict__ seqa,
                                                               const uint32_t *__restrict__ seqb,
@@ -1307,7 +1351,6 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
                                                               sed_result *__restrict__ res,
                                                               uint32_t *__restrict__ ops, sed_i32_params prm) {
     constexpr int R = 16, ROWS = 64 * R, G = Grp<R>::G;
-    using Lad = Ladder<R>;
     const int lane = threadIdx.x;
     const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x);
     if (pair >= npairs) return;
@@ -1315,10 +1358,10 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
     if (d.lane) return;  // scripted by sed_lane.hip
     const int n = d.n, m = d.m;
     uint32_t *out = ops + d.ops_off;
-    uint32_t q = (uint32_t)__builtin_amdgcn_readfirstlane(res[pair].len);
-    uint32_t acc = 0, err = 0;
-    auto emit = [&](uint32_t op) {  // sink -> origin, as sed_traceback_window_kernel
-        if (q == 0) {               // never write below the pair's script
+    const uint32_t q0 = (uint32_t)__builtin_amdgcn_readfirstlane(res[pair].len);
+    uint32_t q = q0, acc = 0, err = 0;
+    auto emit = [&](uint32_t op) {  // sink -> origin (trailing border runs)
+        if (q == 0) {
             err = SED_ERR_TB_LENGTH;
             return;
         }
@@ -1326,6 +1369,7 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
         if ((--q & 15u) == 0) out[q >> 4] = acc;
     };
     __shared__ uint32_t topb[132], selb[132];
+    const uint32_t Kd = (prm.del << 16) + 4u, Ki = (prm.ins << 16) + 4u;
     int i = n, j = m;
     if (i > 0 && j > 0) {
         const int nstripes = (n + ROWS - 1) / ROWS;
@@ -1333,11 +1377,7 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
         const uint32_t *ccp = ck + d.tb_off;
         const uint32_t *rcp = ccp + (uint64_t)nstripes * (uint64_t)nchunks * 1088u;
         const uint32_t *pa = seqa + d.a_off, *pb = seqb + d.b_off;
-        // per-lane constants: tiles start at rows = 0 (mod 64), so lane r is always on rung(r + 1)
         const int band = lane >> 4;
-        const uint32_t crung = (uint32_t)Lad::rung(lane + 1);
-        const int dd = Lad::rung(lane + 1) - Lad::rung(lane);
-        const uint32_t s1 = (uint32_t)(dd - 6), dadd = (uint32_t)(dd + 1);
         const int sig0 = lane - band + 3;  // first real sweep step of this lane (<= 63)
         int guard = 2 * (n + m) + 8;       // tiles visited; every visit makes progress
         while (i > 0 && j > 0) {
@@ -1348,38 +1388,38 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
             const int k = (i - 1) / ROWS, t = ((i - 1) % ROWS) / R, Q = t >> 2;
             const int c = (j - 1 + t) >> 6;
             const int J0 = 64 * c - 4 * Q + 1, rowbase = k * ROWS + 64 * Q;
-            const int re = i - rowbase - 1;              // the entry cell's tile row
-            const int sig_end = (j - J0 + 3) + re;       // the entry cell's sweep step (<= 126)
-            // ---- boundaries (distance keys -> ladder keys; rows rowbase + 16b are on rung 0) ----
+            const int re = i - rowbase - 1;         // the entry cell's tile row
+            const int sig_end = (j - J0 + 3) + re;  // the entry cell's sweep step (<= 126)
+            // ---- boundaries (distance keys -> traceback keys) ----
             const int ir = min(rowbase + lane, n - 1);  // 0-based str1 index of this lane's row (clamped)
             const uint32_t a = (pa[ir >> 4] >> ((ir & 15) * 2)) & 3u;
             const uint32_t cv = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
-            uint32_t V = SED_KB3 + crung, tp = SED_KB3;  // c = 0: the column-0 borders
+            uint32_t V = SED_KB, tp = SED_KB;  // c = 0: the column-0 borders
             if (c >= 1) {
                 const uint32_t *cp = ccp + sed_ck_col_word(k, nchunks, c - 1, lane & 15, 4 * Q + band);
-                V = i32_dist_to_ladder(cp[0], crung);
-                tp = i32_dist_to_ladder(cp[(16 - (lane & 15)) * 64], 0u);
+                V = i32_dist_to_tb(cp[0]);
+                tp = i32_dist_to_tb(cp[(16 - (lane & 15)) * 64]);
             }
             for (int x = lane; x < 132; x += 64) {
                 // the row above the tile at column J0 - 4 + x: row checkpoints (steps clamped: past SG
-                // the columns are beyond m and never read by the walk; before step 0 the border B)
-                uint32_t v = SED_KB3;
+                // the columns are beyond m and never read by the walk; before step 0 the border)
+                uint32_t v = SED_KB;
                 if (Q >= 1) {
                     const int st = 64 * c - 5 + x;
                     if (st >= 0) {
                         const int sc = min(st, SG - 1);
-                        v = i32_dist_to_ladder(rcp[((uint64_t)k * (uint64_t)ngroups + (uint64_t)(sc >> 2)) * 64u +
-                                                   (uint32_t)(Q - 1) * 4u + (uint32_t)(sc & 3)], 0u);
+                        v = i32_dist_to_tb(rcp[((uint64_t)k * (uint64_t)ngroups + (uint64_t)(sc >> 2)) * 64u +
+                                               (uint32_t)(Q - 1) * 4u + (uint32_t)(sc & 3)]);
                     }
                 } else if (k >= 1) {
                     const int sc = min(64 * c + 59 + x, SG - 1);
-                    v = i32_dist_to_ladder(rcp[((uint64_t)(k - 1) * (uint64_t)ngroups + (uint64_t)(sc >> 2)) * 64u +
-                                               60u + (uint32_t)(sc & 3)], 0u);
+                    v = i32_dist_to_tb(rcp[((uint64_t)(k - 1) * (uint64_t)ngroups + (uint64_t)(sc >> 2)) * 64u + 60u +
+                                           (uint32_t)(sc & 3)]);
                 }
                 topb[x] = v;
                 const int col = J0 - 3 + x;  // column of lane 0 at step x
                 const int ci = min(max(col - 1, 0), m - 1);
-                selb[x] = col < 1 ? SED_SEL_SENT3 : i32_sel((pb[ci >> 4] >> ((ci & 15) * 2)) & 3u);
+                selb[x] = col < 1 ? SED_SEL_SENT : i32_sel((pb[ci >> 4] >> ((ci & 15) * 2)) & 3u);
             }
             __syncthreads();
             // ---- sweep: lane r at step sigma computes (row rowbase + r + 1, column J0 - 3 + sigma - r) ----
@@ -1387,17 +1427,23 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
             // holding the entry step also captures each lane's key at that step.
             uint32_t W[8];
             uint32_t tprev = dpp_shr1(topb[0], V);  // diagonal of step 0: the lane above, or row above
-            uint32_t selv = SED_SEL_SENT3, ent = 0;
+            uint32_t selv = SED_SEL_SENT, ent = 0;
             const int w_end = sig_end >> 4;
             auto step = [&](const int sig, uint32_t &wv, const bool capture) {
                 const uint32_t topv = dpp_shr1(topb[sig + 1], V);
                 selv = dpp_shr1(selb[sig], selv);
                 uint32_t diag = tprev;
                 if (sig == 18 || sig == 33 || sig == 48) diag = lane == 16 * ((sig - 3) / 15) ? tp : diag;
-                const uint32_t mm = umin3(V, topv + dadd, diag + __builtin_amdgcn_perm(cv, s1, selv));
-                wv = __builtin_amdgcn_alignbit(mm, wv, 2);
-                const uint32_t vn = (mm & ~7u) | crung;
-                V = (sig < 64 && sig < sig0) ? V : vn;  // left of the band's checkpoint: hold it
+                const uint32_t mm = umin3(V, topv + 1u, diag + __builtin_amdgcn_perm(cv, 0xFFFFFFFEu, selv));
+                const uint32_t vn = mm & ~3u;
+                if (sig < 64) {  // left of the band's checkpoint: hold it, code 3 (outside the window)
+                    const bool hold = sig < sig0;
+                    wv = __builtin_amdgcn_alignbit(hold ? 3u : mm, wv, 2);
+                    V = hold ? V : vn;
+                } else {
+                    wv = __builtin_amdgcn_alignbit(mm, wv, 2);
+                    V = vn;
+                }
                 if (capture) ent = sig == sig_end ? vn : ent;
                 tprev = topv;
             };
@@ -1413,37 +1459,27 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
                 }
             }
             // ---- the entry cell's key must carry the ops still to emit (L of a canonical-path cell) ----
-            if ((uint32_t)i32_decode<R, true>((uint32_t)__builtin_amdgcn_readlane((int)ent, re), i, j, prm).y != q) {
-                err = SED_ERR_TB_CHECK;
-                break;
-            }
-            // ---- walk inside the tile; one copy per code word ----
-            int steps = 0;
-            uint32_t going = 1;
-#pragma unroll
-            for (int w = 7; w >= 0; --w) {
-                while (going) {
-                    const int r = i - rowbase - 1;
-                    if (r < 0 || j < J0 - (r >> 4)) {  // above the tile or left of the band's window
-                        going = 0;
-                        break;
-                    }
-                    const int sg = (j - J0 + 3) + r;
-                    if ((sg >> 4) != w) break;  // in a lower word: the next copy
-                    const uint32_t code = ((uint32_t)__builtin_amdgcn_readlane((int)W[w], r) >> (2 * (sg & 15))) & 3u;
-                    const uint32_t op = (code - (uint32_t)Lad::rung(i)) & 3u;
-                    emit(op);
-                    ++steps;
-                    i -= (int)(op != 0);
-                    j -= (int)(op != 1);
-                    if (i == 0 || j == 0 || err) going = 0;
+            {
+                const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)ent, re) - SED_KB + (uint32_t)i * Kd +
+                                   (uint32_t)j * Ki;
+                if (((v >> 2) & 0x3FFFu) != q) {
+                    err = SED_ERR_TB_CHECK;
+                    break;
                 }
             }
+            // ---- walk inside the tile ----
+            const uint32_t qin = q;
+            const uint32_t S0 = (uint32_t)re | ((uint32_t)sig_end << 7);
+            const uint32_t S = c == 0 ? ck_walk<true>(W, S0, q, acc, err, out, q0, j)
+                                      : ck_walk<false>(W, S0, q, acc, err, out, q0, j);
             if (err) break;
-            if (steps == 0) {  // no progress: give up rather than spin
+            if (q == qin) {  // no progress: give up rather than spin
                 err = SED_ERR_TB_STALL;
                 break;
             }
+            const int sg = (int)((S + 64u) >> 7), r = (int)((S + 64u) & 127u) - 64;
+            i = rowbase + r + 1;
+            j = J0 - 3 + sg - r;
             __syncthreads();  // topb / selb are rewritten for the next tile
         }
     }

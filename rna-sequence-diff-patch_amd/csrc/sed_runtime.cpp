@@ -278,7 +278,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // SED_PIPELINE is a hint: checkpoint batches run their traceback after the DP on one stream.  Both
     // kernels are issue-bound, so overlap only adds contention (config 4: 20.33 ms sequential against
     // 20.5-20.8 ms pipelined, profiles/r01_ck/ab_pipeline.jsonl) and saves two traceback buffers.
-    if (b->ck) b->nbuf = 1;
+    static const bool ck_pipe = [] { const char *e = getenv("SED_CK_PIPELINE"); return e && atoi(e) > 0; }();
+    if (b->ck && !ck_pipe) b->nbuf = 1;
 
     // ---- layout ----
     b->pd.assign(npairs, sed_pair_desc{});
