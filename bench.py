@@ -117,6 +117,83 @@ def script_costs(plan, A, B, ln, ops, ops_off):
     return ok, cost
 
 
+def cpu_share():
+    """Host cores this process may use: the affinity mask, capped by the cgroup CPU quota and by the
+    per-job thread budget the box exports (OMP_NUM_THREADS), whichever is smallest."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _pyref_task(args):
+    """One reference-regime job (oracle/pyref.py, the node graph of StringEditDistance.py:133-334)."""
+    import pyref
+    s1, s2, table, script = args
+    t0 = time.perf_counter()
+    pyref.run_pair(s1, s2, table, script)
+    return len(s1) * len(s2), time.perf_counter() - t0
+
+
+def cpu_baseline_python(table, alphabet, A, B, qa, qb, want_script, cores, seconds):
+    """Reference-regime leg: the pure-Python node-graph restatement on `cores` processes over a bounded
+    sample of the workload.  Long pairs are sampled as leading B x B blocks (one node graph of ~0.6 M
+    cells, ~0.4 GB, per process at a time); short pairs run whole.  Returns the bench object."""
+    import multiprocessing as mp
+    if A is not None:
+        P, n = A.shape
+        m = B.shape[1]
+        blk = min(n, m, 768)
+        jobs = []
+        for k in range(4 * cores):  # leading blocks of successive pairs (of the one pair's diagonal for c2)
+            p = k % P
+            o = 0 if P > 1 else (k * blk) % max(1, min(n, m) - blk + 1)
+            jobs.append(("".join(alphabet[c] for c in A[p, o:o + blk]), "".join(alphabet[c] for c in B[p, o:o + blk]),
+                         table, want_script))
+        what = "leading %dx%d blocks of the first %d pairs" % (blk, blk, min(P, len(jobs))) if P > 1 else \
+            "%d diagonal %dx%d blocks of the pair" % (len(jobs), blk, blk)
+    else:
+        budget = 1.5e5 * cores * seconds  # ~cells the sample may hold at the reference's rate
+        jobs, cells = [], 0
+        for a, b in zip(qa, qb):
+            jobs.append(("".join(alphabet[c] for c in a), "".join(alphabet[c] for c in b), table, want_script))
+            cells += len(a) * len(b)
+            if cells >= budget:
+                break
+        what = "the first %d of the pairs" % len(jobs)
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(cores) as pool:
+        t0 = time.perf_counter()
+        res = pool.map(_pyref_task, jobs, chunksize=max(1, len(jobs) // (4 * cores)))
+        dt = time.perf_counter() - t0
+    cells = float(sum(c for c, _ in res))
+    return {"value": cells / dt, "unit": "cells/s", "cores": cores, "kind": "port",
+            "sample": "%s, pure-Python node graph (oracle/pyref.py: the reference's Node/Edge regime, %s), "
+                      "%.1f s" % (what, "distance + canonical edit script" if want_script else "distance", dt)}
+
+
 def cpu_baseline(plan, packed, seconds, threads, want_ops):
     """Oracle (C restatement, test infrastructure) on a bounded prefix of the same pairs."""
     import oracle
@@ -159,6 +236,8 @@ def main():
                     help="SED_OPT_CHAIN: 0 auto, 1 force, 2 off, L>=3 force with chains of L pairs (A/B)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-python-baseline", action="store_true",
+                    help="skip the reference-regime leg (pure-Python node graph, oracle/pyref.py)")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_dp_i32_c4.json"),
                     help="per-launch HBM traffic of the DP kernel from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                          "(tools/profile_round.sh + tools/summarize_profile.py); used when its workload matches")
@@ -283,10 +362,7 @@ def main():
         check["script_valid_rate"] = good / P
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        try:
-            threads = min(16, len(os.sched_getaffinity(0)))
-        except AttributeError:
-            threads = min(16, os.cpu_count() or 1)
+        threads = cpu_share()
         cpu = cpu_baseline(plan, packed, args.cpu_seconds, threads, want_script)
         c = cpu["count"]
         exact = (cpu["dist"] == d_gpu[:c]) & ((cpu["len"] == ln_gpu[:c]) | (ln_gpu[:c] == -1))
@@ -302,7 +378,12 @@ def main():
         cpu_obj = {"value": cpu["value"], "unit": "cells/s", "cores": threads, "kind": "port",
                    "sample": "first %d of the %d pairs (%s, %s, %s), C oracle sed_oracle.c, %.1f s"
                              % (c, P, shape, costs_file, "distance + script" if want_script else "distance",
-                                cpu["seconds"])}
+                                cpu["seconds"]),
+                   "cpu_model": cpu_model()}
+        if not args.no_python_baseline:
+            cpu_obj["python_node_graph"] = cpu_baseline_python(
+                table, alpha, A, B, qa if A is None else None, qb if A is None else None, want_script, threads,
+                args.cpu_seconds)
 
     if rank != 0:
         if dist is not None:

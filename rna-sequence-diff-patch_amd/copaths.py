@@ -7,21 +7,35 @@ the origin.  BFS pops partial paths level by level, so its output order is
 
     path length ascending, then the op sequence read from the sink, insert < delete < update
 
-(verified on every G1 golden case).  Enumerating that order directly needs, per cell, the
-set of lengths an origin->cell co-optimal path can have; with it a depth-first search that
-tries insert, delete, update in turn never enters a dead end, so each path costs O(length)
-and the first k paths cost O(k * length) instead of the BFS's exponential frontier.
+(verified on every G1 and G8 golden case).  Enumerating that order directly needs, per
+cell, which lengths an origin->cell co-optimal path can have; with them a depth-first search
+that tries insert, delete, update in turn never enters a dead end, so each path costs
+O(length) and the first k paths cost O(k * length) instead of the BFS's exponential
+frontier.
+
+The lengths are kept as windows above each cell's shortest length (_sedhost.length_windows,
+C): 64 * words bits per cell, exact for every path up to lmin(sink) + 64 * words - 1 ops, and
+widened (recomputed with twice the words) only when the enumeration gets there.  A 4097 x
+4097 matrix then needs 268 MB instead of Python bitsets of up to n + m bits per cell.  The
+path count is a multi-limb row-by-row sum in C (_sedhost.count_paths).  Both fall back to
+the Python restatements below when the host extension is not built.
 
 Input everywhere is the edge mask M[(n+1) x (m+1)] of the full matrix (sed_full_matrix:
 bit 1 insert from the left, 2 delete from above, 4 update from the diagonal, 8 int typing).
 """
 import numpy as np
 
+try:
+    import _sedhost
+except ImportError:  # host C extension not built: the Python restatements below
+    _sedhost = None
+
 _PRED = ((0, -1), (-1, 0), (-1, -1))  # insert, delete, update
 
 
 def length_sets(M):
-    """L[i][j] = Python-int bitset of the lengths of co-optimal origin->(i,j) paths."""
+    """L[i][j] = Python-int bitset of the lengths of co-optimal origin->(i,j) paths (Python
+    restatement; small matrices and the tests)."""
     M = np.asarray(M)
     n, m = M.shape[0] - 1, M.shape[1] - 1
     mk = (M & 7).tolist()
@@ -45,36 +59,82 @@ def length_sets(M):
     return L
 
 
+class LengthWindows:
+    """has(i, j, length): is there a co-optimal origin->(i, j) path of that many ops."""
+
+    def __init__(self, M, words=1):
+        M = np.ascontiguousarray(np.asarray(M, dtype=np.uint8) & 7)
+        self.n, self.m = M.shape[0] - 1, M.shape[1] - 1
+        self.cols = self.m + 1
+        self.words = words
+        if _sedhost is not None:
+            lo, hi, win = _sedhost.length_windows(M.tobytes(), self.n, self.m, words)
+            self.lo = memoryview(lo).cast("i")
+            self.hi = memoryview(hi).cast("i")
+            self.win = memoryview(win).cast("Q")
+            self._sets = None
+        else:
+            self._sets = length_sets(M)
+            lo = [[(s & -s).bit_length() - 1 if s else -1 for s in row] for row in self._sets]
+            hi = [[s.bit_length() - 1 if s else -1 for s in row] for row in self._sets]
+            self.lo = [x for row in lo for x in row]
+            self.hi = [x for row in hi for x in row]
+
+    def exact_up_to(self):
+        """Longest total path length this window answers exactly (None: unlimited)."""
+        if self._sets is not None:
+            return None
+        return self.lo[self.n * self.cols + self.m] + 64 * self.words - 1
+
+    def has(self, i, j, length):
+        if self._sets is not None:
+            return (self._sets[i][j] >> length) & 1
+        c = i * self.cols + j
+        d = length - self.lo[c]
+        if d < 0 or d >= 64 * self.words:
+            return 0
+        return (self.win[c * self.words + (d >> 6)] >> (d & 63)) & 1
+
+    def lengths_at_sink(self):
+        c = self.n * self.cols + self.m
+        return self.lo[c], self.hi[c]
+
+
 def iter_paths(M, L=None):
     """Yield every co-optimal path as uint8 op codes (0 insert, 1 delete, 2 update,
     origin -> sink) in the reference's create_paths order."""
     M = np.asarray(M)
     n, m = M.shape[0] - 1, M.shape[1] - 1
-    if L is None:
-        L = length_sets(M)
-    mk = (M & 7).tolist()
-    total = L[n][m]
-    ell = 0
-    while total >> ell:
-        if not (total >> ell) & 1:
-            ell += 1
+    mk = memoryview(np.ascontiguousarray(M & 7, dtype=np.uint8).tobytes())
+    cols = m + 1
+    win = L if isinstance(L, LengthWindows) else LengthWindows(M)
+    lo, hi = win.lengths_at_sink()
+    if lo < 0:
+        return
+    for ell in range(lo, hi + 1):
+        lim = win.exact_up_to()
+        while lim is not None and ell > lim:  # beyond the window: twice as wide
+            win = LengthWindows(M, win.words * 2)
+            lim = win.exact_up_to()
+        if not win.has(n, m, ell):
             continue
         ops = []
         stack = [[n, m, ell, 0]]  # cell, remaining length, next op to try
+        has = win.has
         while stack:
             top = stack[-1]
             i, j, r, k = top
-            if r == 0:  # at the origin (only L[0][0] has bit 0)
+            if r == 0:  # at the origin (the only cell with a length-0 path)
                 yield np.array(ops[::-1], np.uint8)
                 stack.pop()
                 if ops:
                     ops.pop()
                 continue
-            b = mk[i][j]
+            b = mk[i * cols + j]
             for op in range(k, 3):
                 if b & (1 << op):
                     di, dj = _PRED[op]
-                    if (L[i + di][j + dj] >> (r - 1)) & 1:
+                    if has(i + di, j + dj, r - 1):
                         top[3] = op + 1
                         stack.append([i + di, j + dj, r - 1, 0])
                         ops.append(op)
@@ -83,13 +143,19 @@ def iter_paths(M, L=None):
                 stack.pop()
                 if ops:
                     ops.pop()
-        ell += 1
 
 
 def count_paths(M):
-    """Number of co-optimal paths (exact Python int), anti-diagonal by anti-diagonal with
-    object arrays (two diagonals live), so 4096 x 4096 matrices fit in memory."""
+    """Number of co-optimal paths (exact Python int)."""
     M = np.asarray(M)
+    n, m = M.shape[0] - 1, M.shape[1] - 1
+    if _sedhost is not None:
+        return _sedhost.count_paths(np.ascontiguousarray(M & 7, dtype=np.uint8).tobytes(), n, m)
+    return _count_paths_py(M)
+
+
+def _count_paths_py(M):
+    """Python restatement: anti-diagonal by anti-diagonal with object arrays (two diagonals live)."""
     n, m = M.shape[0] - 1, M.shape[1] - 1
     zero = np.zeros(n + 2, dtype=object)
     d2 = zero.copy()  # diagonal d-2, indexed by row i (+1 offset so i-1 = -1 reads 0)

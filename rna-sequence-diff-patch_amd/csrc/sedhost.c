@@ -18,6 +18,8 @@
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
+#include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 static PyObject *K_OPERATION, *K_SOURCE, *K_DESTINATION, *K_CHARACTER, *K_INDEX;
@@ -517,7 +519,185 @@ static PyObject *rev_es(PyObject *self, PyObject *es) {
     return r;
 }
 
+/* ------------------------------------------------------------------ co-optimal path lengths and count
+ * Over the edge mask M of the full matrix ((n+1) x (m+1) bytes, bit 1 insert from the left, 2 delete
+ * from above, 4 update from the diagonal; sed_full_matrix), for copaths.py.
+ *
+ * length_windows(M, n, m, words) -> (lmin, lmax, win) as bytes: per cell the shortest and longest
+ * co-optimal origin->cell path (int32) and a window of 64*words bits, bit b set when a co-optimal path of
+ * length lmin + b exists.  Exact for every path of total length <= lmin(sink) + 64*words - 1: a prefix
+ * of such a path ends at a cell c with length <= lmin(c) + 64*words - 1, since lmin(c) plus the shortest
+ * c->sink suffix is at least lmin(sink).  4097 x 4097 with words = 1: 268 MB instead of a Python bitset
+ * of up to n+m bits per cell.
+ *
+ * count_paths(M, n, m) -> int: the number of co-optimal origin->sink paths, a row-by-row sum over the
+ * optimal edges in multi-limb integers (two rows live), returned as a Python int. */
+static PyObject *length_windows(PyObject *self, PyObject *args) {
+    Py_buffer mb;
+    Py_ssize_t n, m;
+    int W;
+    if (!PyArg_ParseTuple(args, "y*nni", &mb, &n, &m, &W)) return NULL;
+    PyObject *ret = NULL, *bl = NULL, *bh = NULL, *bw = NULL;
+    const Py_ssize_t cols = m + 1, cells = (n + 1) * cols;
+    if (n < 0 || m < 0 || W < 1 || W > 1024 || mb.len < cells) {
+        PyErr_SetString(PyExc_ValueError, "length_windows: bad shape");
+        goto done;
+    }
+    bl = PyBytes_FromStringAndSize(NULL, 4 * cells);
+    bh = PyBytes_FromStringAndSize(NULL, 4 * cells);
+    bw = PyBytes_FromStringAndSize(NULL, 8 * (Py_ssize_t)W * cells);
+    if (!bl || !bh || !bw) goto done;
+    {
+        const unsigned char *M = (const unsigned char *)mb.buf;
+        int32_t *lo = (int32_t *)PyBytes_AS_STRING(bl), *hi = (int32_t *)PyBytes_AS_STRING(bh);
+        uint64_t *win = (uint64_t *)PyBytes_AS_STRING(bw);
+        Py_BEGIN_ALLOW_THREADS
+        memset(win, 0, 8 * (size_t)W * (size_t)cells);
+        lo[0] = hi[0] = 0;
+        win[0] = 1;
+        for (Py_ssize_t i = 0; i <= n; ++i) {
+            for (Py_ssize_t j = 0; j <= m; ++j) {
+                if (!i && !j) continue;
+                const Py_ssize_t c = i * cols + j;
+                const int mk = M[c] & 7;
+                Py_ssize_t pr[3];
+                int np_ = 0;
+                if ((mk & 1) && j > 0) pr[np_++] = c - 1;
+                if ((mk & 2) && i > 0) pr[np_++] = c - cols;
+                if ((mk & 4) && i > 0 && j > 0) pr[np_++] = c - cols - 1;
+                if (!np_) {  /* unreachable (not in a valid mask): no paths */
+                    lo[c] = hi[c] = -1;
+                    continue;
+                }
+                int32_t a = INT32_MAX, b = -1;
+                for (int k = 0; k < np_; ++k) {
+                    if (lo[pr[k]] < 0) continue;
+                    if (lo[pr[k]] + 1 < a) a = lo[pr[k]] + 1;
+                    if (hi[pr[k]] + 1 > b) b = hi[pr[k]] + 1;
+                }
+                if (b < 0) {
+                    lo[c] = hi[c] = -1;
+                    continue;
+                }
+                lo[c] = a;
+                hi[c] = b;
+                uint64_t *out = win + (size_t)W * (size_t)c;
+                for (int k = 0; k < np_; ++k) {
+                    if (lo[pr[k]] < 0) continue;
+                    const uint64_t *in = win + (size_t)W * (size_t)pr[k];
+                    const int sh = lo[pr[k]] + 1 - a, ws = sh >> 6, bs = sh & 63;
+                    for (int t = W - 1; t >= ws; --t) {
+                        uint64_t v = in[t - ws] << bs;
+                        if (bs && t - ws - 1 >= 0) v |= in[t - ws - 1] >> (64 - bs);
+                        out[t] |= v;
+                    }
+                }
+            }
+        }
+        Py_END_ALLOW_THREADS
+    }
+    ret = PyTuple_Pack(3, bl, bh, bw);
+done:
+    Py_XDECREF(bl);
+    Py_XDECREF(bh);
+    Py_XDECREF(bw);
+    PyBuffer_Release(&mb);
+    return ret;
+}
+
+static PyObject *count_paths(PyObject *self, PyObject *args) {
+    Py_buffer mb;
+    Py_ssize_t n, m;
+    if (!PyArg_ParseTuple(args, "y*nn", &mb, &n, &m)) return NULL;
+    PyObject *ret = NULL;
+    const Py_ssize_t cols = m + 1;
+    uint64_t *prev = NULL, *cur = NULL;
+    size_t cap = 1;  /* limbs per cell, both rows */
+    if (n < 0 || m < 0 || mb.len < (n + 1) * cols) {
+        PyErr_SetString(PyExc_ValueError, "count_paths: bad shape");
+        goto done;
+    }
+    prev = calloc((size_t)cols * cap, 8);
+    cur = calloc((size_t)cols * cap, 8);
+    if (!prev || !cur) {
+        PyErr_NoMemory();
+        goto done;
+    }
+    {
+        const unsigned char *M = (const unsigned char *)mb.buf;
+        int oom = 0;
+        Py_BEGIN_ALLOW_THREADS
+        for (Py_ssize_t i = 0; i <= n && !oom; ++i) {
+            for (Py_ssize_t j = 0; j <= m; ++j) {
+                uint64_t *o = cur + (size_t)j * cap;
+                memset(o, 0, 8 * cap);
+                if (!i && !j) {
+                    o[0] = 1;
+                    continue;
+                }
+                const int mk = M[i * cols + j] & 7;
+                const uint64_t *src[3];
+                int ns = 0;
+                if ((mk & 1) && j > 0) src[ns++] = cur + (size_t)(j - 1) * cap;
+                if ((mk & 2) && i > 0) src[ns++] = prev + (size_t)j * cap;
+                if ((mk & 4) && i > 0 && j > 0) src[ns++] = prev + (size_t)(j - 1) * cap;
+                uint64_t carry_out = 0;
+                for (int k = 0; k < ns; ++k) {
+                    uint64_t carry = 0;
+                    for (size_t t = 0; t < cap; ++t) {
+                        uint64_t s1 = o[t] + src[k][t];
+                        uint64_t c1 = s1 < o[t];
+                        uint64_t s2 = s1 + carry;
+                        c1 += s2 < s1;
+                        o[t] = s2;
+                        carry = c1;
+                    }
+                    carry_out += carry;
+                }
+                if (carry_out) {  /* grow every cell of both rows by one limb, then redo this cell */
+                    const size_t nc = cap + 1;
+                    uint64_t *np2 = calloc((size_t)cols * nc, 8), *nc2 = calloc((size_t)cols * nc, 8);
+                    if (!np2 || !nc2) {
+                        free(np2);
+                        free(nc2);
+                        oom = 1;
+                        break;
+                    }
+                    for (Py_ssize_t x = 0; x <= m; ++x) {
+                        memcpy(np2 + (size_t)x * nc, prev + (size_t)x * cap, 8 * cap);
+                        memcpy(nc2 + (size_t)x * nc, cur + (size_t)x * cap, 8 * cap);
+                    }
+                    free(prev);
+                    free(cur);
+                    prev = np2;
+                    cur = nc2;
+                    cap = nc;
+                    --j;  /* recompute cell j with the wider limbs */
+                    continue;
+                }
+            }
+            uint64_t *t = prev;
+            prev = cur;
+            cur = t;
+        }
+        Py_END_ALLOW_THREADS
+        if (oom) {
+            PyErr_NoMemory();
+            goto done;
+        }
+        /* the last row finished is in prev */
+        ret = _PyLong_FromByteArray((const unsigned char *)(prev + (size_t)m * cap), 8 * cap, 1, 0);
+    }
+done:
+    free(prev);
+    free(cur);
+    PyBuffer_Release(&mb);
+    return ret;
+}
+
 static PyMethodDef methods[] = {
+    {"length_windows", length_windows, METH_VARARGS, "co-optimal path length windows per cell"},
+    {"count_paths", count_paths, METH_VARARGS, "number of co-optimal paths (Python int)"},
     {"es_from_ops", es_from_ops, METH_VARARGS, "generate_es over a canonical op sequence"},
     {"rev_es", rev_es, METH_O, "generate_rev_es"},
     {"seq_from_es", seq_from_es, METH_O, "generate_sequence_from_es"},

@@ -1,9 +1,24 @@
 """ctypes binding of libsed.so (include/sed.h) — the only way the Python side
 reaches the GPU engine.  There is deliberately no CPU fallback: if the library
 or a HIP device is missing, every entry point raises.
+
+Process model.  The reference's callers parallelise by forking: gui.py runs
+wagnerFisher in the GUI process (gui.py:360), then IRMethods.create_search_threads
+forks a multiprocessing.Process per similarity method and again for wf_score
+(IRMethods.py:487-491, 511-514).  HIP cannot be used in a child forked after the
+parent initialised it.  context() therefore returns, in such a child, an
+EngineClient: on first use the child starts one engine worker (a fresh
+interpreter running this file, which owns its own HIP context) and sends every
+call to it over a pipe.  Processes that never inherited a HIP context use the
+GPU directly.  SED_ENGINE=worker keeps HIP out of the calling process always;
+SED_ENGINE=inproc forbids the worker (a forked child then raises SedError).
+An inherited Context is never touched by the child (not even by __del__).
 """
 import ctypes as C
 import os
+import pickle
+import subprocess
+import sys
 import threading
 
 import numpy as np
@@ -89,21 +104,31 @@ def load():
     return lib
 
 
+_hip_pid = None  # pid of the process whose HIP context this module created (inherited by forked children)
+
+
 class Context:
-    """One sed_ctx (device + stream + cost table)."""
+    """One sed_ctx (device + stream + cost table), owned by the process that created it."""
 
     def __init__(self, device=0):
+        global _hip_pid
+        if _hip_pid is not None and _hip_pid != os.getpid():
+            raise SedError("HIP was initialised by process %d and this process is a fork of it: use "
+                           "sedgpu.context(), which runs the engine in a worker process" % _hip_pid)
         lib = load()
         self._lib = lib
+        self._pid = os.getpid()
         self.ptr = lib.sed_create(device)
+        _hip_pid = self._pid
         if not self.ptr:
             raise SedError("sed_create(%d) failed: no usable HIP device" % device)
         self._cost_key = None
 
     def close(self):
-        if self.ptr:
+        # a forked child must not call into the parent's HIP context (it would destroy or hang on it)
+        if self.ptr and self._pid == os.getpid():
             self._lib.sed_destroy(self.ptr)
-            self.ptr = None
+        self.ptr = None
 
     def __del__(self):
         try:
@@ -112,6 +137,8 @@ class Context:
             pass
 
     def _check(self, rc, what):
+        if self._pid != os.getpid():
+            raise SedError("%s: this Context belongs to process %d (fork); use sedgpu.context()" % (what, self._pid))
         if rc != 0:
             msg = self._lib.sed_last_error(self.ptr)
             raise SedError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
@@ -229,9 +256,9 @@ class Batch:
             raise SedError("sed_batch_create failed: %s" % (msg.decode() if msg else ""))
 
     def close(self):
-        if self.ptr:
+        if self.ptr and self.ctx._pid == os.getpid():
             self._lib.sed_batch_destroy(self.ptr)
-            self.ptr = None
+        self.ptr = None
 
     def __del__(self):
         try:
@@ -323,15 +350,169 @@ class Batch:
         return dist[:P], is_int[:P], ln[:P], ops
 
 
+class EngineClient:
+    """The Context interface (set_costs, set_option, set_mode, run, full_matrix, selftest) served by an
+    engine worker process: a fresh interpreter running this file, started on first use, that owns its
+    own HIP context.  One request at a time over a pipe pair; the worker exits when the pipe closes."""
+
+    def __init__(self, device=0):
+        self.device = device
+        self._proc = None
+        self._tx = self._rx = None
+        self._cost_key = None
+        self._pid = os.getpid()
+
+    def _start(self):
+        from multiprocessing.connection import Connection
+        c2w_r, c2w_w = os.pipe()
+        w2c_r, w2c_w = os.pipe()
+        env = dict(os.environ)
+        env["SED_ENGINE"] = "inproc"
+        try:
+            self._proc = subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), "--engine-worker",
+                                           str(self.device), str(c2w_r), str(w2c_w)],
+                                          pass_fds=(c2w_r, w2c_w), close_fds=True, env=env)
+        finally:
+            os.close(c2w_r)
+            os.close(w2c_w)
+        self._tx = Connection(c2w_w, readable=False)
+        self._rx = Connection(w2c_r, writable=False)
+
+    def _call(self, *req):
+        if self._pid != os.getpid():  # a fork of a process with a client: start its own worker
+            self.__init__(self.device)
+        if self._proc is None:
+            self._start()
+        try:
+            self._tx.send_bytes(pickle.dumps(req, protocol=pickle.HIGHEST_PROTOCOL))
+            status, val = pickle.loads(self._rx.recv_bytes())
+        except (EOFError, OSError) as ex:
+            raise SedError("engine worker (pid %s) is gone: %s" % (self._proc.pid if self._proc else "?", ex))
+        if status != "ok":
+            raise SedError(val)
+        return val
+
+    def close(self):
+        if self._proc is not None and self._pid == os.getpid():
+            for f in (self._tx, self._rx):
+                try:
+                    f.close()
+                except OSError:
+                    pass
+            try:
+                self._proc.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                self._proc.kill()
+        self._proc = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_option(self, key, value):
+        self._call("set_option", key, value)
+
+    def set_mode(self, mode):
+        self.set_option(SED_OPT_MODE, mode)
+        self._cost_key = None
+
+    def set_costs(self, plan):
+        key = plan.key()
+        if key == self._cost_key:
+            return
+        self._call("set_costs", plan.K, plan.sub, plan.sub_int, plan.ins, plan.ins_int, plan.dele, plan.del_int)
+        self._cost_key = key
+
+    def selftest(self):
+        return self._call("selftest")
+
+    def run(self, packed, want_script, no_len=False):
+        return self._call("run", packed, want_script, no_len)
+
+    def full_matrix(self, codes_a, codes_b):
+        return self._call("full_matrix", np.asarray(codes_a, np.uint8), np.asarray(codes_b, np.uint8))
+
+
+class _PlanArgs:
+    """The fields Context.set_costs reads from a sedcost.CostPlan."""
+
+    def __init__(self, K, sub, sub_int, ins, ins_int, dele, del_int):
+        self.K, self.sub, self.sub_int = K, sub, sub_int
+        self.ins, self.ins_int, self.dele, self.del_int = ins, ins_int, dele, del_int
+
+    def key(self):
+        return (self.K, self.sub.tobytes(), self.sub_int.tobytes(), self.ins, self.ins_int, self.dele, self.del_int)
+
+
+def _engine_worker(device, rfd, wfd):
+    """Serve EngineClient requests until the client closes the pipe."""
+    from multiprocessing.connection import Connection
+    rx, tx = Connection(rfd, writable=False), Connection(wfd, readable=False)
+    ctx = None
+    while True:
+        try:
+            req = pickle.loads(rx.recv_bytes())
+        except (EOFError, OSError):
+            break
+        try:
+            if ctx is None:
+                ctx = Context(device)
+            op, args = req[0], req[1:]
+            if op == "set_costs":
+                ctx.set_costs(_PlanArgs(*args))
+                val = None
+            elif op == "set_option":
+                ctx.set_option(*args)
+                val = None
+            elif op == "selftest":
+                val = ctx.selftest()
+            elif op == "run":
+                val = ctx.run(*args)
+            elif op == "full_matrix":
+                val = ctx.full_matrix(*args)
+            else:
+                raise SedError("unknown engine request %r" % (op,))
+            out = ("ok", val)
+        except Exception as ex:  # reported to the client as SedError
+            out = ("err", "%s: %s" % (type(ex).__name__, ex))
+        tx.send_bytes(pickle.dumps(out, protocol=pickle.HIGHEST_PROTOCOL))
+    if ctx is not None:
+        ctx.close()
+
+
 _ctx = None
+_ctx_pid = None
+
+
+def _reset_lock_in_child():
+    global _lock
+    _lock = threading.Lock()  # a fork taken while another thread held it must not deadlock the child
+
+
+if hasattr(os, "register_at_fork"):
+    os.register_at_fork(after_in_child=_reset_lock_in_child)
 
 
 def context(device=None):
-    """Process-wide default context (device from SED_DEVICE / LOCAL_RANK, else 0)."""
-    global _ctx
+    """Process-wide default engine (device from SED_DEVICE / LOCAL_RANK, else 0): an in-process Context,
+    or an EngineClient in a child forked after its parent initialised HIP (or with SED_ENGINE=worker)."""
+    global _ctx, _ctx_pid
     with _lock:
-        if _ctx is None:
+        pid = os.getpid()
+        if _ctx is None or _ctx_pid != pid:
             if device is None:
                 device = int(os.environ.get("SED_DEVICE", os.environ.get("LOCAL_RANK", "0")))
-            _ctx = Context(device)
+            mode = os.environ.get("SED_ENGINE", "auto")
+            inherited = _hip_pid is not None and _hip_pid != pid
+            if mode == "worker" or (inherited and mode != "inproc"):
+                _ctx = EngineClient(device)
+            else:
+                _ctx = Context(device)  # raises SedError in a fork of a HIP process (SED_ENGINE=inproc)
+            _ctx_pid = pid
         return _ctx
+
+
+if __name__ == "__main__" and len(sys.argv) == 5 and sys.argv[1] == "--engine-worker":
+    _engine_worker(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))

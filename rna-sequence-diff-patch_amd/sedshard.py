@@ -38,17 +38,21 @@ def gather_to_rank0(tensors, world, rank):
     return out if rank == 0 else None
 
 
-def all_vs_all(seqs, userCosts=False, world=1, rank=0, device=None):
+def all_vs_all(seqs, userCosts=False, world=1, rank=0, device=None, distance_fn=None):
     """Row block of the len(seqs) x len(seqs) matrix of dp[n][m].value
     (query = row = str1, document = column = str2, as IRMethods.search_collection
     orders them) computed on this rank's GPU, gathered to rank 0 as a float64
-    numpy matrix (None on other ranks).  One engine launch per rank."""
+    numpy matrix (None on other ranks).  One engine launch per rank.
+    distance_fn(strs1, strs2, userCosts) -> values replaces StringEditDistance.distance_batch
+    (the CPU tests inject the oracle to check the sharding and reassembly)."""
     import torch
-    import StringEditDistance as SED
+    if distance_fn is None:
+        import StringEditDistance as SED
+        distance_fn = SED.distance_batch
     lo, hi = shard_range(len(seqs), world, rank)
     q = [a for a in seqs[lo:hi] for _ in seqs]
     d = [b for _ in seqs[lo:hi] for b in seqs]
-    vals = np.array(SED.distance_batch(q, d, userCosts), dtype=np.float64) if q else np.zeros(0)
+    vals = np.array(distance_fn(q, d, userCosts), dtype=np.float64) if q else np.zeros(0)
     if world == 1:
         return vals.reshape(hi - lo, len(seqs))
     t = torch.from_numpy(vals).to(device if device is not None else "cpu")

@@ -24,6 +24,13 @@ Fixture sets:
 
     python -B tests/golden/make_golden.py --g7       # G7 only
     python -B tests/golden/make_golden.py --g8       # G8 only
+    python -B tests/golden/make_golden.py --g9       # G9 only
+
+  G9  FASTA ingest: the reference's fa_import.py itself (its import-time loop,
+      fa_import.py:39-62) run on synthetic ./data/ocu.fa files in a scratch
+      directory, with pymongo's MongoClient replaced by a list-backed collection
+      (the inserted documents are recorded); data, get_all_keys() and the
+      inserted sequences per file.
 
   G8  cost tables the GUI (gui.py:193-252) and hand-edited JSON can produce, each
       installed as the reference's user_costs global (what reload_user_costs does):
@@ -410,6 +417,84 @@ def gen_g8(S):
     return out
 
 
+FASTA_CASES = {
+    # multi-line records, T->U / X->N on the accumulated sequence, IUPAC codes, an empty record, duplicate
+    # titles; the last record is never stored.  (Symbols outside the 15-letter alphabet -- lowercase, a
+    # '\r' kept by line[:-1] -- make the reference's tf vector, IRMethods.convert_to_tf_vector, raise
+    # ValueError inside fa_import, so they are not fixture material.)
+    "quirks": ">piR-1 first\nACGT\nTTXA\n>piR-2\nGGGG\n>empty\n>piR-3\nAXT\nRYKM\n>piR-1 first\nUUUU\n"
+              ">piR-4\nCCCC\nNN\n>last\nAAAA\n",
+    "no_trailing_newline": ">a\nACGT\n>b\nTTTT\n>c\nGGXX",
+}
+
+
+def _fasta_cap_case():
+    rng = random.Random(99)
+    lines = []
+    for k in range(520):  # more than the 500-record cap (fa_import.py:22)
+        lines.append(">piR-ocu-%d some description\n" % k)
+        seq = "".join(rng.choice("ACGTX") for _ in range(rng.randint(24, 32)))
+        for a in range(0, len(seq), 10):
+            lines.append(seq[a:a + 10] + "\n")
+    return "".join(lines)
+
+
+class _MongoStandIn:
+    """pymongo.MongoClient stand-in for fa_import.py's import-time code (fa_import.py:14-16,49): no
+    server; insert_one appends to a list."""
+
+    inserted = []
+
+    class _Coll:
+        def insert_one(self, doc):
+            _MongoStandIn.inserted.append(doc["sequence"])
+
+        def find(self, flt):
+            return iter([])
+
+    class _Db:
+        def __init__(self):
+            self.sequences = _MongoStandIn._Coll()
+
+    def __init__(self, *a, **k):
+        self.rna_db = _MongoStandIn._Db()
+
+
+def gen_g9():
+    import tempfile
+    import types
+    cases = dict(FASTA_CASES)
+    cases["cap_520_records"] = _fasta_cap_case()
+    fake = types.ModuleType("pymongo")
+    fake.MongoClient = _MongoStandIn
+    real = sys.modules.get("pymongo")
+    sys.modules["pymongo"] = fake
+    out = {}
+    cwd = os.getcwd()
+    try:
+        for name, text in cases.items():
+            with tempfile.TemporaryDirectory() as tmp:
+                os.mkdir(os.path.join(tmp, "data"))
+                with open(os.path.join(tmp, "data", "ocu.fa"), "w", newline="") as f:
+                    f.write(text)
+                os.chdir(tmp)
+                _MongoStandIn.inserted = []
+                sys.modules.pop("fa_import", None)
+                with contextlib.redirect_stdout(io.StringIO()):
+                    import fa_import  # runs the reference's import loop on ./data/ocu.fa
+                out[name] = {"fasta": text, "data": list(fa_import.data.items()),
+                             "keys": fa_import.get_all_keys(), "inserted": list(_MongoStandIn.inserted)}
+                os.chdir(cwd)
+    finally:
+        os.chdir(cwd)
+        sys.modules.pop("fa_import", None)
+        if real is not None:
+            sys.modules["pymongo"] = real
+        else:
+            sys.modules.pop("pymongo", None)
+    return out
+
+
 def dump(name, obj):
     path = os.path.join(HERE, name)
     with open(path, "w") as f:
@@ -428,6 +513,9 @@ def main():
     if "--g8" in sys.argv:
         dump("g8_cost_tables.json", gen_g8(S))
         return
+    if "--g9" in sys.argv:
+        dump("g9_fasta.json", gen_g9())
+        return
     dump("g1_small.json", gen_g1(S))
     dump("g6_errors.json", gen_g6(S))
     dump("g5_patching.json", gen_g5(S))
@@ -435,6 +523,7 @@ def main():
     dump("g2_medium.json", gen_g2(S))
     dump("g7_ingest_search.json", gen_g7(IR, IX))
     dump("g8_cost_tables.json", gen_g8(S))
+    dump("g9_fasta.json", gen_g9())
 
 
 if __name__ == "__main__":

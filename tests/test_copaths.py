@@ -73,3 +73,56 @@ def test_g8_path_order_on_gui_cost_tables():
         assert copaths.count_paths(M) == r["npaths"]
         n += 1
     assert n > 300
+
+
+def test_c_windows_and_count_match_the_python_restatement():
+    """_sedhost.length_windows / count_paths (C) against the Python bitsets and big-int count on random
+    masks of real DPs (oracle full matrices), including windows narrower than the path-length spread."""
+    import oracle
+    import sedcost
+    rng = np.random.default_rng(11)
+    table = load_golden("g8_cost_tables.json")["tables"]["zero_insert"]  # many co-optimal paths
+    for _ in range(30):
+        a = "".join(rng.choice(list("ACGU"), size=int(rng.integers(0, 25))))
+        b = "".join(rng.choice(list("ACGU"), size=int(rng.integers(0, 25))))
+        plan = sedcost.build_plan(table, [a], [b])
+        M = oracle.pair(oracle.Costs.from_plan(plan), plan.encode(a), plan.encode(b), full=True)["M"]
+        sets = copaths.length_sets(M)
+        for words in (1, 2):
+            w = copaths.LengthWindows(M, words)
+            for i in range(M.shape[0]):
+                for j in range(M.shape[1]):
+                    s = sets[i][j]
+                    assert w.lo[i * w.cols + j] == ((s & -s).bit_length() - 1 if s else -1)
+                    assert w.hi[i * w.cols + j] == (s.bit_length() - 1 if s else -1)
+                    for ell in range(w.lo[i * w.cols + j], w.lo[i * w.cols + j] + 64 * words):
+                        assert w.has(i, j, ell) == (s >> ell) & 1
+        assert copaths.count_paths(M) == copaths._count_paths_py(np.asarray(M))
+        got = list(itertools.islice(copaths.iter_paths(M), 300))
+        saved, copaths._sedhost = copaths._sedhost, None
+        try:
+            ref = list(itertools.islice(copaths.iter_paths(M), 300))
+        finally:
+            copaths._sedhost = saved
+        assert [p.tolist() for p in got] == [p.tolist() for p in ref]
+
+
+def test_window_bounds_and_large_counts():
+    """Every monotone path is co-optimal (all edges set): length classes come out in order, the sink's
+    window reports its exact range, and the C count equals the Python big-int count (Delannoy D(40, 40))."""
+    n = m = 40
+    M = np.zeros((n + 1, m + 1), np.uint8)
+    M[0, 1:] = 1
+    M[1:, 0] = 2
+    M[1:, 1:] = 7
+    lengths = []
+    for p in copaths.iter_paths(M):
+        if not lengths or len(p) != lengths[-1]:
+            lengths.append(len(p))
+        if len(lengths) > 3:
+            break
+    assert lengths == [40, 41, 42, 43]
+    w = copaths.LengthWindows(M)
+    assert w.lengths_at_sink() == (40, 80) and w.exact_up_to() == 103
+    total = copaths.count_paths(M)
+    assert total == copaths._count_paths_py(M) and total.bit_length() > 64  # Delannoy D(40, 40)

@@ -1,0 +1,81 @@
+"""CPU: the drop-in module under the reference's process model (IRMethods.create_search_threads forks a
+multiprocessing.Process per method after gui.py ran wagnerFisher in the parent, IRMethods.py:487-491,
+511-514).  A child forked after its parent initialised HIP must never call into the inherited context:
+sedgpu.context() gives it an engine worker process instead (SED_ENGINE=inproc: a clear SedError).  Here
+the parent's HIP initialisation is simulated (no GPU in this container), so the worker itself reports
+that no device exists -- as an error, within seconds, not a hang."""
+import multiprocessing as mp
+import os
+
+import numpy as np
+import pytest
+
+import sedgpu
+
+
+class _NoCallLib:
+    """Stands in for libsed in an inherited Context: any call from the child fails the test."""
+
+    def __getattr__(self, name):
+        raise AssertionError("child called %s on the parent's HIP context" % name)
+
+
+def _child(q, engine):
+    try:
+        if engine is not None:
+            os.environ["SED_ENGINE"] = engine
+        inherited = sedgpu._ctx
+        inherited.close()  # must not touch the parent's context
+        assert inherited.ptr is None
+        ctx = sedgpu.context()
+        kind = type(ctx).__name__
+        packed = sedgpu.PackedPairs([np.array([0, 1, 2], np.uint8)], [np.array([0, 2], np.uint8)])
+        try:
+            ctx.run(packed, False)
+            q.put((kind, "no error"))
+        except sedgpu.SedError as ex:
+            q.put((kind, str(ex)))
+    except BaseException as ex:  # reported to the parent
+        q.put(("crash", repr(ex)))
+
+
+def _fake_parent_context():
+    """A Context as the parent would hold after gui.py's wagnerFisher (HIP initialised in this pid)."""
+    c = sedgpu.Context.__new__(sedgpu.Context)
+    c._lib, c.ptr, c._pid, c._cost_key = _NoCallLib(), 12345, os.getpid(), None
+    return c
+
+
+@pytest.mark.parametrize("engine", [None, "inproc"])
+def test_forked_child_never_uses_the_parents_hip_context(monkeypatch, engine):
+    monkeypatch.setattr(sedgpu, "_hip_pid", os.getpid())
+    monkeypatch.setattr(sedgpu, "_ctx", _fake_parent_context())
+    monkeypatch.setattr(sedgpu, "_ctx_pid", os.getpid())
+    monkeypatch.delenv("SED_ENGINE", raising=False)
+    fork = mp.get_context("fork")
+    q = fork.Queue()
+    p = fork.Process(target=_child, args=(q, engine))
+    p.start()
+    kind, msg = q.get(timeout=120)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    if engine == "inproc":
+        assert kind == "crash" and "fork" in msg  # context() refuses to build a Context in the fork
+    else:
+        assert kind == "EngineClient", msg
+        assert "sed_create(0) failed" in msg or "libsed.so not found" in msg, msg
+    sedgpu._ctx.ptr = None  # the fake must not reach sed_destroy here either
+
+
+def test_worker_engine_reports_errors_without_a_device(monkeypatch):
+    """SED_ENGINE=worker: the calling process never loads HIP; requests go to the worker, whose errors
+    come back as SedError."""
+    monkeypatch.setattr(sedgpu, "_ctx", None)
+    monkeypatch.setattr(sedgpu, "_ctx_pid", None)
+    monkeypatch.setenv("SED_ENGINE", "worker")
+    ctx = sedgpu.context()
+    assert isinstance(ctx, sedgpu.EngineClient)
+    with pytest.raises(sedgpu.SedError):
+        ctx.selftest()
+    ctx.close()
+    monkeypatch.setattr(sedgpu, "_ctx", None)

@@ -1,7 +1,6 @@
-"""CPU: sequence ingest (seqio.py) against the reference's import_xml output (G7, generated
-by importing the reference) and against fa_import.py's loop restated line by line
-(fa_import.py cannot be imported: it connects to MongoDB and opens ./data/ocu.fa at import,
-so the FASTA cases below are parity-unpinned restatements of fa_import.py:39-62)."""
+"""CPU: sequence ingest (seqio.py) against the reference's own outputs: import_xml (G7) and
+fa_import.py's import loop (G9: the reference module run on synthetic ./data/ocu.fa files with a
+list-backed stand-in for its MongoDB collection, tests/golden/make_golden.py --g9)."""
 import os
 
 import numpy as np
@@ -60,3 +59,17 @@ def test_encode_many():
         seqio.encode_many(["ACX"], code)
     assert ei.value.args == ("X",)
     assert seqio.encode_many([], code)[0].size == 0
+
+
+@pytest.mark.parametrize("case", ["quirks", "no_trailing_newline", "cap_520_records"])
+def test_fasta_matches_reference_fa_import(case):
+    """G9: fa_import.data (title -> sequence, dict order), get_all_keys() and the documents it inserted
+    (order, T->U / X->N, 500-record cap, the dropped last record) from the same file."""
+    g9 = load_golden("g9_fasta.json")[case]
+    lines = g9["fasta"].splitlines(keepends=True)
+    recs = seqio.read_fasta(lines)
+    assert [s for _, s in recs] == g9["inserted"]
+    d = seqio.fasta_dict(lines)
+    assert list(d.items()) == [tuple(x) for x in g9["data"]]
+    assert list(d) == g9["keys"]
+    assert seqio.ListCollection.from_fasta(lines).sequences() == g9["inserted"]

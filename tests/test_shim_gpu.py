@@ -193,3 +193,52 @@ def test_script_hint_runs_agree(SED):
     SED._script_hint = True
     assert SED.wagnerFisher("ACGU", "AGU")._script is not None
     assert SED.wagnerFisher("ACGU", "AGU")._script is None  # nobody asked for the last script: distance-only again
+
+
+def _ref_search_collection(query, vector_type, collection, method, return_dict=None, callback=None):
+    """IRMethods.search_collection (IRMethods.py:443-477) for method == wf_score: one wagnerFisher per
+    document through the drop-in module, exactly as the unchanged caller does."""
+    scores = []
+    for doc in collection.find({}):
+        scores.append((doc['sequence'], method(query, doc['sequence'])))
+    if callback is not None:
+        callback(scores)
+    elif return_dict is not None:
+        return_dict[method.__name__] = scores
+    else:
+        return scores
+
+
+def test_create_search_threads_process_model(SED):
+    """gui.py:360 runs wagnerFisher in the GUI process (HIP initialised there), then
+    IRMethods.create_search_threads forks a Process per method and another for wf_score, delivering through
+    Manager dicts (IRMethods.py:480-515).  The forked children get an engine worker; results match G7."""
+    import multiprocessing as mp
+    import seqio
+    import sedgpu
+    import wfsearch
+    g7 = load_golden("g7_ingest_search.json")
+    coll = seqio.ListCollection.from_sequences(list(g7["test_input"].values()))
+    SED.wagnerFisher("AGRGA", "AGGGAA", True)  # the parent's GPU call (gui.py:360)
+    assert isinstance(sedgpu.context(), sedgpu.Context)
+    fork = mp.get_context("fork")
+    manager = fork.Manager()
+    for s in g7["searches"][:2]:
+        want = [[seq, float.fromhex(h)] for seq, h in s["scores"]]
+        return_dict, wagner_dict = manager.dict(), manager.dict()
+        jobs = [fork.Process(target=_ref_search_collection, args=(s["query"], "tf", coll, wfsearch.wf_score,
+                                                                  return_dict))]
+        for p in jobs:
+            p.start()
+        for p in jobs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+        p = fork.Process(target=_ref_search_collection, args=(s["query"], "tf", coll, wfsearch.wf_score, wagner_dict))
+        p.start()
+        p.join(timeout=120)
+        assert p.exitcode == 0
+        assert [[a, b] for a, b in return_dict["wf_score"]] == want
+        assert [[a, b] for a, b in wagner_dict["wf_score"]] == want
+    manager.shutdown()
+    dp = SED.wagnerFisher("ACGU", "AGU")  # the parent's own context still works
+    assert dp[len(dp) - 1][len(dp[0]) - 1].value == 1
