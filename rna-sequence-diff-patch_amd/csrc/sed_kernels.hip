@@ -1297,8 +1297,8 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
 //     above the band at that column), or the column-0 borders for c = 0;
 //   - the row above the tile: the row checkpoints of lane 4Q-1 (or lane 63 of the stripe above, or
 //     row 0), read through LDS by lane 0;
-// with one lane per row (row r at sweep step sigma is at column J0 - 3 + sigma - r, J0 = 64c - 4Q + 1,
-// so that every lane's str2 selectors arrive through the DPP chain from lane 0).  The forward kernel
+// with one lane per row (row r at sweep step sigma is at column J0 - 3 + sigma - r, J0 = 64c - 4Q + 1; the
+// cell above arrives through the DPP chain from lane r - 1, the str2 selector from LDS).  The forward kernel
 // stores distance keys (D, L without the op); every checkpoint value is converted on load to the
 // traceback key of the same (D, L) (i32_dist_to_tb), whose min carries the canonical op in its low two
 // bits: 6 VALU per cell (perm, 2 adds, min3, and, alignbit).  Lanes of band b hold their checkpoint
@@ -1313,32 +1313,32 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
 // 3 = left of the window), one unrolled copy per code word since the step only decreases.
 // ---------------------------------------------------------------------------
 #define SED_TB_MOVES (128ull | (129ull << 16) | (257ull << 32))  // S decrement per op (insert, delete, update)
+// The walk of one tile from state S; returns the state of the first cell it did not take (outside the
+// tile: above it, left of its band's window, or at column 0 for C0).  One loop per code word, each with a
+// single exit: the next code is read before the bounds test, and a cell past the word's bound or
+// outside the tile reads as the marker 3.
 template <bool C0>  // C0: chunk-0 tile, whose window reaches the column-0 border: stop at j = 0
 __device__ __forceinline__ uint32_t ck_walk(const uint32_t (&W)[8], uint32_t S, uint32_t &q, uint32_t &acc,
                                             uint32_t &err, uint32_t *__restrict__ out, const uint32_t q0, int jcol) {
 #pragma unroll
     for (int w = 7; w >= 0; --w) {
-        if (S >= ((uint32_t)(16 * w) << 7) && S < ((uint32_t)(16 * w + 16) << 7)) {
-            for (;;) {
-                const uint32_t code =
-                    ((uint32_t)__builtin_amdgcn_readlane((int)W[w], (int)(S & 63u)) >> ((S >> 6) & 31u)) & 3u;
-                if (code == 3u) return S;  // left of the band's window
-                if constexpr (C0) {
-                    if (jcol == 0) return S;
-                    jcol -= (int)((5u >> code) & 1u);
-                }
+        const uint32_t lo = (uint32_t)(16 * w) << 7;
+        if (S >= lo && S < lo + (16u << 7) && !(S & 64u)) {
+            uint32_t code = ((uint32_t)__builtin_amdgcn_readlane((int)W[w], (int)S) >> ((S >> 6) & 31u)) & 3u;
+            if (C0 && jcol == 0) code = 3u;
+            while (code != 3u) {
                 acc = (acc << 2) | code;
                 if ((--q & 15u) == 0) {
-                    if (q >= q0) {  // ran past the sink's L
-                        err = SED_ERR_TB_LENGTH;
-                        return S;
-                    }
-                    out[q >> 4] = acc;
+                    if (q < q0) out[q >> 4] = acc;
+                    else err = SED_ERR_TB_LENGTH;  // ran past the sink's L (the tile still bounds the walk)
                 }
+                if constexpr (C0) jcol -= (int)((5u >> code) & 1u);
                 S -= (uint32_t)(SED_TB_MOVES >> (code << 4)) & 0xFFFFu;
-                if (S & 64u) return S;  // above the tile
-                if (S < ((uint32_t)(16 * w) << 7)) break;
+                const uint32_t f = ((uint32_t)__builtin_amdgcn_readlane((int)W[w], (int)S) >> ((S >> 6) & 31u)) & 3u;
+                const bool out_of = (S & 64u) || S < lo || (C0 && jcol == 0);
+                code = out_of ? 3u : f;
             }
+            if ((S & 64u) || S >= lo || (C0 && jcol == 0)) return S;  // left the tile (not just the word)
         }
     }
     return S;
@@ -1368,7 +1368,9 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
         acc = (acc << 2) | op;
         if ((--q & 15u) == 0) out[q >> 4] = acc;
     };
-    __shared__ uint32_t topb[132], selb[132];
+    // selb[64 + x]: str2 selector of lane 0's column at step x; lane r reads selb[64 + sigma - r] itself
+    // (its column at step sigma), so no selector travels through the DPP chain
+    __shared__ uint32_t topb[132], selb[64 + 132];
     const uint32_t Kd = (prm.del << 16) + 4u, Ki = (prm.ins << 16) + 4u;
     int i = n, j = m;
     if (i > 0 && j > 0) {
@@ -1419,7 +1421,7 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
                 topb[x] = v;
                 const int col = J0 - 3 + x;  // column of lane 0 at step x
                 const int ci = min(max(col - 1, 0), m - 1);
-                selb[x] = col < 1 ? SED_SEL_SENT : i32_sel((pb[ci >> 4] >> ((ci & 15) * 2)) & 3u);
+                selb[64 + x] = col < 1 ? SED_SEL_SENT : i32_sel((pb[ci >> 4] >> ((ci & 15) * 2)) & 3u);
             }
             __syncthreads();
             // ---- sweep: lane r at step sigma computes (row rowbase + r + 1, column J0 - 3 + sigma - r) ----
@@ -1427,17 +1429,22 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
             // holding the entry step also captures each lane's key at that step.
             uint32_t W[8];
             uint32_t tprev = dpp_shr1(topb[0], V);  // diagonal of step 0: the lane above, or row above
-            uint32_t selv = SED_SEL_SENT, ent = 0;
+            uint32_t ent = 0;
+            const uint32_t *selp = selb + 64 - lane;  // lane r's selector at step sigma: selp[sigma]
             const int w_end = sig_end >> 4;
+            // the hold threshold, opaque per tile: otherwise all 64 `sig < sig0` masks are hoisted out of the
+            // tile loop into SGPR pairs, which spill to VGPR lanes and come back with a v_readlane per step
+            int hold_below = sig0;
+            asm volatile("" : "+v"(hold_below));
             auto step = [&](const int sig, uint32_t &wv, const bool capture) {
                 const uint32_t topv = dpp_shr1(topb[sig + 1], V);
-                selv = dpp_shr1(selb[sig], selv);
+                const uint32_t selv = selp[sig];  // steps before the lane's first column read don't-care
                 uint32_t diag = tprev;
                 if (sig == 18 || sig == 33 || sig == 48) diag = lane == 16 * ((sig - 3) / 15) ? tp : diag;
                 const uint32_t mm = umin3(V, topv + 1u, diag + __builtin_amdgcn_perm(cv, 0xFFFFFFFEu, selv));
                 const uint32_t vn = mm & ~3u;
                 if (sig < 64) {  // left of the band's checkpoint: hold it, code 3 (outside the window)
-                    const bool hold = sig < sig0;
+                    const bool hold = sig < hold_below;
                     wv = __builtin_amdgcn_alignbit(hold ? 3u : mm, wv, 2);
                     V = hold ? V : vn;
                 } else {
