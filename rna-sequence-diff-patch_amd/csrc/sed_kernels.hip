@@ -156,13 +156,16 @@ template <int R> struct Ladder {
 // for lane 0 (the stripe's top row and str2 symbol): every lane reads the same
 // LDS word, only lane 0 keeps it (the DPP move's `old` operand).  Lane rows are
 // i = (multiple of P) + r + 1, so row r sits on rung Ladder::rung(r + 1).
-template <int R, bool TB, bool LEN, bool COLLECT = true>
+// SELL: the lane's own selector arrives in tv.y (read from the wave's LDS selector ring, see
+// sed_wf_i32_kernel), instead of flowing from lane 0 through a DPP move (one DPP + one copy per step).
+template <int R, bool TB, bool LEN, bool COLLECT = true, bool SELL = false>
 __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                          uint32_t &bottom, uint32_t &selv, const uint2 tv, uint32_t &outc,
                                          uint32_t (&W)[4], const int u) {
     using Lad = Ladder<R>;
     const uint32_t topv = dpp_shr1(tv.x, bottom);  // cell above the band, this column
-    selv = dpp_shr1(tv.y, selv);                   // perm selector of this column's str2 symbol
+    if constexpr (SELL) selv = tv.y;
+    else selv = dpp_shr1(tv.y, selv);  // perm selector of this column's str2 symbol
     uint32_t up = topv, diag = top_prev;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -245,21 +248,24 @@ __device__ __forceinline__ uint32_t i32_sel(uint32_t b) { return 0x0D000100u | (
 
 // CAP: the group that produces the sink cell (captured on its lane); every extra variant is
 // another merge point where the register allocator may insert copies of the whole state.
+// The stripe kernel's group: lane 0's top values from the chunk's LDS slots (ltop, broadcast reads),
+// each lane's str2 selectors from the wave's LDS selector ring at its own column (lsel: this group's
+// first step for this lane, doubled ring so the G reads never wrap).
 template <int R, bool TB, bool LEN, bool CAP, bool CK = false>
 __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
-                                          uint32_t &bottom, uint32_t &selv, const uint2 *__restrict__ lch,
-                                          uint32_t &outc, uint32_t (&W)[4], const int s0, const int lane,
-                                          const int cap_step, const int cap_lane, const int cap_row, uint32_t &cap,
-                                          uint32_t (&rcv)[Grp<R>::G]) {
+                                          uint32_t &bottom, uint32_t &selv, const uint32_t *__restrict__ ltop,
+                                          const uint32_t *__restrict__ lsel, uint32_t &outc, uint32_t (&W)[4],
+                                          const int s0, const int lane, const int cap_step, const int cap_lane,
+                                          const int cap_row, uint32_t &cap, uint32_t (&rcv)[Grp<R>::G]) {
     constexpr int G = Grp<R>::G;
     uint2 tv[G];
-    const uint2 *lp = lch + (s0 & 63);  // G divides 64: a group never wraps the chunk
+    const uint32_t *lp = ltop + (s0 & 63);  // G divides 64: a group never wraps the chunk
 #pragma unroll
-    for (int u = 0; u < G; ++u) tv[u] = lp[u];
+    for (int u = 0; u < G; ++u) tv[u] = make_uint2(lp[u], lsel[u]);
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         const int s = s0 + u;
-        i32_step<R, TB, LEN, !CK>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u);
+        i32_step<R, TB, LEN, !CK, true>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u);
         if constexpr (CK) rcv[u] = V[R - 1];  // the band's bottom row, step s (row checkpoints)
         if constexpr (CAP) {
             const bool hit = (s == cap_step) && (lane == cap_lane);
@@ -273,6 +279,9 @@ __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)
 // the hot loop does not spill (R=16: 96 VGPRs / 5 waves; the 80-VGPR budget of 6 waves spills the
 // cost rows and ran 2.5x slower; R=4/8: 72 / 7; R=32: 128 / 4, which still spills: never chosen).
 template <int R> struct I32Waves { static constexpr int value = R >= 32 ? 4 : (R == 16 ? 5 : 7); };
+#ifndef SED_CK_WAVES
+#define SED_CK_WAVES 5
+#endif
 #ifdef SED_I32_WAVES_PER_EU
 #define SED_I32_WAVES(R) SED_I32_WAVES_PER_EU
 #else
@@ -316,9 +325,11 @@ __device__ __forceinline__ bool wait_progress(const uint32_t *prog, uint32_t epo
 // t = 3 (mod 4) ("row checkpoints", [group][16][4 steps]) -- 0.13 B per cell instead of 0.25.  The CK
 // kernel runs distance keys (LEN = false, 3 VALU per cell instead of the ladder keys' 5.19): they carry
 // (D, L), which is all the checkpoints need; the traceback recomputes the op tie-break.
+// The CK kernel (distance keys, no codes) would fit 80 VGPRs (6 waves per SIMD, spills per chunk only) but
+// ran slower: 12.45 against 12.11 ms at 5 waves (profiles/r02/ab_ck_waves.txt).
 template <int R, bool TB, bool SPLIT, bool LEN = true, bool CK = false>
-__global__ __launch_bounds__(SPLIT ? 64 : 256) __attribute__((amdgpu_waves_per_eu(SED_I32_WAVES(R)))) void
-sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *__restrict__ tasks,
+__global__ __launch_bounds__(SPLIT ? 64 : 256) __attribute__((amdgpu_waves_per_eu(CK ? SED_CK_WAVES : SED_I32_WAVES(R))))
+void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *__restrict__ tasks,
                   uint32_t *__restrict__ prog, const uint32_t *__restrict__ seqa, const uint32_t *__restrict__ seqb,
                   uint32_t *__restrict__ tb, uint32_t *__restrict__ bnd, sed_result *__restrict__ res,
                   sed_i32_params prm) {
@@ -360,9 +371,13 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
     const int cap_lane = wsink / R, cap_row = wsink % R;
     uint32_t cap = 0;
     bool ok = true;
-    // lane 0's inputs of the current 64-step chunk ({top, sel} per step), one slot per wave
-    __shared__ uint2 lds_chunk[SPLIT ? 1 : 4][64];
-    uint2 *lch = lds_chunk[SPLIT ? 0 : (threadIdx.x >> 6)];
+    // per wave: lane 0's top values of the current 64-step chunk, and a ring of str2 selectors by column
+    // (column ci at slots ci & 127 and (ci & 127) + 128; the 64 columns before 0 hold the virtual-column
+    // sentinel), from which lane t reads column s - t at step s
+    __shared__ uint32_t lds_top[SPLIT ? 1 : 4][64];
+    __shared__ uint32_t lds_sel[SPLIT ? 1 : 4][256];
+    uint32_t *lch = lds_top[SPLIT ? 0 : (threadIdx.x >> 6)];
+    uint32_t *ring = lds_sel[SPLIT ? 0 : (threadIdx.x >> 6)];
 
     for (int k = kfirst; k <= klast; ++k) {
         // in-place single buffer per pair when one wave does all stripes; one buffer per stripe otherwise
@@ -403,7 +418,9 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             return i32_sel((pb[ci >> 4] >> ((ci & 15) * 2)) & 3u);
         };
         uint32_t tch = load_top(0), sch = load_sel(0);
-        lch[lane] = make_uint2(tch, sch);
+        lch[lane] = tch;
+        ring[lane] = ring[lane + 128] = sch;
+        ring[lane + 64] = ring[lane + 192] = i32_sent<LEN>();
         uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * 256u;
         // CK: column checkpoints of stripe k at ccb[(chunk * 17 + v) * 64 + lane], row checkpoints at
         // rcb[(group * 16 + lane / 4) * 4 + step % 4] (the layout sed_traceback_ck_kernel reads)
@@ -417,13 +434,14 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
         for (int c = 0; c < nchunks; ++c) {
             uint32_t tnx = 0, snx = 0;
             if (c + 1 < nchunks) { tnx = load_top(c + 1); snx = load_sel(c + 1); }
-            for (int g = 0; g < 64 / G && s < SG; ++g, s += G) {
+            const uint32_t *lsel = ring + ((64 * c - lane) & 127);  // this lane's column at the chunk's first step
+            for (int g = 0; g < 64 / G && s < SG; ++g, s += G, lsel += G) {
                 const bool capg = cap_step >= s && cap_step < s + G;
                 if (capg)
-                    i32_group<R, TB, LEN, true, CK>(V, cv, top_prev, bottom, selv, lch, outc, W, s, lane, cap_step,
-                                                    cap_lane, cap_row, cap, rcv);
+                    i32_group<R, TB, LEN, true, CK>(V, cv, top_prev, bottom, selv, lch, lsel, outc, W, s, lane,
+                                                    cap_step, cap_lane, cap_row, cap, rcv);
                 else
-                    i32_group<R, TB, LEN, false, CK>(V, cv, top_prev, bottom, selv, lch, outc, W, s, lane,
+                    i32_group<R, TB, LEN, false, CK>(V, cv, top_prev, bottom, selv, lch, lsel, outc, W, s, lane,
                                                      cap_step, cap_lane, cap_row, cap, rcv);
                 if constexpr (TB) {
                     uint32_t *gp = tbk + (uint64_t)(s / G) * 256u;  // wave-uniform base, per-lane 16-byte offset
@@ -449,7 +467,9 @@ sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *
             }
             tch = tnx;
             sch = snx;
-            lch[lane] = make_uint2(tch, sch);  // after the chunk's last LDS read (in order)
+            lch[lane] = tch;  // after the chunk's last LDS read (in order)
+            const uint32_t slot = (uint32_t)(64 * (c + 1) + lane) & 127u;  // replaces column 64(c-1) + lane
+            ring[slot] = ring[slot + 128] = sch;
         }
         if (!last) __builtin_amdgcn_s_waitcnt(0);  // own bottom-row stores done before the next stripe reads them
     }
