@@ -397,17 +397,13 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         uint32_t bottom = V[R - 1], selv = i32_sent<LEN>(), outc = 0;
         uint32_t W[4] = {0, 0, 0, 0};
 
-        // CK: the previous stripe's lane 63 stored its bottom row as row checkpoints (column j at step
-        // j + 62, clamped: past SG the columns are beyond m and never read)
-        const uint32_t *rck_prev = tb + d.tb_off + (uint64_t)nstripes * (uint64_t)nchunks * 1088u +
-                                   (uint64_t)(k - 1) * (uint64_t)(SG / G) * 64u + 60u;
+        // CK: the previous stripe's lane 63 stored its bottom row contiguously by step into the pair's
+        // bottom-row buffer (column j at step j + 62, in place: this stripe writes step s while it reads
+        // steps >= s + 64; past SG the columns are beyond m and never read)
         auto load_top = [&](int c) -> uint32_t {
             const int j = 64 * c + lane + 1;
             if (k == 0) return i32_row0<LEN>();
-            if constexpr (CK) {
-                const int st = min(j + 62, SG - 1);
-                return load_sc1(rck_prev + (uint32_t)(st >> 2) * 64u + (uint32_t)(st & 3));
-            }
+            if constexpr (CK) return load_sc1(bnd + d.bnd_off + (uint32_t)(j + 62));
             if constexpr (SPLIT) {  // after one timeout stop waiting: the kernel must still drain quickly
                 if (ok) ok = wait_progress(prog + d.prog_off + k - 1, prm.epoch << 16, (uint32_t)min(m, 64 * c + 64));
             }
@@ -450,6 +446,7 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                 if constexpr (CK) {
                     if ((lane & 3) == 3)
                         store_tb(rcb + (uint64_t)(s / G) * 64u + (uint32_t)(lane >> 2) * 4u, rcv);
+                    if (lane == 63 && !last) store_tb(bnd + d.bnd_off + (uint32_t)s, rcv);  // next stripe's top row
                 }
             }
             if constexpr (CK) {  // column checkpoint: state after the chunk's last step
