@@ -650,3 +650,28 @@ def edit_script_batch(strs1, strs2, userCosts=False):
         v = float(dist[p])
         out.append((int(v) if is_int[p] else v, es))
     return out
+
+
+# ---------------------------------------------------------------------------
+# the reference's import-time demo globals (StringEditDistance.py:459-466), on first access
+# ---------------------------------------------------------------------------
+_DEMO_NAMES = ("dp", "all_paths", "path", "es")
+str1 = 'AGRGA'
+str2 = 'AGGGAA'
+
+
+def __getattr__(name):
+    """PEP 562: the reference builds dp / all_paths / path / es for ('AGRGA', 'AGGGAA', user costs) and prints
+    them when it is imported.  Here importing stays free of GPU work and output; the first access to any of
+    these names computes them the same way (with the user costs loaded at that moment)."""
+    if name in _DEMO_NAMES:
+        g = globals()
+        d = wagnerFisher('AGRGA', 'AGGGAA', True)
+        paths = create_paths(d)
+        last = None
+        for last in paths:  # the reference's loop leaves path / es at the last path
+            pass
+        g["dp"], g["all_paths"], g["path"] = d, paths, last
+        g["es"] = generate_es(last, 'AGRGA', 'AGGGAA')
+        return g[name]
+    raise AttributeError("module %r has no attribute %r" % (__name__, name))

@@ -242,3 +242,17 @@ def test_create_search_threads_process_model(SED):
     manager.shutdown()
     dp = SED.wagnerFisher("ACGU", "AGU")  # the parent's own context still works
     assert dp[len(dp) - 1][len(dp[0]) - 1].value == 1
+
+
+def test_import_time_demo_globals(SED):
+    """StringEditDistance.py:459-466 leaves str1, str2, dp, all_paths, path (the last path) and es (its edit
+    script) as module globals; the drop-in computes them on first access (G1 holds the same case)."""
+    rec = next(r for r in load_golden("g1_small.json") if (r["s1"], r["s2"], r["user"]) == ("AGRGA", "AGGGAA", True))
+    assert (SED.str1, SED.str2) == ("AGRGA", "AGGGAA")
+    v = SED.dp[len(SED.dp) - 1][len(SED.dp[0]) - 1].value
+    assert (float(v), isinstance(v, int)) == (float.fromhex(rec["dist"][0]), rec["dist"][1])
+    assert len(SED.all_paths) == rec["npaths"]
+    ops = "".join("u" if (b.i - a.i, b.j - a.j) == (1, 1) else ("d" if b.i > a.i else "i")
+                  for a, b in zip(SED.path, SED.path[1:]))
+    assert ops == rec["paths"][-1]
+    assert SED.es == SED.generate_es(SED.path, "AGRGA", "AGGGAA")
