@@ -106,10 +106,23 @@ hipError_t sed_launch_lane_i32x2(const sed_launch &L, const int32_t *idx, int nl
 hipError_t sed_launch_lane_f64(const sed_launch &L, const int32_t *idx, int nidx, const double *gtab, double ins,
                                double del, int K);
 hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops);
-// checkpoint layout of the CK forward kernel (R = 16): per stripe nchunks x 17 x 64 column checkpoints, then
-// for all stripes (SG/G) x 64 row checkpoints; word offset of forward lane t's row r at the end of chunk c
-__host__ __device__ inline uint64_t sed_ck_col_word(int stripe, int nchunks, int c, int r, int t) {
-    return ((uint64_t)stripe * (uint64_t)nchunks + (uint64_t)c) * 1088u + (uint64_t)r * 64u + (uint64_t)t;
+// Checkpoint layout of the CK forward kernels (R = 4, 8 or 16 rows per lane, G = 64/R steps per group):
+//   column checkpoints, per stripe [nchunks][R + 1][64 lanes]: each lane's R row values and its top_prev
+//   at every 64-step chunk end;
+//   then row checkpoints, per stripe [SG/G groups][64/G lanes t = G-1 (mod G)][G steps]: the bottom row of
+//   every G-th lane at every step (the row above each 64-row traceback tile).
+__host__ __device__ inline uint64_t sed_ck_col_word(int R, int stripe, int nchunks, int c, int r, int t) {
+    return (((uint64_t)stripe * (uint64_t)nchunks + (uint64_t)c) * (uint64_t)(R + 1) + (uint64_t)r) * 64u +
+           (uint64_t)t;
+}
+__host__ __device__ inline uint64_t sed_ck_col_words(int R, int nstripes, int nchunks) {
+    return (uint64_t)nstripes * (uint64_t)nchunks * (uint64_t)(R + 1) * 64u;
+}
+// row checkpoint of forward lane t (t = G-1 mod G) at step s of stripe k (G = 64/R)
+__host__ __device__ inline uint64_t sed_ck_row_word(int R, int k, int ngroups, int s, int t) {
+    const int G = 64 / R;
+    return ((uint64_t)k * (uint64_t)ngroups + (uint64_t)(s / G)) * 64u + (uint64_t)(t / G) * (uint64_t)G +
+           (uint64_t)(s % G);
 }
 // CK batches (L.ck): the traceback that recomputes tiles from the forward kernel's checkpoints
 hipError_t sed_launch_traceback_ck(const sed_launch &L, uint32_t *ops, const sed_i32_params &prm);

@@ -97,6 +97,11 @@ template <int R> struct Grp { static constexpr int G = 64 / R; };
 __device__ __forceinline__ void store_tb(uint32_t *p, const uint32_t (&w)[4]) {
     *reinterpret_cast<uint4 *>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
+// G (a multiple of 4) consecutive words, 16-byte aligned
+template <int G> __device__ __forceinline__ void store_words(uint32_t *p, const uint32_t (&w)[G]) {
+#pragma unroll
+    for (int k = 0; k < G; k += 4) *reinterpret_cast<uint4 *>(p + k) = make_uint4(w[k], w[k + 1], w[k + 2], w[k + 3]);
+}
 
 // ---------------------------------------------------------------------------
 // Integer (packed-key) kernels.  The reference's decision per cell is the
@@ -158,12 +163,14 @@ template <int R> struct Ladder {
 // i = (multiple of P) + r + 1, so row r sits on rung Ladder::rung(r + 1).
 // SELL: the lane's own selector arrives in tv.y (read from the wave's LDS selector ring, see
 // sed_wf_i32_kernel), instead of flowing from lane 0 through a DPP move (one DPP + one copy per step).
-template <int R, bool TB, bool LEN, bool COLLECT = true, bool SELL = false>
+// TOPC: lane 0's top is the row-0 constant, which its top_prev already holds (single-stripe pairs: the CHAIN
+// kernel), so the DPP move writes over top_prev in place instead of over a copy of tv.x.
+template <int R, bool TB, bool LEN, bool COLLECT = true, bool SELL = false, bool TOPC = false>
 __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                          uint32_t &bottom, uint32_t &selv, const uint2 tv, uint32_t &outc,
                                          uint32_t (&W)[4], const int u) {
     using Lad = Ladder<R>;
-    const uint32_t topv = dpp_shr1(tv.x, bottom);  // cell above the band, this column
+    const uint32_t topv = dpp_shr1(TOPC ? top_prev : tv.x, bottom);  // cell above the band, this column
     if constexpr (SELL) selv = tv.y;
     else selv = dpp_shr1(tv.y, selv);  // perm selector of this column's str2 symbol
     uint32_t up = topv, diag = top_prev;
@@ -319,10 +326,10 @@ __device__ __forceinline__ bool wait_progress(const uint32_t *prog, uint32_t epo
 // SPLIT = true : one wave (one 64-thread workgroup) per stripe, all stripes of
 //                a pair run concurrently, each one 3 chunks (192 steps) behind the
 //                stripe above it (single long pairs: config 2, the GUI).
-// CK (R = 16, not SPLIT): instead of per-cell codes, tb receives checkpoints for the recompute
-// traceback (sed_traceback_ck_kernel): per stripe, at every chunk end each lane's 16 row values and its
-// top_prev ("column checkpoints", [chunk][17][64 lanes]), and every step the bottom row of the lanes
-// t = 3 (mod 4) ("row checkpoints", [group][16][4 steps]) -- 0.13 B per cell instead of 0.25.  The CK
+// CK (not SPLIT): instead of per-cell codes, tb receives checkpoints for the recompute traceback
+// (sed_traceback_ck_kernel; layout in sed_internal.h): per stripe, at every chunk end each lane's R row values
+// and its top_prev ("column checkpoints", [chunk][R+1][64 lanes]), and every step the bottom row of the lanes
+// t = G-1 (mod G) ("row checkpoints", [group][64/G][G steps]) -- ~0.13 B per cell instead of 0.25.  The CK
 // kernel runs distance keys (LEN = false, 3 VALU per cell instead of the ladder keys' 5.19): they carry
 // (D, L), which is all the checkpoints need; the traceback recomputes the op tie-break.
 // The CK kernel (distance keys, no codes) would fit 80 VGPRs (6 waves per SIMD, spills per chunk only) but
@@ -335,7 +342,7 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                   sed_i32_params prm) {
     constexpr int ROWS = 64 * R;
     constexpr int G = Grp<R>::G;
-    static_assert(!CK || (R == 16 && !SPLIT && !TB && !LEN), "checkpoints: R = 16 distance keys, one wave per pair");
+    static_assert(!CK || (R <= 16 && !SPLIT && !TB && !LEN), "checkpoints: R <= 16, distance keys, one wave per pair");
     const int lane = threadIdx.x & 63;
     int pair, kfirst = 0;
     if constexpr (SPLIT) {
@@ -418,11 +425,10 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         ring[lane] = ring[lane + 128] = sch;
         ring[lane + 64] = ring[lane + 192] = i32_sent<LEN>();
         uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * 256u;
-        // CK: column checkpoints of stripe k at ccb[(chunk * 17 + v) * 64 + lane], row checkpoints at
-        // rcb[(group * 16 + lane / 4) * 4 + step % 4] (the layout sed_traceback_ck_kernel reads)
-        uint32_t *ccb = tb + d.tb_off + (uint64_t)k * (uint64_t)nchunks * 1088u;
-        uint32_t *rcb = tb + d.tb_off + (uint64_t)nstripes * (uint64_t)nchunks * 1088u +
-                        (uint64_t)k * (uint64_t)(SG / G) * 64u;
+        // CK: column checkpoints of stripe k at ccb[(chunk * (R+1) + v) * 64 + lane], row checkpoints at
+        // rcb[group * 64 + (lane / G) * G + step % G] (sed_ck_*_word, the layout sed_traceback_ck_kernel reads)
+        uint32_t *ccb = tb + d.tb_off + sed_ck_col_word(R, k, nchunks, 0, 0, 0);
+        uint32_t *rcb = tb + d.tb_off + sed_ck_col_words(R, nstripes, nchunks) + (uint64_t)k * (uint64_t)(SG / G) * 64u;
         uint32_t rcv[G];
         const bool last = (k == nstripes - 1);
         const int cap_step = last ? m - 1 + cap_lane : -1;
@@ -444,16 +450,15 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                     store_tb(gp + lane * 4, W);
                 }
                 if constexpr (CK) {
-                    if ((lane & 3) == 3)
-                        store_tb(rcb + (uint64_t)(s / G) * 64u + (uint32_t)(lane >> 2) * 4u, rcv);
-                    if (lane == 63 && !last) store_tb(bnd + d.bnd_off + (uint32_t)s, rcv);  // next stripe's top row
+                    if ((lane & (G - 1)) == G - 1) store_words<G>(rcb + (uint64_t)(s / G) * 64u + (uint32_t)(lane / G) * G, rcv);
+                    if (lane == 63 && !last) store_words<G>(bnd + d.bnd_off + (uint32_t)s, rcv);  // next stripe's top row
                 }
             }
             if constexpr (CK) {  // column checkpoint: state after the chunk's last step
-                uint32_t *cp = ccb + (uint64_t)c * 1088u + lane;
+                uint32_t *cp = ccb + (uint64_t)c * (uint64_t)(R + 1) * 64u + lane;
 #pragma unroll
                 for (int r = 0; r < R; ++r) cp[r * 64] = V[r];
-                cp[16 * 64] = top_prev;
+                cp[R * 64] = top_prev;
             }
             // lane i holds lane 63's bottom cell of step s-64+i, i.e. column s-126+i at bnd index col+64
             if (!CK && !last) {
@@ -652,6 +657,7 @@ struct chain_pair_state {
     int cap_step, cap_lane, cap_row;   // the sink cell (n, m)
     uint64_t tb_off;
     int sg;                            // traceback groups allocated per stripe
+    int nchunks;                       // CK: 64-step chunks of the pair's stripe (column checkpoints)
     const uint32_t *pb;                // str2 codes
 };
 
@@ -673,6 +679,7 @@ __device__ __forceinline__ chain_pair_state chain_load(const sed_pair_desc *__re
     c.cap_step = T + d.m - 1 + c.cap_lane;
     c.tb_off = d.tb_off;
     c.sg = (d.m + 63 + G - 1) / G;
+    c.nchunks = (c.sg * G + 63) >> 6;
     c.pb = seqb + d.b_off;
     return c;
 }
@@ -680,23 +687,26 @@ __device__ __forceinline__ chain_pair_state chain_load(const sed_pair_desc *__re
 // One group of G steps.  SW: lanes switch from the previous pair to the pair starting at
 // `Tcur` after the step at which lane == s + 1 - Tcur.  GEN (rare groups: sink captures of the
 // previous (A) and current (B) pair, and any switch in those groups) additionally captures.
-template <int R, bool TB, bool LEN, bool SW, bool GEN>
+// Lane 0's top value is row 0 (single-stripe pairs); every lane reads its str2 selector from the wave's
+// selector ring by global column s - t (lsel: this lane's column at the group's first step), which always
+// belongs to the pair the lane is working on: lane t is on the pair starting at T exactly when s - t >= T.
+template <int R, bool TB, bool LEN, bool SW, bool GEN, bool CK>
 __device__ __forceinline__ void i32_chain_group(uint32_t (&V)[R], uint32_t (&cv)[R], const uint32_t (&cvn)[R],
                                                 const uint32_t (&Vb)[R], const uint32_t tpb, uint32_t &top_prev,
-                                                uint32_t &bottom, uint32_t &selv, const uint2 *__restrict__ lch,
+                                                uint32_t &bottom, uint32_t &selv, const uint32_t *__restrict__ lsel,
                                                 uint32_t &outc, uint32_t (&W)[4], const int s0, const int lane,
                                                 const int Tcur, const int csA, const int clA, const int crA,
                                                 uint32_t &capA, const int csB, const int clB, const int crB,
-                                                uint32_t &capB) {
+                                                uint32_t &capB, uint32_t (&rcv)[Grp<R>::G]) {
     constexpr int G = Grp<R>::G;
     uint2 tv[G];
-    const uint2 *lp = lch + (s0 & 63);
 #pragma unroll
-    for (int u = 0; u < G; ++u) tv[u] = lp[u];
+    for (int u = 0; u < G; ++u) tv[u] = make_uint2(i32_row0<LEN>(), lsel[u]);
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         const int s = s0 + u;
-        i32_step<R, TB, LEN>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u);
+        i32_step<R, TB, LEN, false, true, true>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u);
+        if constexpr (CK) rcv[u] = V[R - 1];  // the band's bottom row (row checkpoints), before any switch
         if constexpr (GEN) {
             const bool hA = (s == csA) && (lane == clA), hB = (s == csB) && (lane == clB);
 #pragma unroll
@@ -717,10 +727,10 @@ __device__ __forceinline__ void i32_chain_group(uint32_t (&V)[R], uint32_t (&cv)
     }
 }
 
-template <int R, bool TB, bool LEN>
+template <int R, bool TB, bool LEN, bool CK>
 __device__ __forceinline__ void chain_store_result(sed_result *__restrict__ res, int pair, uint32_t cap, int n,
                                                    int m, int seq, const sed_i32_params &prm) {
-    const int2 dl = i32_decode<R, LEN>(cap, n, m, prm);
+    const int2 dl = i32_decode<R, LEN, CK>(cap, n, m, prm);
     res[pair].dist = (double)dl.x;
     res[pair].len = dl.y;
     res[pair].is_int = (dl.x == 0);
@@ -731,13 +741,17 @@ __device__ __forceinline__ void chain_store_result(sed_result *__restrict__ res,
 // the chain kernel also holds the next pair's cost rows and the column-0 constants
 template <int R> struct ChainWaves { static constexpr int value = R >= 16 ? 4 : 5; };
 
-template <int R, bool TB, bool LEN>
+// CK: distance keys, and checkpoints instead of codes (the stripe kernel's layout, one stripe per pair).  At every
+// chunk end all lanes are on the pair lane 0 is on (a lane switches at most 63 steps after lane 0), so the column
+// checkpoints go to that pair; a row-checkpoint group of a switch window goes to both pairs, like the codes.
+template <int R, bool TB, bool LEN, bool CK = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainWaves<R>::value))) void
 sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restrict__ chain_pairs,
                         const int32_t *__restrict__ chain_off, int nchains, uint32_t *__restrict__ counter,
                         int nlist, const uint32_t *__restrict__ seqa, const uint32_t *__restrict__ seqb,
                         uint32_t *__restrict__ tb, sed_result *__restrict__ res, sed_i32_params prm) {
     constexpr int G = Grp<R>::G;
+    static_assert(!CK || (!TB && !LEN), "checkpoints: distance keys, no codes");
     const int lane = threadIdx.x & 63;
     const int chain = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (chain >= nchains) return;
@@ -758,8 +772,10 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
         c0 = chain_off[chain];
         c1 = chain_off[chain + 1];
     }
-    __shared__ uint2 lds_chunk[4][64];
-    uint2 *lch = lds_chunk[threadIdx.x >> 6];
+    // per wave: str2 selectors by global column (column g at slots g & 127 and (g & 127) + 128; the 64 columns
+    // before the chain's first pair hold the virtual-column sentinel)
+    __shared__ uint32_t lds_sel[4][256];
+    uint32_t *ring = lds_sel[threadIdx.x >> 6];
     const int row0 = lane * R;
 
     // per-lane constants: column-0 state of this lane's rows (the same for every pair)
@@ -793,7 +809,9 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
     }
     uint32_t top_prev = tpb, bottom = V[R - 1], selv = i32_sent<LEN>(), outc = 0, capA = 0, capB = 0;
     uint32_t W[4] = {0, 0, 0, 0};
-    lch[lane] = chunk_of(cur, 0);
+    uint32_t rcv[G];
+    ring[lane] = ring[lane + 128] = chunk_of(cur, 0).y;
+    ring[lane + 64] = ring[lane + 192] = i32_sent<LEN>();
 
     for (int s0 = 0;; s0 += 64) {
         // prefetch the next chunk's lane-0 inputs (this pair's next chunk, or the next pair's first)
@@ -811,17 +829,19 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
                 q = qn - 1;  // advanced below when nxt becomes cur
             }
         }
+        const uint32_t *lsel0 = ring + ((s0 - lane) & 127);  // this lane's global column at the chunk's first step
         for (int g = 0; g < 64 / G; ++g) {
             const int s = s0 + g * G;
+            const uint32_t *lsel = lsel0 + g * G;
             const bool win = have_cur && have_prv && s < cur.T + 64;  // lanes switch from prv to cur
             const bool capg = (have_prv && prv.cap_step >= s && prv.cap_step < s + G) ||
                               (have_cur && cur.cap_step >= s && cur.cap_step < s + G);
             // wave-uniform: which body; Tsw never matches a lane outside a switch window
             const int Tsw = win ? cur.T : -(1 << 30);
 #define SED_CGROUP(SW, GEN)                                                                               \
-    i32_chain_group<R, TB, LEN, SW, GEN>(V, cv, cvn, Vb, tpb, top_prev, bottom, selv, lch, outc, W, s, lane, Tsw, \
-                                         prv.cap_step, prv.cap_lane, prv.cap_row, capA, cur.cap_step,             \
-                                         cur.cap_lane, cur.cap_row, capB)
+    i32_chain_group<R, TB, LEN, SW, GEN, CK>(V, cv, cvn, Vb, tpb, top_prev, bottom, selv, lsel, outc, W, s, lane, \
+                                             Tsw, prv.cap_step, prv.cap_lane, prv.cap_row, capA, cur.cap_step,    \
+                                             cur.cap_lane, cur.cap_row, capB, rcv)
             if (capg) SED_CGROUP(false, true);
             else if (win) SED_CGROUP(true, false);
             else SED_CGROUP(false, false);
@@ -842,14 +862,39 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
                     *reinterpret_cast<uint4 *>(gp + lo) = make_uint4(W[0], W[1], W[2], W[3]);
                 }
             }
+            if constexpr (CK) {  // row checkpoints of lanes t = G-1 (mod G), to the pair(s) the group's steps belong to
+                if ((lane & (G - 1)) == G - 1) {
+                    const uint32_t lo = (uint32_t)(lane / G) * G;
+                    if (have_cur && s >= cur.T)
+                        store_words<G>(tb + cur.tb_off + sed_ck_col_words(R, 1, cur.nchunks) +
+                                           (uint64_t)((s - cur.T) / G) * 64u + lo, rcv);
+                    if (have_prv && s < (have_cur ? cur.T + 64 : prv.end) && (s - prv.T) / G < prv.sg)
+                        store_words<G>(tb + prv.tb_off + sed_ck_col_words(R, 1, prv.nchunks) +
+                                           (uint64_t)((s - prv.T) / G) * 64u + lo, rcv);
+                }
+            }
             if (capg) {
                 if (have_prv && prv.cap_step >= s && prv.cap_step < s + G && lane == prv.cap_lane)
-                    chain_store_result<R, TB, LEN>(res, prv.pair, capA, prv.n, prv.m, ord_prv, prm);
+                    chain_store_result<R, TB, LEN, CK>(res, prv.pair, capA, prv.n, prv.m, ord_prv, prm);
                 if (have_cur && cur.cap_step >= s && cur.cap_step < s + G && lane == cur.cap_lane)
-                    chain_store_result<R, TB, LEN>(res, cur.pair, capB, cur.n, cur.m, ord, prm);
+                    chain_store_result<R, TB, LEN, CK>(res, cur.pair, capB, cur.n, cur.m, ord, prm);
             }
         }
-        lch[lane] = nx;  // after the chunk's last LDS read (in order)
+        if constexpr (CK) {  // column checkpoint of cur's local chunk: every lane is on cur at a chunk end
+            if (have_cur) {
+                const int lc = (s0 - cur.T) >> 6;
+                if (lc < cur.nchunks) {
+                    uint32_t *cp = tb + cur.tb_off + sed_ck_col_word(R, 0, cur.nchunks, lc, 0, lane);
+#pragma unroll
+                    for (int r = 0; r < R; ++r) cp[r * 64] = V[r];
+                    cp[R * 64] = top_prev;
+                }
+            }
+        }
+        {  // global columns s0 + 64 .. s0 + 127, after the chunk's last LDS read (in order)
+            const uint32_t slot = (uint32_t)(s0 + 64 + lane) & 127u;
+            ring[slot] = ring[slot + 128] = nx.y;
+        }
         const int s1 = s0 + 64;
         if (have_cur && s1 == cur.T + cur.S) {  // lane 0 is done with cur: it becomes the draining pair
             prv = cur;
@@ -1306,21 +1351,22 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
 }
 
 // ---------------------------------------------------------------------------
-// Traceback from checkpoints (CK, the R = 16 wave kernel's script batches).  One wave per pair walks
-// the canonical path back from (n, m) tile by tile.  A tile is 64 rows (forward lanes 4Q .. 4Q+3 of a
-// stripe) x the 64 columns those lanes processed in one chunk c, a staircase: band t = 4Q + b covers
-// columns 64c - t + 1 .. 64c - t + 64.  Entering a tile, the wave recomputes it from
-//   - the column checkpoints of chunk c-1 (each band's 16 row values at column 64c - t, and the value
+// Traceback from checkpoints (CK: script batches of the stripe and CHAIN kernels with R = 4, 8 or 16 rows
+// per lane, G = 64/R).  One wave per pair walks the canonical path back from (n, m) tile by tile.  A tile
+// is 64 rows (forward lanes GQ .. GQ+G-1 of a stripe, the tile's G bands of R rows) x the 64 columns those
+// lanes processed in one chunk c, a staircase: band t = GQ + b covers columns 64c - t + 1 .. 64c - t + 64.
+// Entering a tile, the wave recomputes it from
+//   - the column checkpoints of chunk c-1 (each band's R row values at column 64c - t, and the value
 //     above the band at that column), or the column-0 borders for c = 0;
-//   - the row above the tile: the row checkpoints of lane 4Q-1 (or lane 63 of the stripe above, or
+//   - the row above the tile: the row checkpoints of lane GQ-1 (or lane 63 of the stripe above, or
 //     row 0), read through LDS by lane 0;
-// with one lane per row (row r at sweep step sigma is at column J0 - 3 + sigma - r, J0 = 64c - 4Q + 1; the
-// cell above arrives through the DPP chain from lane r - 1, the str2 selector from LDS).  The forward kernel
+// with one lane per row (row r at sweep step sigma is at column J0 - (G-1) + sigma - r, J0 = 64c - GQ + 1;
+// the cell above arrives through the DPP chain from lane r - 1, the str2 selector from LDS).  The forward kernel
 // stores distance keys (D, L without the op); every checkpoint value is converted on load to the
 // traceback key of the same (D, L) (i32_dist_to_tb), whose min carries the canonical op in its low two
 // bits: 6 VALU per cell (perm, 2 adds, min3, and, alignbit).  Lanes of band b hold their checkpoint
-// until their first column (step r - b + 3) and store code 3 there (outside the band's window); the
-// first row of bands 1..3 takes its first diagonal from the checkpoint; columns < 1 get the sentinel
+// until their first column (step r - b + G - 1) and store code 3 there (outside the band's window); the
+// first row of bands 1..G-1 takes its first diagonal from the checkpoint; columns < 1 get the sentinel
 // selector, so they keep the column-0 border.  The sweep stops after the 16-step word holding the
 // entry cell's step (the path only goes up and left), and the entry cell's key must carry the path
 // length still to emit: a mismatch (a corrupted checkpoint, SED_OPT_DEBUG_CORRUPT) sets res.err
@@ -1361,13 +1407,25 @@ __device__ __forceinline__ uint32_t ck_walk(const uint32_t (&W)[8], uint32_t S, 
     return S;
 }
 
+// band b >= 1 of a tile starts (its first row takes the checkpoint's top_prev as diagonal) at sweep step
+// (R - 1) b + G - 1; returns b, or 0 when `sig` starts no band
+template <int R> constexpr int ck_band_start(int sig) {
+    constexpr int G = 64 / R;
+    for (int b = 1; b < G; ++b)
+        if (sig == (R - 1) * b + G - 1) return b;
+    return 0;
+}
+
+template <int R>
 __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
                                                               const uint32_t *__restrict__ seqa,
                                                               const uint32_t *__restrict__ seqb,
                                                               const uint32_t *__restrict__ ck,
                                                               sed_result *__restrict__ res,
                                                               uint32_t *__restrict__ ops, sed_i32_params prm) {
-    constexpr int R = 16, ROWS = 64 * R, G = Grp<R>::G;
+    constexpr int ROWS = 64 * R, G = Grp<R>::G;  // a tile: G forward lanes (bands) of R rows
+    constexpr int LR = R == 4 ? 2 : R == 8 ? 3 : 4;
+    static_assert((1 << LR) == R, "R in {4, 8, 16}");
     const int lane = threadIdx.x;
     const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x);
     if (pair >= npairs) return;
@@ -1394,54 +1452,50 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
         const int nstripes = (n + ROWS - 1) / ROWS;
         const int SG = (m + 63 + G - 1) / G * G, nchunks = (SG + 63) >> 6, ngroups = SG / G;
         const uint32_t *ccp = ck + d.tb_off;
-        const uint32_t *rcp = ccp + (uint64_t)nstripes * (uint64_t)nchunks * 1088u;
+        const uint32_t *rcp = ccp + sed_ck_col_words(R, nstripes, nchunks);
         const uint32_t *pa = seqa + d.a_off, *pb = seqb + d.b_off;
-        const int band = lane >> 4;
-        const int sig0 = lane - band + 3;  // first real sweep step of this lane (<= 63)
+        const int band = lane >> LR;
+        const int sig0 = lane - band + G - 1;  // first real sweep step of this lane (<= 63)
         int guard = 2 * (n + m) + 8;       // tiles visited; every visit makes progress
         while (i > 0 && j > 0) {
             if (--guard <= 0) {
                 err = SED_ERR_TB_GUARD;
                 break;
             }
-            const int k = (i - 1) / ROWS, t = ((i - 1) % ROWS) / R, Q = t >> 2;
+            const int k = (i - 1) / ROWS, t = ((i - 1) % ROWS) / R, Q = t / G;
             const int c = (j - 1 + t) >> 6;
-            const int J0 = 64 * c - 4 * Q + 1, rowbase = k * ROWS + 64 * Q;
-            const int re = i - rowbase - 1;         // the entry cell's tile row
-            const int sig_end = (j - J0 + 3) + re;  // the entry cell's sweep step (<= 126)
+            const int J0 = 64 * c - G * Q + 1, rowbase = k * ROWS + 64 * Q;
+            const int re = i - rowbase - 1;             // the entry cell's tile row
+            const int sig_end = (j - J0 + G - 1) + re;  // the entry cell's sweep step (<= 126)
             // ---- boundaries (distance keys -> traceback keys) ----
             const int ir = min(rowbase + lane, n - 1);  // 0-based str1 index of this lane's row (clamped)
             const uint32_t a = (pa[ir >> 4] >> ((ir & 15) * 2)) & 3u;
             const uint32_t cv = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
             uint32_t V = SED_KB, tp = SED_KB;  // c = 0: the column-0 borders
             if (c >= 1) {
-                const uint32_t *cp = ccp + sed_ck_col_word(k, nchunks, c - 1, lane & 15, 4 * Q + band);
+                const uint32_t *cp = ccp + sed_ck_col_word(R, k, nchunks, c - 1, lane & (R - 1), G * Q + band);
                 V = i32_dist_to_tb(cp[0]);
-                tp = i32_dist_to_tb(cp[(16 - (lane & 15)) * 64]);
+                tp = i32_dist_to_tb(cp[(R - (lane & (R - 1))) * 64]);
             }
             for (int x = lane; x < 132; x += 64) {
-                // the row above the tile at column J0 - 4 + x: row checkpoints (steps clamped: past SG
-                // the columns are beyond m and never read by the walk; before step 0 the border)
+                // the row above the tile at column J0 - G + x: row checkpoints of forward lane G*Q - 1 (or lane 63
+                // of the stripe above); steps clamped: past SG the columns are beyond m and never read by the
+                // walk; before step 0 the border
+                // (columns < 1 are the column-0 border: a CHAIN wave's lanes still hold the previous pair there)
                 uint32_t v = SED_KB;
-                if (Q >= 1) {
-                    const int st = 64 * c - 5 + x;
-                    if (st >= 0) {
-                        const int sc = min(st, SG - 1);
-                        v = i32_dist_to_tb(rcp[((uint64_t)k * (uint64_t)ngroups + (uint64_t)(sc >> 2)) * 64u +
-                                               (uint32_t)(Q - 1) * 4u + (uint32_t)(sc & 3)]);
-                    }
-                } else if (k >= 1) {
-                    const int sc = min(64 * c + 59 + x, SG - 1);
-                    v = i32_dist_to_tb(rcp[((uint64_t)(k - 1) * (uint64_t)ngroups + (uint64_t)(sc >> 2)) * 64u + 60u +
-                                           (uint32_t)(sc & 3)]);
+                if (J0 - G + x >= 1) {
+                    if (Q >= 1)
+                        v = i32_dist_to_tb(rcp[sed_ck_row_word(R, k, ngroups, min(64 * c - G - 1 + x, SG - 1), G * Q - 1)]);
+                    else if (k >= 1)
+                        v = i32_dist_to_tb(rcp[sed_ck_row_word(R, k - 1, ngroups, min(64 * c + 63 - G + x, SG - 1), 63)]);
                 }
                 topb[x] = v;
-                const int col = J0 - 3 + x;  // column of lane 0 at step x
+                const int col = J0 - (G - 1) + x;  // column of lane 0 at step x
                 const int ci = min(max(col - 1, 0), m - 1);
                 selb[64 + x] = col < 1 ? SED_SEL_SENT : i32_sel((pb[ci >> 4] >> ((ci & 15) * 2)) & 3u);
             }
             __syncthreads();
-            // ---- sweep: lane r at step sigma computes (row rowbase + r + 1, column J0 - 3 + sigma - r) ----
+            // ---- sweep: lane r at step sigma computes (row rowbase + r + 1, column J0 - (G-1) + sigma - r) ----
             // Whole 16-step words (a branch per step would keep the LDS reads from running ahead); the block
             // holding the entry step also captures each lane's key at that step.
             uint32_t W[8];
@@ -1457,7 +1511,8 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
                 const uint32_t topv = dpp_shr1(topb[sig + 1], V);
                 const uint32_t selv = selp[sig];  // steps before the lane's first column read don't-care
                 uint32_t diag = tprev;
-                if (sig == 18 || sig == 33 || sig == 48) diag = lane == 16 * ((sig - 3) / 15) ? tp : diag;
+                const int bs = ck_band_start<R>(sig);  // folds to a constant in the unrolled sweep
+                if (bs > 0) diag = lane == R * bs ? tp : diag;
                 const uint32_t mm = umin3(V, topv + 1u, diag + __builtin_amdgcn_perm(cv, 0xFFFFFFFEu, selv));
                 const uint32_t vn = mm & ~3u;
                 if (sig < 64) {  // left of the band's checkpoint: hold it, code 3 (outside the window)
@@ -1503,7 +1558,7 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
             }
             const int sg = (int)((S + 64u) >> 7), r = (int)((S + 64u) & 127u) - 64;
             i = rowbase + r + 1;
-            j = J0 - 3 + sg - r;
+            j = J0 - (G - 1) + sg - r;
             __syncthreads();  // topb / selb are rewritten for the next tile
         }
     }
@@ -1555,9 +1610,9 @@ static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
     return hipGetLastError();
 }
 
-template <int R, bool TB, bool LEN>
+template <int R, bool TB, bool LEN, bool CK = false>
 static hipError_t launch_chain_R(const sed_launch &L, const sed_i32_params &prm) {
-    hipLaunchKernelGGL((sed_wf_i32_chain_kernel<R, TB, LEN>), dim3((L.nchains + 3) / 4), dim3(256), 0, L.stream, L.pd,
+    hipLaunchKernelGGL((sed_wf_i32_chain_kernel<R, TB, LEN, CK>), dim3((L.nchains + 3) / 4), dim3(256), 0, L.stream, L.pd,
                        L.chain_pairs, L.chain_off, L.nchains, L.chain_counter, L.chain_list,
                        (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.res, prm);
     return hipGetLastError();
@@ -1565,6 +1620,14 @@ static hipError_t launch_chain_R(const sed_launch &L, const sed_i32_params &prm)
 
 hipError_t sed_launch_i32_chain(const sed_launch &L, const sed_i32_params &prm, bool len) {
     const bool tb = L.tb != nullptr;
+    if (tb && L.ck) {  // distance keys + checkpoints
+        switch (L.R) {
+        case 4: return launch_chain_R<4, false, false, true>(L, prm);
+        case 8: return launch_chain_R<8, false, false, true>(L, prm);
+        case 16: return launch_chain_R<16, false, false, true>(L, prm);
+        default: return hipErrorInvalidValue;
+        }
+    }
     switch (L.R) {
 #define CASE(RR)                                                                                   \
     case RR:                                                                                       \
@@ -1592,9 +1655,14 @@ hipError_t sed_launch_i32x2(const sed_launch &L, const int32_t *list, int nwaves
 
 hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm, bool len) {
     const bool tb = L.tb != nullptr;
-    if (tb && L.ck) {
-        if (L.R != 16 || L.ntasks > 0) return hipErrorInvalidValue;
-        return launch_i32_R<16, false, false, true>(L, prm);  // distance keys + checkpoints
+    if (tb && L.ck) {  // distance keys + checkpoints
+        if (L.ntasks > 0) return hipErrorInvalidValue;
+        switch (L.R) {
+        case 4: return launch_i32_R<4, false, false, true>(L, prm);
+        case 8: return launch_i32_R<8, false, false, true>(L, prm);
+        case 16: return launch_i32_R<16, false, false, true>(L, prm);
+        default: return hipErrorInvalidValue;
+        }
     }
     switch (L.R) {
 #define CASE(RR)                                                                                     \
@@ -1638,8 +1706,14 @@ hipError_t sed_launch_f64(const sed_launch &L, const double *gtab, const sed_f64
 }
 
 hipError_t sed_launch_traceback_ck(const sed_launch &L, uint32_t *ops, const sed_i32_params &prm) {
-    hipLaunchKernelGGL(sed_traceback_ck_kernel, dim3(L.npairs), dim3(64), 0, L.stream, L.pd, L.npairs,
-                       (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.res, ops, prm);
+    const dim3 grid(L.npairs), block(64);
+    const uint32_t *a = (const uint32_t *)L.seqa, *b = (const uint32_t *)L.seqb;
+    switch (L.R) {
+    case 4: hipLaunchKernelGGL(sed_traceback_ck_kernel<4>, grid, block, 0, L.stream, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
+    case 8: hipLaunchKernelGGL(sed_traceback_ck_kernel<8>, grid, block, 0, L.stream, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
+    case 16: hipLaunchKernelGGL(sed_traceback_ck_kernel<16>, grid, block, 0, L.stream, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -271,10 +271,18 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     b->R = R;
     const int ROWS = 64 * R;
     const bool want_tb = (flags & SED_WANT_SCRIPT) != 0;
-    // CK traceback (R = 16 wave kernel, not SPLIT; CHAIN mode needs R <= 8): checkpoints + recompute,
-    // by default for batches past the window kernel's 256 pairs
-    b->ck = want_tb && mode == SED_MODE_I32 && !split && R == 16 && c->opt_tb != 1 &&
-            (c->opt_tb == 2 || npairs > 256);
+    // CK traceback (R = 4/8/16 wave kernels, stripe or CHAIN, not SPLIT): distance-key forward kernel +
+    // checkpoints, traceback recomputes tiles.  Auto: batches past the window kernel's 256 pairs whose pairs
+    // are large enough.  The forward kernel saves ~1.7 VALU per cell (n m), the tile recompute costs per
+    // path step (n + m): measured, config 4 (4096^2) step 20.4 -> 15.0 ms, config 3 (512^2) 2.90 -> 4.40 ms;
+    // break-even near 1024^2, i.e. sum(n m) / sum(n + m) = 512.
+    double sum_nm = 0, sum_len = 0;
+    for (int p = 0; p < npairs; ++p) {
+        sum_nm += (double)len_a[p] * len_b[p];
+        sum_len += (double)len_a[p] + len_b[p];
+    }
+    b->ck = want_tb && mode == SED_MODE_I32 && !split && (R == 4 || R == 8 || R == 16) && c->opt_tb != 1 &&
+            (c->opt_tb == 2 || (npairs > 256 && sum_nm >= 512.0 * sum_len));
     // SED_PIPELINE is a hint: checkpoint batches run their traceback after the DP on one stream.  Both
     // kernels are issue-bound, so overlap only adds contention (config 4: 20.33 ms sequential against
     // 20.5-20.8 ms pipelined, profiles/r01_ck/ab_pipeline.jsonl) and saves two traceback buffers.
@@ -318,8 +326,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
             const uint64_t nstripes = (nn + ROWS - 1) / ROWS;
             const uint64_t SG = (mm + 63 + G - 1) / G * G;
             const uint64_t nchunks = (SG + 63) / 64;
-            if (want_tb) {  // CK: per stripe nchunks x 17 x 64 column checkpoints + (SG/G) x 64 row checkpoints
-                const uint64_t w = b->ck ? nstripes * (nchunks * 17 * 64 + (SG / G) * 64) : nstripes * (SG / G) * 64 * 4;
+            if (want_tb) {  // CK: per stripe nchunks x (R+1) x 64 column checkpoints + (SG/G) x 64 row checkpoints
+                const uint64_t w = b->ck ? nstripes * (nchunks * (R + 1) * 64 + (SG / G) * 64) : nstripes * (SG / G) * 64 * 4;
                 tbw += w;
                 ck_bytes += 4.0 * (double)w;
             }
@@ -628,12 +636,12 @@ int run_batch(sed_batch *b) {
         // spreads to the sink (test of the traceback's error path: the pair must come back SED_E_DEVICE)
         const int p = c->opt_debug_corrupt - 1;
         const sed_pair_desc &d = b->pd[p];
-        const int ROWS = 16 * 64, G = 4;
+        const int R = b->R, ROWS = R * 64, G = 64 / R;
         if (!d.lane && d.n > 0 && d.m > 0) {
             const int nstripes = (d.n + ROWS - 1) / ROWS, SG = (d.m + 63 + G - 1) / G * G, nchunks = (SG + 63) >> 6;
-            const int t = ((d.n - 1) % ROWS) / 16, r = (d.n - 1) % 16, cs = (d.m - 1 + t) >> 6;
+            const int t = ((d.n - 1) % ROWS) / R, r = (d.n - 1) % R, cs = (d.m - 1 + t) >> 6;
             if (cs >= 1) {
-                uint32_t *w = (uint32_t *)b->d_tb[k].p + d.tb_off + sed_ck_col_word(nstripes - 1, nchunks, cs - 1, r, t);
+                uint32_t *w = (uint32_t *)b->d_tb[k].p + d.tb_off + sed_ck_col_word(R, nstripes - 1, nchunks, cs - 1, r, t);
                 if ((e = hipMemsetD32Async((hipDeviceptr_t)w, 0x0000FFFCu, 1, c->stream)) != hipSuccess)
                     return c->hipfail(e, "debug corrupt");
             }

@@ -493,3 +493,45 @@ def test_g8_tables_random_batches_vs_oracle(gpu, name):
     _oracle_check(table, pairs, gpu_run(gpu, table, pairs, script=False))
     _oracle_check(table, pairs, gpu_run(gpu, table, pairs, script=False, no_len=True), no_len=True)
     _oracle_check(table, pairs, gpu_run(gpu, table, pairs, mode=3))
+
+
+@pytest.mark.parametrize("R", [4, 8, 16])
+@pytest.mark.parametrize("chain", [1, 2])
+def test_checkpoint_route_every_R_stripe_and_chain(gpu, tables, R, chain):
+    """Checkpoints (SED_OPT_TB = 2) at R = 4/8/16 rows per lane: tiles of 64/R bands of R rows.  Stripe kernel
+    (chain off) on ragged multi-stripe pairs, CHAIN kernel (forced, static chains of 5 and dynamic; CHAIN runs
+    at R = 4/8 only, R = 16 stays on the stripe kernel) on ragged single-stripe pairs, lane route off so short
+    str2 chain too; scripts equal the oracle's and the per-cell codes'."""
+    rng = np.random.default_rng(1700 + R + chain)
+    rows = 64 * R
+    pairs = []
+    for _ in range(90):
+        n = int(rng.choice([rng.integers(1, rows + 1), rows, 1]) if chain == 1 else rng.integers(1, 3 * rows + 70))
+        m = int(rng.choice([rng.integers(1, 700), 63, 64, 65, 128, 1, 2, 33]))
+        a = "".join(rng.choice(list("ACGU"), size=n))
+        if rng.random() < 0.5:
+            b = "".join(c if rng.random() > 0.12 else rng.choice(list("ACGU")) for c in (a * 3)[:m])
+        else:
+            b = "".join(rng.choice(list("ACGU"), size=m))
+        pairs.append((a, b))
+    for user in (False, True):
+        for ch in ([1, 5] if chain == 1 else [2]):
+            got = gpu_run(gpu, tables[user], pairs, R=R, split=2, lane=2, chain=ch, tb=2)
+            _oracle_check(tables[user], pairs, got)
+            assert got == gpu_run(gpu, tables[user], pairs, R=R, split=2, lane=2, chain=ch, tb=1)
+    plan = sedcost.build_plan(tables[True], [a for a, _ in pairs], [b for _, b in pairs])
+    gpu.set_costs(plan)
+    gpu.set_option(sedgpu.SED_OPT_TB, 2)
+    gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, R)
+    gpu.set_option(sedgpu.SED_OPT_CHAIN, chain)
+    gpu.set_option(sedgpu.SED_OPT_LANE, 2)
+    gpu.set_option(sedgpu.SED_OPT_SPLIT, 2)  # a batch this small would otherwise run SPLIT (codes)
+    try:
+        b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(x) for x, _ in pairs], [plan.encode(y) for _, y in pairs]),
+                         True)
+        assert b.traceback_mode == 2 and b.rows_per_lane == R and (b.chains > 0) == (chain == 1 and R < 16)
+        b.close()
+    finally:
+        for k in (sedgpu.SED_OPT_TB, sedgpu.SED_OPT_ROWS_PER_LANE, sedgpu.SED_OPT_CHAIN, sedgpu.SED_OPT_LANE,
+                  sedgpu.SED_OPT_SPLIT):
+            gpu.set_option(k, 0)

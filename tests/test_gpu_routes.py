@@ -75,12 +75,18 @@ def test_dynamic_chain_config3_route(gpu, tables, user):
     plan = _plan(tables[user])
     gpu.set_costs(plan)
     packed = sedgpu.PackedPairs(A, B)
-    for script, no_len in ((True, False), (False, False), (False, True)):
-        b, (d, ii, ln, ops) = _batch_run(gpu, packed, script, no_len=no_len)
+    # scripts on the automatic route (per-cell codes at this size) and forced onto checkpoints (SED_OPT_TB = 2)
+    for script, no_len, tb in ((True, False, 0), (True, False, 2), (False, False, 0), (False, True, 0)):
+        gpu.set_option(sedgpu.SED_OPT_TB, tb)
+        try:
+            b, (d, ii, ln, ops) = _batch_run(gpu, packed, script, no_len=no_len)
+        finally:
+            gpu.set_option(sedgpu.SED_OPT_TB, 0)
         try:
             nwave = packed.npairs - b.lane_pairs
             if not no_len:  # distance-only batches pack pairs two per wave instead (SED_OPT_PACK)
                 assert b.rows_per_lane == 8 and b.chains == 5120
+                assert b.traceback_mode == (0 if not script else 2 if tb == 2 else 1)
                 fetched, per_wave = b.chain_stats()
                 assert fetched == nwave and per_wave >= 2, (fetched, nwave, per_wave)
         finally:
@@ -98,17 +104,20 @@ def test_dynamic_chain_capped_waves(gpu, tables):
     gpu.set_option(sedgpu.SED_OPT_CHAIN, 1)
     gpu.set_option(sedgpu.SED_OPT_CHAIN_WAVES, 300)
     try:
-        b, (d, ii, ln, ops) = _batch_run(gpu, packed, True)
-        try:
-            assert b.chains == 300
-            fetched, per_wave = b.chain_stats()
-            assert fetched == packed.npairs - b.lane_pairs and per_wave >= 25, (fetched, per_wave)
-        finally:
-            b.close()
+        for tb in (0, 2):  # per-cell codes, then checkpoints
+            gpu.set_option(sedgpu.SED_OPT_TB, tb)
+            b, (d, ii, ln, ops) = _batch_run(gpu, packed, True)
+            try:
+                assert b.chains == 300 and b.traceback_mode == (2 if tb else 1)
+                fetched, per_wave = b.chain_stats()
+                assert fetched == packed.npairs - b.lane_pairs and per_wave >= 25, (fetched, per_wave)
+            finally:
+                b.close()
+            _check_all(plan, packed, d, ii, ln, ops)
     finally:
         gpu.set_option(sedgpu.SED_OPT_CHAIN, 0)
         gpu.set_option(sedgpu.SED_OPT_CHAIN_WAVES, 0)
-    _check_all(plan, packed, d, ii, ln, ops)
+        gpu.set_option(sedgpu.SED_OPT_TB, 0)
 
 
 def test_checkpoint_default_route_with_lane_pairs_and_pipeline(gpu, tables):
@@ -116,7 +125,7 @@ def test_checkpoint_default_route_with_lane_pairs_and_pipeline(gpu, tables):
     codes, long pairs (n up to 2600) on the R = 16 checkpoint route, in one batch.  Every pair vs the
     oracle, then the same batch pipelined (SED_PIPELINE, ignored by checkpoint batches) run 3 times."""
     A1, B1 = _ragged(3200, 200, 1, 512, 1, 32)
-    A2, B2 = _ragged(3201, 120, 513, 2600, 33, 2600)
+    A2, B2 = _ragged(3201, 120, 1200, 2600, 1200, 2600)  # large enough for the automatic checkpoint route
     A, B = A1 + A2, B1 + B2
     order = np.random.default_rng(3202).permutation(len(A))
     A, B = [A[i] for i in order], [B[i] for i in order]
@@ -143,13 +152,17 @@ def test_checkpoint_traceback_reports_a_corrupt_checkpoint(gpu, tables):
     gpu.set_costs(plan)
     packed = sedgpu.PackedPairs(A, B)
     victim = 123
+    gpu.set_option(sedgpu.SED_OPT_TB, 2)
     gpu.set_option(sedgpu.SED_OPT_DEBUG_CORRUPT, victim + 1)
     try:
         with pytest.raises(sedgpu.SedError, match="pair %d: traceback failed" % victim):
             gpu.run(packed, True)
     finally:
         gpu.set_option(sedgpu.SED_OPT_DEBUG_CORRUPT, 0)
-    d, ii, ln, ops = gpu.run(packed, True)  # the same context recovers
+    try:
+        d, ii, ln, ops = gpu.run(packed, True)  # the same context recovers
+    finally:
+        gpu.set_option(sedgpu.SED_OPT_TB, 0)
     _check_all(plan, packed, d, ii, ln, ops)
 
 
