@@ -54,6 +54,12 @@ __device__ __forceinline__ uint32_t dpp_shl1(uint32_t old, uint32_t src) {
 __device__ __forceinline__ uint32_t dpp_rol1(uint32_t src) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)src, (int)src, DPP_WAVE_ROL1, 0xf, 0xf, false);
 }
+// lane i <- lane i-1's src + addv, lane 0 keeps `old`: one v_add_u32_dpp (the s_nop covers the DPP read of
+// a VGPR written by the previous VALU instruction)
+__device__ __forceinline__ uint32_t dpp_shr1_add(uint32_t old, uint32_t src, uint32_t addv) {
+    asm("s_nop 1\n\tv_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(old) : "v"(src), "v"(addv));
+    return old;
+}
 __device__ __forceinline__ double dpp_shr1_f64(double old, double src) {
     const uint64_t o = __double_as_longlong(old), s = __double_as_longlong(src);
     const uint32_t lo = dpp_shr1((uint32_t)o, (uint32_t)s);
@@ -1364,47 +1370,72 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
 // the cell above arrives through the DPP chain from lane r - 1, the str2 selector from LDS).  The forward kernel
 // stores distance keys (D, L without the op); every checkpoint value is converted on load to the
 // traceback key of the same (D, L) (i32_dist_to_tb), whose min carries the canonical op in its low two
-// bits: 6 VALU per cell (perm, 2 adds, min3, and, alignbit).  Lanes of band b hold their checkpoint
-// until their first column (step r - b + G - 1) and store code 3 there (outside the band's window); the
-// first row of bands 1..G-1 takes its first diagonal from the checkpoint; columns < 1 get the sentinel
-// selector, so they keep the column-0 border.  The sweep stops after the 16-step word holding the
-// entry cell's step (the path only goes up and left), and the entry cell's key must carry the path
-// length still to emit: a mismatch (a corrupted checkpoint, SED_OPT_DEBUG_CORRUPT) sets res.err
-// instead of writing a wrong script.  Codes stay in registers, 16 steps per word.  The walk is scalar:
-// one v_readlane per step and the state packed as S = row + (step << 7), so a step is ~16 SALU
-// (a step moves S by 128 / 129 / 257 for insert / delete / update; bit 6 set = above the tile; code
-// 3 = left of the window), one unrolled copy per code word since the step only decreases.
+// bits: 6 VALU per cell (v_add_u32_dpp for the cell above + 1, perm, add, min3, and, alignbit).  Lanes of
+// band b hold their checkpoint until their first column (step r - b + G - 1: one v_cndmask on a scalar
+// mask) and read code 3 there (outside the band's window, OR-ed in per word); the first row of bands
+// 1..G-1 takes its first diagonal from the checkpoint; columns < 1 get the sentinel selector, so they keep
+// the column-0 border.  The sweep stops after the 16-step word holding the entry cell's step (the path only
+// goes up and left), and the entry cell's key must carry the path length still to emit: a mismatch (a
+// corrupted checkpoint, SED_OPT_DEBUG_CORRUPT) sets res.err instead of writing a wrong script.  Codes stay
+// in registers, 16 steps per word.  The walk is scalar: one v_readlane per step and the state packed as
+// S = row + (step << 7), ~15 SALU per step (a step moves S by 128 / 129 / 257 for insert / delete /
+// update; one masked compare catches leaving the word, the tile (bit 6 = above it) and the window (code
+// 3)), one unrolled copy per code word since the step only decreases.
 // ---------------------------------------------------------------------------
-#define SED_TB_MOVES (128ull | (129ull << 16) | (257ull << 32))  // S decrement per op (insert, delete, update)
+// S decrement per code: insert 128, delete 129, update 257 (S = row | step << 7); the marker 3 (left of the
+// band's window) moves S by 0x8000, out of every word, and is taken back at the exit.  Only the low 16 bits of S
+// are kept: a move subtracts the next code's field << 16 as well.
+#define SED_TB_MOVES (128ull | (129ull << 16) | (257ull << 32) | (0x8000ull << 48))
+#define SED_TB_WORD 0xF840u  // S bits that change when the walk leaves a 16-step word or the tile (bit 6: above it)
 // The walk of one tile from state S; returns the state of the first cell it did not take (outside the
-// tile: above it, left of its band's window, or at column 0 for C0).  One loop per code word, each with a
-// single exit: the next code is read before the bounds test, and a cell past the word's bound or
-// outside the tile reads as the marker 3.
+// tile: above it, left of its band's window, or at column 0 for C0), low 16 bits.  One loop per code word with a
+// single exit test: the next state's word bits (S & SED_TB_WORD) must still be the word's tag.
 template <bool C0>  // C0: chunk-0 tile, whose window reaches the column-0 border: stop at j = 0
 __device__ __forceinline__ uint32_t ck_walk(const uint32_t (&W)[8], uint32_t S, uint32_t &q, uint32_t &acc,
                                             uint32_t &err, uint32_t *__restrict__ out, const uint32_t q0, int jcol) {
 #pragma unroll
     for (int w = 7; w >= 0; --w) {
-        const uint32_t lo = (uint32_t)(16 * w) << 7;
-        if (S >= lo && S < lo + (16u << 7) && !(S & 64u)) {
-            uint32_t code = ((uint32_t)__builtin_amdgcn_readlane((int)W[w], (int)S) >> ((S >> 6) & 31u)) & 3u;
-            if (C0 && jcol == 0) code = 3u;
-            while (code != 3u) {
-                acc = (acc << 2) | code;
+        const uint32_t tag = (uint32_t)w << 11;
+        if ((S & SED_TB_WORD) == tag) {
+            uint32_t code;
+            do {
+                // s_lshr takes the low 5 bits of S >> 6: 2 * (step & 15), bit 6 of S being clear inside the tile
+                code = ((uint32_t)__builtin_amdgcn_readlane((int)W[w], (int)S) >> ((S >> 6) & 31u)) & 3u;
+                if (C0 && jcol == 0) code = 3u;
+                acc = (acc << 2) + code;  // the marker too: taken back below
                 if ((--q & 15u) == 0) {
                     if (q < q0) out[q >> 4] = acc;
                     else err = SED_ERR_TB_LENGTH;  // ran past the sink's L (the tile still bounds the walk)
                 }
                 if constexpr (C0) jcol -= (int)((5u >> code) & 1u);
-                S -= (uint32_t)(SED_TB_MOVES >> (code << 4)) & 0xFFFFu;
-                const uint32_t f = ((uint32_t)__builtin_amdgcn_readlane((int)W[w], (int)S) >> ((S >> 6) & 31u)) & 3u;
-                const bool out_of = (S & 64u) || S < lo || (C0 && jcol == 0);
-                code = out_of ? 3u : f;
+                S -= (uint32_t)(SED_TB_MOVES >> (code << 4));
+            } while ((S & SED_TB_WORD) == tag);
+            if (code == 3u) {  // the marker: not an op, the walk stays at the cell before it
+                acc >>= 2;
+                ++q;  // a word stored at this q is stored again when the walk gets there
+                return (S + 0x8000u) & 0xFFFFu;
             }
-            if ((S & 64u) || S >= lo || (C0 && jcol == 0)) return S;  // left the tile (not just the word)
         }
     }
-    return S;
+    return S & 0xFFFFu;
+}
+
+// lanes 0 .. n-1 have reached their window at sweep step sig (sig0(r) = r - r/R + G - 1 is nondecreasing)
+template <int R> constexpr int ck_active_lanes(int sig) {
+    constexpr int G = 64 / R;
+    int n = 0;
+    for (int r = 0; r < 64; ++r)
+        if (r - r / R + G - 1 <= sig) n = r + 1;
+    return n;
+}
+// lanes >= act keep v, the others take vn: the mask is built on the scalar unit inside the asm, so the
+// compiler can neither hoist the 60-odd constant masks (they spill) nor turn them into a VALU compare
+__device__ __forceinline__ uint32_t ck_hold(uint32_t vn, uint32_t v, const int act) {
+    uint32_t r;
+    uint64_t m;
+    // (s_lshl_b64 writes SCC: without the clobber a compare's SCC could be read across the asm)
+    asm("s_lshl_b64 %1, -1, %4\n\tv_cndmask_b32 %0, %2, %3, %1" : "=v"(r), "=&s"(m) : "v"(vn), "v"(v), "i"(act) : "scc");
+    return r;
 }
 
 // band b >= 1 of a tile starts (its first row takes the checkpoint's top_prev as diagonal) at sweep step
@@ -1431,6 +1462,9 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
     if (pair >= npairs) return;
     const sed_pair_desc d = pd[pair];
     if (d.lane) return;  // scripted by sed_lane.hip
+#ifdef SED_TB_DEBUG
+    if (pair != 0) return;
+#endif
     const int n = d.n, m = d.m;
     uint32_t *out = ops + d.ops_off;
     const uint32_t q0 = (uint32_t)__builtin_amdgcn_readfirstlane(res[pair].len);
@@ -1443,6 +1477,7 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
         acc = (acc << 2) | op;
         if ((--q & 15u) == 0) out[q >> 4] = acc;
     };
+    // topb[x]: the row above the tile at lane 0's column of step x, plus 1 (lane 0's delete candidate);
     // selb[64 + x]: str2 selector of lane 0's column at step x; lane r reads selb[64 + sigma - r] itself
     // (its column at step sigma), so no selector travels through the DPP chain
     __shared__ uint32_t topb[132], selb[64 + 132];
@@ -1456,6 +1491,15 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
         const uint32_t *pa = seqa + d.a_off, *pb = seqb + d.b_off;
         const int band = lane >> LR;
         const int sig0 = lane - band + G - 1;  // first real sweep step of this lane (<= 63)
+        // code 3 (outside the window) for the steps before sig0, OR-ed into words 0..3 once they are complete
+        uint32_t hm[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const int h = min(max(sig0 - 16 * w, 0), 16);
+            hm[w] = h >= 16 ? ~0u : (1u << (2 * h)) - 1u;
+        }
+        uint32_t one = 1u;  // the delete candidate's +1, a VGPR operand of v_add_u32_dpp
+        asm volatile("" : "+v"(one));
         int guard = 2 * (n + m) + 8;       // tiles visited; every visit makes progress
         while (i > 0 && j > 0) {
             if (--guard <= 0) {
@@ -1477,6 +1521,9 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
                 V = i32_dist_to_tb(cp[0]);
                 tp = i32_dist_to_tb(cp[(R - (lane & (R - 1))) * 64]);
             }
+            tp += 1u;  // diagonals carry the +1 of the delete candidate they were taken from
+            {
+            }
             for (int x = lane; x < 132; x += 64) {
                 // the row above the tile at column J0 - G + x: row checkpoints of forward lane G*Q - 1 (or lane 63
                 // of the stripe above); steps clamped: past SG the columns are beyond m and never read by the
@@ -1489,7 +1536,7 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
                     else if (k >= 1)
                         v = i32_dist_to_tb(rcp[sed_ck_row_word(R, k - 1, ngroups, min(64 * c + 63 - G + x, SG - 1), 63)]);
                 }
-                topb[x] = v;
+                topb[x] = v + 1u;
                 const int col = J0 - (G - 1) + x;  // column of lane 0 at step x
                 const int ci = min(max(col - 1, 0), m - 1);
                 selb[64 + x] = col < 1 ? SED_SEL_SENT : i32_sel((pb[ci >> 4] >> ((ci & 15) * 2)) & 3u);
@@ -1497,32 +1544,29 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
             __syncthreads();
             // ---- sweep: lane r at step sigma computes (row rowbase + r + 1, column J0 - (G-1) + sigma - r) ----
             // Whole 16-step words (a branch per step would keep the LDS reads from running ahead); the block
-            // holding the entry step also captures each lane's key at that step.
+            // holding the entry step also captures each lane's key at that step.  The cell above and the diagonal
+            // carry the delete candidate's +1 (one v_add_u32_dpp: lane r - 1's key + 1, or topb for lane 0), so
+            // the update constant is one less.  Lanes still left of their window (sigma < sig0: lanes
+            // ck_active_lanes(sigma) .. 63, a compile-time count) keep their checkpoint through one v_cndmask on a
+            // scalar mask; their codes become 3 through hm.  Steps 0 .. G-2 hold every lane and are skipped.
             uint32_t W[8];
-            uint32_t tprev = dpp_shr1(topb[0], V);  // diagonal of step 0: the lane above, or row above
+            W[0] = 0u;  // steps 0 .. G-2 are skipped: their bits are OR-ed to 3 from a defined word
+            uint32_t tprev = dpp_shr1_add(topb[G - 1], V, one);  // diagonal of step G-1 (+1)
             uint32_t ent = 0;
             const uint32_t *selp = selb + 64 - lane;  // lane r's selector at step sigma: selp[sigma]
             const int w_end = sig_end >> 4;
-            // the hold threshold, opaque per tile: otherwise all 64 `sig < sig0` masks are hoisted out of the
-            // tile loop into SGPR pairs, which spill to VGPR lanes and come back with a v_readlane per step
-            int hold_below = sig0;
-            asm volatile("" : "+v"(hold_below));
             auto step = [&](const int sig, uint32_t &wv, const bool capture) {
-                const uint32_t topv = dpp_shr1(topb[sig + 1], V);
+                if (sig < G - 1) return;  // every lane holds
+                const uint32_t topv = dpp_shr1_add(topb[sig + 1], V, one);
                 const uint32_t selv = selp[sig];  // steps before the lane's first column read don't-care
                 uint32_t diag = tprev;
                 const int bs = ck_band_start<R>(sig);  // folds to a constant in the unrolled sweep
                 if (bs > 0) diag = lane == R * bs ? tp : diag;
-                const uint32_t mm = umin3(V, topv + 1u, diag + __builtin_amdgcn_perm(cv, 0xFFFFFFFEu, selv));
+                const uint32_t mm = umin3(V, topv, diag + __builtin_amdgcn_perm(cv, 0xFFFFFFFDu, selv));
                 const uint32_t vn = mm & ~3u;
-                if (sig < 64) {  // left of the band's checkpoint: hold it, code 3 (outside the window)
-                    const bool hold = sig < hold_below;
-                    wv = __builtin_amdgcn_alignbit(hold ? 3u : mm, wv, 2);
-                    V = hold ? V : vn;
-                } else {
-                    wv = __builtin_amdgcn_alignbit(mm, wv, 2);
-                    V = vn;
-                }
+                const int act = ck_active_lanes<R>(sig);  // lanes 0 .. act-1 are inside their window
+                V = act >= 64 ? vn : ck_hold(vn, V, act);
+                wv = __builtin_amdgcn_alignbit(mm, wv, 2);
                 if (capture) ent = sig == sig_end ? vn : ent;
                 tprev = topv;
             };
@@ -1536,7 +1580,20 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
 #pragma unroll
                     for (int u = 0; u < 16; ++u) step(16 * w + u, W[w], false);
                 }
+                if (w < 4) W[w] |= hm[w];
             }
+#ifdef SED_TB_DEBUG
+            {  // debug builds only: pair 0's first tile -> ops[0 .. 648), then stop
+                for (int w = 0; w < 8; ++w) out[w * 64 + lane] = w <= w_end ? W[w] : 0u;
+                out[512 + lane] = ent;
+                out[576 + lane] = V;
+                if (lane == 0) {
+                    out[640] = (uint32_t)i; out[641] = (uint32_t)j; out[642] = (uint32_t)c; out[643] = (uint32_t)Q;
+                    out[644] = (uint32_t)k; out[645] = (uint32_t)sig_end; out[646] = (uint32_t)re; out[647] = q;
+                }
+                return;
+            }
+#endif
             // ---- the entry cell's key must carry the ops still to emit (L of a canonical-path cell) ----
             {
                 const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)ent, re) - SED_KB + (uint32_t)i * Kd +
