@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <type_traits>
 #include "sed_internal.h"
 
 #define DPP_WAVE_SHL1 0x130  // lane i <- lane i+1, lane 63 keeps `old`
@@ -438,26 +439,46 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         uint32_t rcv[G];
         const bool last = (k == nstripes - 1);
         const int cap_step = last ? m - 1 + cap_lane : -1;
+        // CK: a chunk is 64/G groups, unrolled (LDS and store addresses are immediates) and always whole: the last
+        // chunk's steps past SG compute columns beyond m that nothing reads, and only their stores are skipped.
+        // The chunk holding the sink runs the rolled loop below, so the unrolled groups have no merge point (a
+        // CAP/plain choice per group made the register allocator move the whole row state every group).  The
+        // other kernels keep the rolled loop everywhere (unrolling all of their variants multiplies compile time).
+        const int c_cap = last ? cap_step >> 6 : -1;
         int s = 0;
         for (int c = 0; c < nchunks; ++c) {
             uint32_t tnx = 0, snx = 0;
             if (c + 1 < nchunks) { tnx = load_top(c + 1); snx = load_sel(c + 1); }
             const uint32_t *lsel = ring + ((64 * c - lane) & 127);  // this lane's column at the chunk's first step
-            for (int g = 0; g < 64 / G && s < SG; ++g, s += G, lsel += G) {
-                const bool capg = cap_step >= s && cap_step < s + G;
-                if (capg)
-                    i32_group<R, TB, LEN, true, CK>(V, cv, top_prev, bottom, selv, lch, lsel, outc, W, s, lane,
-                                                    cap_step, cap_lane, cap_row, cap, rcv);
-                else
-                    i32_group<R, TB, LEN, false, CK>(V, cv, top_prev, bottom, selv, lch, lsel, outc, W, s, lane,
-                                                     cap_step, cap_lane, cap_row, cap, rcv);
+            auto stores = [&](const int s0) {
                 if constexpr (TB) {
-                    uint32_t *gp = tbk + (uint64_t)(s / G) * 256u;  // wave-uniform base, per-lane 16-byte offset
+                    uint32_t *gp = tbk + (uint64_t)(s0 / G) * 256u;  // wave-uniform base, per-lane 16-byte offset
                     store_tb(gp + lane * 4, W);
                 }
                 if constexpr (CK) {
-                    if ((lane & (G - 1)) == G - 1) store_words<G>(rcb + (uint64_t)(s / G) * 64u + (uint32_t)(lane / G) * G, rcv);
-                    if (lane == 63 && !last) store_words<G>(bnd + d.bnd_off + (uint32_t)s, rcv);  // next stripe's top row
+                    if ((lane & (G - 1)) == G - 1) store_words<G>(rcb + (uint64_t)(s0 / G) * 64u + (uint32_t)(lane / G) * G, rcv);
+                    if (lane == 63 && !last) store_words<G>(bnd + d.bnd_off + (uint32_t)s0, rcv);  // next stripe's top row
+                }
+            };
+            if (CK && c != c_cap) {
+#pragma unroll 2
+                for (int g = 0; g < 64 / G; ++g) {
+                    const int s0 = 64 * c + g * G;  // (s0 & 63 folds to g * G)
+                    i32_group<R, TB, LEN, false, CK>(V, cv, top_prev, bottom, selv, lch, lsel + g * G, outc, W, s0, lane,
+                                                     cap_step, cap_lane, cap_row, cap, rcv);
+                    if (s0 < SG) stores(s0);
+                }
+                s = min(64 * (c + 1), SG);
+            } else {
+                for (int g = 0; g < 64 / G && s < SG; ++g, s += G, lsel += G) {
+                    const bool capg = cap_step >= s && cap_step < s + G;
+                    if (capg)
+                        i32_group<R, TB, LEN, true, CK>(V, cv, top_prev, bottom, selv, lch, lsel, outc, W, s, lane,
+                                                        cap_step, cap_lane, cap_row, cap, rcv);
+                    else
+                        i32_group<R, TB, LEN, false, CK>(V, cv, top_prev, bottom, selv, lch, lsel, outc, W, s, lane,
+                                                         cap_step, cap_lane, cap_row, cap, rcv);
+                    stores(s);
                 }
             }
             if constexpr (CK) {  // column checkpoint: state after the chunk's last step
