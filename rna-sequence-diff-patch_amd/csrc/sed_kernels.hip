@@ -439,11 +439,12 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         uint32_t rcv[G];
         const bool last = (k == nstripes - 1);
         const int cap_step = last ? m - 1 + cap_lane : -1;
-        // CK: a chunk is 64/G groups, unrolled (LDS and store addresses are immediates) and always whole: the last
-        // chunk's steps past SG compute columns beyond m that nothing reads, and only their stores are skipped.
-        // The chunk holding the sink runs the rolled loop below, so the unrolled groups have no merge point (a
-        // CAP/plain choice per group made the register allocator move the whole row state every group).  The
-        // other kernels keep the rolled loop everywhere (unrolling all of their variants multiplies compile time).
+        // CK: a chunk is 64/G groups (unrolled by 2) and always whole: the last chunk's steps past SG compute
+        // columns beyond m that nothing reads, and only their stores are skipped.  The chunk holding the sink
+        // runs the rolled loop below, so the others have no merge point: a CAP/plain choice per group made the
+        // register allocator move the whole row state every group (3.30 -> 3.11 VALU per cell).  The per-cell-code
+        // kernels keep the rolled loop for every chunk: split the same way, their hot loop spills.  (Fully
+        // unrolled chunks take the compiler > 15 min.)
         const int c_cap = last ? cap_step >> 6 : -1;
         int s = 0;
         for (int c = 0; c < nchunks; ++c) {
@@ -468,7 +469,7 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                                                      cap_step, cap_lane, cap_row, cap, rcv);
                     if (s0 < SG) stores(s0);
                 }
-                s = min(64 * (c + 1), SG);
+                s = 64 * (c + 1);  // lane 63's bottom cells of the whole chunk are in outc (!CK)
             } else {
                 for (int g = 0; g < 64 / G && s < SG; ++g, s += G, lsel += G) {
                     const bool capg = cap_step >= s && cap_step < s + G;
