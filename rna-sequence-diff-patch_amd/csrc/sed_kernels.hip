@@ -1565,8 +1565,8 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
             }
             __syncthreads();
             // ---- sweep: lane r at step sigma computes (row rowbase + r + 1, column J0 - (G-1) + sigma - r) ----
-            // Whole 16-step words (a branch per step would keep the LDS reads from running ahead); the block
-            // holding the entry step also captures each lane's key at that step.  The cell above and the diagonal
+            // Whole 16-step words (a branch per step would keep the LDS reads from running ahead), except the
+            // word holding the entry step, which stops at it: the lanes' keys are then the entry keys.  The cell above and the diagonal
             // carry the delete candidate's +1 (one v_add_u32_dpp: lane r - 1's key + 1, or topb for lane 0), so
             // the update constant is one less.  Lanes still left of their window (sigma < sig0: lanes
             // ck_active_lanes(sigma) .. 63, a compile-time count) keep their checkpoint through one v_cndmask on a
@@ -1577,7 +1577,7 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
             uint32_t ent = 0;
             const uint32_t *selp = selb + 64 - lane;  // lane r's selector at step sigma: selp[sigma]
             const int w_end = sig_end >> 4;
-            auto step = [&](const int sig, uint32_t &wv, const bool capture) {
+            auto step = [&](const int sig, uint32_t &wv) {
                 if (sig < G - 1) return;  // every lane holds
                 const uint32_t topv = dpp_shr1_add(topb[sig + 1], V, one);
                 const uint32_t selv = selp[sig];  // steps before the lane's first column read don't-care
@@ -1589,21 +1589,25 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
                 const int act = ck_active_lanes<R>(sig);  // lanes 0 .. act-1 are inside their window
                 V = act >= 64 ? vn : ck_hold(vn, V, act);
                 wv = __builtin_amdgcn_alignbit(mm, wv, 2);
-                if (capture) ent = sig == sig_end ? vn : ent;
                 tprev = topv;
             };
 #pragma unroll
             for (int w = 0; w < 8; ++w) {
                 if (w > w_end) break;  // the path never needs later steps
-                if (w == w_end) {
+                if (w == w_end) {  // up to the entry step exactly: the lanes then hold the entry keys
 #pragma unroll
-                    for (int u = 0; u < 16; ++u) step(16 * w + u, W[w], true);
+                    for (int u = 0; u < 16; ++u) {
+                        if (16 * w + u > sig_end) break;
+                        step(16 * w + u, W[w]);
+                    }
+                    W[w] >>= 2u * (15u - ((uint32_t)sig_end & 15u));  // step u's code to bits 2u, 2u+1
                 } else {
 #pragma unroll
-                    for (int u = 0; u < 16; ++u) step(16 * w + u, W[w], false);
+                    for (int u = 0; u < 16; ++u) step(16 * w + u, W[w]);
                 }
                 if (w < 4) W[w] |= hm[w];
             }
+            ent = V;
 #ifdef SED_TB_DEBUG
             {  // debug builds only: pair 0's first tile -> ops[0 .. 648), then stop
                 for (int w = 0; w < 8; ++w) out[w * 64 + lane] = w <= w_end ? W[w] : 0u;
