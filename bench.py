@@ -215,6 +215,48 @@ def cpu_baseline(plan, packed, seconds, threads, want_ops):
             "ops": ops, "ops_off": ops_off}
 
 
+def measure_traffic(kernels):
+    """HBM bytes per launch of `kernels` (summed), measured now: this bench re-run as a child process for one
+    step under rocprofv3, one pass per counter (FETCH_SIZE and WRITE_SIZE do not fit one pass).  Units and the
+    gfx950 correction per MI355X_MICROARCH.md "HBM": both counters in KiB, FETCH_SIZE reports half the bytes of
+    wide streaming reads, so bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.  Returns (bytes, detail) or
+    (None, reason)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    rp = shutil.which("rocprofv3")
+    if rp is None:
+        return None, "rocprofv3 not found"
+    kib = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="sedpmc_", dir="/tmp")
+        # argparse keeps the last occurrence: one untimed-warmup-free step, no CPU legs, no nested measurement
+        child = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:] + [
+            "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--traffic", "none"]
+        cmd = ["timeout", "-s", "KILL", "240", rp, "--pmc", ctr, "-T", "-d", d, "-o", "pmc",
+               "--output-format", "csv", "--"] + child
+        try:
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                               env=dict(os.environ, TMPDIR="/tmp"), timeout=300)
+        except subprocess.TimeoutExpired:
+            return None, "%s pass timed out" % ctr
+        vals = {}
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    if row["Counter_Name"] == ctr and row["Kernel_Name"] in kernels:
+                        vals.setdefault(row["Kernel_Name"], []).append(float(row["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+        if r.returncode != 0 or not vals:
+            return None, "%s pass failed (rc %d)" % (ctr, r.returncode)
+        kib[ctr] = sum(sum(v) / len(v) for v in vals.values())  # per launch, summed over the kernels
+    total = 2.0 * kib["FETCH_SIZE"] * 1024.0 + kib["WRITE_SIZE"] * 1024.0
+    return total, {"FETCH_SIZE_KiB": kib["FETCH_SIZE"], "WRITE_SIZE_KiB": kib["WRITE_SIZE"],
+                   "correction": "KiB; FETCH_SIZE x2 on gfx950 (MI355X_MICROARCH.md HBM)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -241,6 +283,9 @@ def main():
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_dp_i32_c4.json"),
                     help="per-launch HBM traffic of the DP kernel from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                          "(tools/profile_round.sh + tools/summarize_profile.py); used when its workload matches")
+    ap.add_argument("--traffic", default="measure", choices=["measure", "file", "none"],
+                    help="roofline.traffic: measure = two rocprofv3 --pmc child runs of this workload (FETCH_SIZE, "
+                         "WRITE_SIZE, one step each) on rank 0 at N = 1; file = --pmc-json; none")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse ranks sharing one GPU")
     args = ap.parse_args()
@@ -391,12 +436,6 @@ def main():
         return
     dp_avg = float(np.mean(dp_ms))
     achieved = algo_bytes / (dp_avg * 1e-3) / 1e9
-    traffic = None
-    if args.pmc_json and os.path.exists(args.pmc_json):
-        with open(args.pmc_json) as f:
-            pm = json.load(f)
-        if pm.get("workload") == desc and batch.mode == "i32" and want_script and P == WORKLOADS[args.workload][0]:
-            traffic = pm.get("hbm_bytes_per_launch")
     nl, npk = batch.lane_pairs, batch.packed_pairs
     lane_x2 = batch.mode == "i32" and not want_script and nl > 0 and not args.no_pack
     wave_x2 = npk - (nl if lane_x2 else 0)  # wave pairs computed two per wave
@@ -415,6 +454,17 @@ def main():
         parts = ((["sed_wf_i32x2_kernel"] if wave_x2 else []) + ([wave_k] if nl + wave_x2 < P else []) +
                  ([("sed_lane_i32x2_kernel" if lane_x2 else "sed_lane_i32_kernel")] if nl else []))
     kname = "+".join(parts)
+    traffic, traffic_src = None, None
+    if args.traffic == "measure" and world == 1:
+        traffic, detail = measure_traffic(set(parts))
+        traffic_src = {"measured": "rocprofv3 --pmc, this workload, one step per counter", **detail} \
+            if traffic is not None else {"measure_failed": detail}
+    if traffic is None and args.traffic != "none" and args.pmc_json and os.path.exists(args.pmc_json):
+        with open(args.pmc_json) as f:
+            pm = json.load(f)
+        if pm.get("workload") == desc and batch.mode == "i32" and want_script and P == WORKLOADS[args.workload][0]:
+            traffic = pm.get("hbm_bytes_per_launch")
+            traffic_src = dict(traffic_src or {}, file=os.path.relpath(args.pmc_json, REPO))
     line = {
         "metric": METRIC, "value": value, "unit": "cells/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
@@ -426,7 +476,7 @@ def main():
                    "traceback": {0: None, 1: "per-cell codes", 2: "checkpoints + recompute"}[batch.traceback_mode],
                    "parallelism": "dp%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": kname,
                      "kernel_ms": dp_avg, "algo_bytes_per_launch": algo_bytes},
         "valu": None if valu_peak is None else {
