@@ -260,7 +260,7 @@ def measure_traffic(kernels):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)  # per-cell-code batches: the last traceback is not overlapped
+    ap.add_argument("--steps", type=int, default=20)  # per-cell-code batches pipeline traceback k beside DP k+1 (the last one is not overlapped); checkpoint batches run DP then traceback
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     ap.add_argument("--pairs", type=int, default=0, help="override pairs per GPU")
