@@ -177,9 +177,14 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
                                          uint32_t &bottom, uint32_t &selv, const uint2 tv, uint32_t &outc,
                                          uint32_t (&W)[4], const int u) {
     using Lad = Ladder<R>;
-    const uint32_t topv = dpp_shr1(TOPC ? top_prev : tv.x, bottom);  // cell above the band, this column
     if constexpr (SELL) selv = tv.y;
     else selv = dpp_shr1(tv.y, selv);  // perm selector of this column's str2 symbol
+    constexpr int d0 = Lad::rung(1) - Lad::rung(0);
+    // row 0's update candidate from top_prev, before the DPP move overwrites top_prev in place (TOPC): the
+    // empty asm makes the move's `old` depend on it, so top_prev needs no copy
+    uint32_t dg0 = top_prev + __builtin_amdgcn_perm(cv[0], LEN ? (uint32_t)(d0 - 6) : 0xFFFFFFFFu, selv);
+    if constexpr (TOPC) asm("" : "+v"(top_prev) : "v"(dg0));
+    const uint32_t topv = dpp_shr1(TOPC ? top_prev : tv.x, bottom);  // cell above the band, this column
     uint32_t up = topv, diag = top_prev;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -190,14 +195,14 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
             // insert (op 0) = left, delete (op 1) = up + d + 1, update (op 2) = diag + offset constant
             // (perm bytes 1:0 from the inline constant d - 6)
             mm = umin3(left, d == -1 ? up : up + (uint32_t)(d + 1),
-                       diag + __builtin_amdgcn_perm(cv[r], (uint32_t)(d - 6), selv));
+                       r == 0 ? dg0 : diag + __builtin_amdgcn_perm(cv[r], (uint32_t)(d - 6), selv));
             if constexpr (TB) {
                 const int k = u * R + r;
                 W[k >> 4] = __builtin_amdgcn_alignbit(mm, W[k >> 4], 2);
             }
             up = (mm & ~7u) | (uint32_t)c;
         } else {
-            mm = umin3(left, up, diag + __builtin_amdgcn_perm(cv[r], 0xFFFFFFFFu, selv));
+            mm = umin3(left, up, r == 0 ? dg0 : diag + __builtin_amdgcn_perm(cv[r], 0xFFFFFFFFu, selv));
             up = mm;
         }
         diag = left;
