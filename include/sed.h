@@ -65,8 +65,10 @@ enum {
 #define SED_OPT_CHAIN 5         /* integer kernel, single-stripe pairs run back to back in one wave (no
                                    per-pair ramp): 0 auto (large batches), 1 whenever eligible, 2 never,
                                    L >= 3 whenever eligible with chains of L pairs */
-#define SED_OPT_TB 7            /* script batches on the R = 16 integer wave kernel: 0 auto (checkpoints + recompute
-                                   for > 256 pairs), 1 per-cell traceback codes, 2 checkpoints whenever eligible */
+#define SED_OPT_TB 7            /* integer script batches at R = 4/8/16 (stripe and CHAIN kernels, not SPLIT): 0 auto
+                                   (checkpoints + recompute for > 256 pairs averaging >= 512 cells per path op,
+                                   i.e. sum n*m >= 512 * sum (n+m)), 1 per-cell traceback codes, 2 checkpoints
+                                   whenever eligible */
 #define SED_OPT_PACK 6          /* distance-only integer batches (SED_NO_LEN): two pairs per lane (equal n) or per
                                    wave (equal n and m) in packed 16-bit cells: 0 auto (on), 2 never */
 #define SED_OPT_CHAIN_WAVES 8   /* dynamic CHAIN mode: persistent waves, 0 auto (every SIMD's resident waves), else a
