@@ -1474,27 +1474,31 @@ template <int R> constexpr int ck_band_start(int sig) {
     return 0;
 }
 
-template <int R>
-__global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
-                                                              const uint32_t *__restrict__ seqa,
-                                                              const uint32_t *__restrict__ seqb,
-                                                              const uint32_t *__restrict__ ck,
-                                                              sed_result *__restrict__ res,
-                                                              uint32_t *__restrict__ ops, sed_i32_params prm) {
+// LDS ordering inside the traceback: a workgroup barrier for the one-wave traceback kernel; WAVE: a wave-local
+// wait, for a traceback run by a wave of a larger workgroup (LDS accesses of one wave execute in order; the
+// clobber keeps the compiler from moving them across).  Fusing the traceback into the CK forward kernel this way
+// (each wave walks its pair after its forward pass) measured 13.9-14.0 ms per config-4 step against 13.87 ms
+// for the separate kernel (profiles/r02/abfuse), so the traceback stays a kernel of its own.
+template <bool WAVE> __device__ __forceinline__ void ck_sync() {
+    if constexpr (WAVE) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else __syncthreads();
+}
+
+// topb[x] (132 words): the row above the tile at lane 0's column of step x, plus 1 (lane 0's delete candidate);
+// selb[64 + x] (196 words): str2 selector of lane 0's column at step x; lane r reads selb[64 + sigma - r] itself
+// (its column at step sigma), so no selector travels through the DPP chain.  q0: the sink's L.
+template <int R, bool WAVE>
+__device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const int pair, const uint32_t q0,
+                                                  const int lane, const uint32_t *__restrict__ seqa,
+                                                  const uint32_t *__restrict__ seqb, const uint32_t *__restrict__ ck,
+                                                  sed_result *__restrict__ res, uint32_t *__restrict__ ops,
+                                                  const sed_i32_params &prm, uint32_t *__restrict__ topb,
+                                                  uint32_t *__restrict__ selb) {
     constexpr int ROWS = 64 * R, G = Grp<R>::G;  // a tile: G forward lanes (bands) of R rows
     constexpr int LR = R == 4 ? 2 : R == 8 ? 3 : 4;
     static_assert((1 << LR) == R, "R in {4, 8, 16}");
-    const int lane = threadIdx.x;
-    const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x);
-    if (pair >= npairs) return;
-    const sed_pair_desc d = pd[pair];
-    if (d.lane) return;  // scripted by sed_lane.hip
-#ifdef SED_TB_DEBUG
-    if (pair != 0) return;
-#endif
     const int n = d.n, m = d.m;
     uint32_t *out = ops + d.ops_off;
-    const uint32_t q0 = (uint32_t)__builtin_amdgcn_readfirstlane(res[pair].len);
     uint32_t q = q0, acc = 0, err = 0;
     auto emit = [&](uint32_t op) {  // sink -> origin (trailing border runs)
         if (q == 0) {
@@ -1504,10 +1508,6 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
         acc = (acc << 2) | op;
         if ((--q & 15u) == 0) out[q >> 4] = acc;
     };
-    // topb[x]: the row above the tile at lane 0's column of step x, plus 1 (lane 0's delete candidate);
-    // selb[64 + x]: str2 selector of lane 0's column at step x; lane r reads selb[64 + sigma - r] itself
-    // (its column at step sigma), so no selector travels through the DPP chain
-    __shared__ uint32_t topb[132], selb[64 + 132];
     const uint32_t Kd = (prm.del << 16) + 4u, Ki = (prm.ins << 16) + 4u;
     int i = n, j = m;
     if (i > 0 && j > 0) {
@@ -1568,7 +1568,7 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
                 const int ci = min(max(col - 1, 0), m - 1);
                 selb[64 + x] = col < 1 ? SED_SEL_SENT : i32_sel((pb[ci >> 4] >> ((ci & 15) * 2)) & 3u);
             }
-            __syncthreads();
+            ck_sync<WAVE>();
             // ---- sweep: lane r at step sigma computes (row rowbase + r + 1, column J0 - (G-1) + sigma - r) ----
             // Whole 16-step words (a branch per step would keep the LDS reads from running ahead), except the
             // word holding the entry step, which stops at it: the lanes' keys are then the entry keys.  The cell above and the diagonal
@@ -1647,7 +1647,7 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
             const int sg = (int)((S + 64u) >> 7), r = (int)((S + 64u) & 127u) - 64;
             i = rowbase + r + 1;
             j = J0 - (G - 1) + sg - r;
-            __syncthreads();  // topb / selb are rewritten for the next tile
+            ck_sync<WAVE>();  // topb / selb are rewritten for the next tile
         }
     }
     if (!err) {
@@ -1656,6 +1656,26 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
         if (q != 0) err = SED_ERR_TB_LENGTH;
     }
     if (err && lane == 0) res[pair].err = (uint8_t)err;
+}
+
+template <int R>
+__global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
+                                                              const uint32_t *__restrict__ seqa,
+                                                              const uint32_t *__restrict__ seqb,
+                                                              const uint32_t *__restrict__ ck,
+                                                              sed_result *__restrict__ res,
+                                                              uint32_t *__restrict__ ops, sed_i32_params prm) {
+    const int lane = threadIdx.x;
+    const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x);
+    if (pair >= npairs) return;
+    const sed_pair_desc d = pd[pair];
+    if (d.lane) return;  // scripted by sed_lane.hip
+#ifdef SED_TB_DEBUG
+    if (pair != 0) return;
+#endif
+    __shared__ uint32_t topb[132], selb[64 + 132];
+    const uint32_t q0 = (uint32_t)__builtin_amdgcn_readfirstlane(res[pair].len);
+    ck_traceback_pair<R, false>(d, pair, q0, lane, seqa, seqb, ck, res, ops, prm, topb, selb);
 }
 
 // ---------------------------------------------------------------------------
