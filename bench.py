@@ -226,6 +226,8 @@ def measure_traffic(kernels):
     import shutil
     import subprocess
     import tempfile
+    if any(k.startswith("ROCPROF") for k in os.environ):
+        return None, "this bench already runs under rocprofv3"  # no nested profilers
     rp = shutil.which("rocprofv3")
     if rp is None:
         return None, "rocprofv3 not found"
