@@ -1405,7 +1405,7 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
 // goes up and left), and the entry cell's key must carry the path length still to emit: a mismatch (a
 // corrupted checkpoint, SED_OPT_DEBUG_CORRUPT) sets res.err instead of writing a wrong script.  Codes stay
 // in registers, 16 steps per word.  The walk is scalar: one v_readlane per step and the state packed as
-// S = row + (step << 7), ~15 SALU per step (a step moves S by 128 / 129 / 257 for insert / delete /
+// S = row + (step << 7), 12 SALU per step (a step moves S by 128 / 129 / 257 for insert / delete /
 // update; one masked compare catches leaving the word, the tile (bit 6 = above it) and the window (code
 // 3)), one unrolled copy per code word since the step only decreases.
 // ---------------------------------------------------------------------------
@@ -1418,30 +1418,39 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
 // tile: above it, left of its band's window, or at column 0 for C0), low 16 bits.  One loop per code word with a
 // single exit test: the next state's word bits (S & SED_TB_WORD) must still be the word's tag.
 template <bool C0>  // C0: chunk-0 tile, whose window reaches the column-0 border: stop at j = 0
-__device__ __forceinline__ uint32_t ck_walk(const uint32_t (&W)[8], uint32_t S, uint32_t &q, uint32_t &acc,
-                                            uint32_t &err, uint32_t *__restrict__ out, const uint32_t q0, int jcol) {
+__device__ __forceinline__ uint32_t ck_walk(const uint32_t (&W)[8], uint32_t S, uint32_t &q, uint64_t &acc,
+                                            uint32_t &err, uint32_t *__restrict__ out, int jcol) {
 #pragma unroll
     for (int w = 7; w >= 0; --w) {
         const uint32_t tag = (uint32_t)w << 11;
         if ((S & SED_TB_WORD) == tag) {
+            // Every op moves the walk at least one step left, so one word yields at most 16 ops: acc (the last 32
+            // ops, position q in bits 1:0) never overflows inside the loop, and the script words completed in it
+            // are stored after it.  A step is then one v_readlane and 12 SALU.
+            const uint32_t qs = q;
             uint32_t code;
             do {
                 // s_lshr takes the low 5 bits of S >> 6: 2 * (step & 15), bit 6 of S being clear inside the tile
                 code = ((uint32_t)__builtin_amdgcn_readlane((int)W[w], (int)S) >> ((S >> 6) & 31u)) & 3u;
                 if (C0 && jcol == 0) code = 3u;
-                acc = (acc << 2) + code;  // the marker too: taken back below
-                if ((--q & 15u) == 0) {
-                    if (q < q0) out[q >> 4] = acc;
-                    else err = SED_ERR_TB_LENGTH;  // ran past the sink's L (the tile still bounds the walk)
-                }
+                acc = (acc << 2) | code;  // the marker too: taken back below
                 if constexpr (C0) jcol -= (int)((5u >> code) & 1u);
                 S -= (uint32_t)(SED_TB_MOVES >> (code << 4));
+                --q;
             } while ((S & SED_TB_WORD) == tag);
-            if (code == 3u) {  // the marker: not an op, the walk stays at the cell before it
+            const bool marker = code == 3u;
+            // opaque: otherwise the compiler keeps the previous acc and q alive through the loop for the undo
+            asm volatile("" : "+s"(acc), "+s"(q));
+            if (marker) {  // not an op: the walk stays at the cell before it
                 acc >>= 2;
-                ++q;  // a word stored at this q is stored again when the walk gets there
-                return (S + 0x8000u) & 0xFFFFu;
+                ++q;
             }
+            // the script word [p, p + 16) completed in this word, if any: [q, qs) holds at most 16 positions, so at most
+            // one p = 16k with q <= p < qs
+            const uint32_t p = (q + 15u) & ~15u;
+            if (q > qs) err = SED_ERR_TB_LENGTH;  // ran past the sink's L (q wrapped; the tile still bounds the walk)
+            else if (p < qs) out[p >> 4] = (uint32_t)(acc >> (2u * (p - q)));
+            if (marker) return (S + 0x8000u) & 0xFFFFu;
         }
     }
     return S & 0xFFFFu;
@@ -1499,14 +1508,15 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
     static_assert((1 << LR) == R, "R in {4, 8, 16}");
     const int n = d.n, m = d.m;
     uint32_t *out = ops + d.ops_off;
-    uint32_t q = q0, acc = 0, err = 0;
+    uint32_t q = q0, err = 0;
+    uint64_t acc = 0;  // the last 32 ops, the latest (position q) in bits 1:0
     auto emit = [&](uint32_t op) {  // sink -> origin (trailing border runs)
         if (q == 0) {
             err = SED_ERR_TB_LENGTH;
             return;
         }
         acc = (acc << 2) | op;
-        if ((--q & 15u) == 0) out[q >> 4] = acc;
+        if ((--q & 15u) == 0) out[q >> 4] = (uint32_t)acc;
     };
     const uint32_t Kd = (prm.del << 16) + 4u, Ki = (prm.ins << 16) + 4u;
     int i = n, j = m;
@@ -1637,8 +1647,8 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
             // ---- walk inside the tile ----
             const uint32_t qin = q;
             const uint32_t S0 = (uint32_t)re | ((uint32_t)sig_end << 7);
-            const uint32_t S = c == 0 ? ck_walk<true>(W, S0, q, acc, err, out, q0, j)
-                                      : ck_walk<false>(W, S0, q, acc, err, out, q0, j);
+            const uint32_t S = c == 0 ? ck_walk<true>(W, S0, q, acc, err, out, j)
+                                      : ck_walk<false>(W, S0, q, acc, err, out, j);
             if (err) break;
             if (q == qin) {  // no progress: give up rather than spin
                 err = SED_ERR_TB_STALL;
