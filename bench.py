@@ -475,7 +475,8 @@ def main():
                    "script": want_script, "pipeline": pipeline and batch.traceback_mode != 2, "mode": batch.mode,
                    "rows_per_lane": batch.rows_per_lane, "lane_pairs": nl, "packed_pairs": npk,
                    "chains": batch.chains,
-                   "traceback": {0: None, 1: "per-cell codes", 2: "checkpoints + recompute"}[batch.traceback_mode],
+                   "traceback": {0: None, 1: "per-cell codes", 2: "checkpoints + recompute",
+                                 3: "per-cell codes, stripe-parallel walk"}[batch.traceback_mode],
                    "parallelism": "dp%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,

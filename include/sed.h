@@ -123,7 +123,8 @@ int sed_batch_rows_per_lane(const sed_batch *b);
 int sed_batch_lane_pairs(const sed_batch *b);         /* pairs on the lane-per-pair kernel (short str2) */
 int sed_batch_chains(const sed_batch *b);             /* CHAIN mode: number of chains (0 = not used) */
 int sed_batch_packed_pairs(const sed_batch *b);       /* pairs computed two per lane / wave (SED_OPT_PACK) */
-int sed_batch_traceback_mode(const sed_batch *b);     /* 0 no script, 1 per-cell codes, 2 checkpoints (SED_OPT_TB) */
+int sed_batch_traceback_mode(const sed_batch *b);     /* 0 no script, 1 per-cell codes, 2 checkpoints (SED_OPT_TB),
+                                                         3 per-cell codes walked stripe-parallel (<= 64 pairs, R = 4) */
 /* CHAIN diagnostics of the last run (waits for it): pairs handed out by the dynamic-CHAIN device counter, and
  * the most pairs one wave computed back to back (0 when CHAIN mode is off). */
 int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave);

@@ -15,7 +15,8 @@ struct sed_pair_desc {
     int32_t n, m;
     int32_t prog_off;  // SPLIT mode: index of stripe 0's progress word
     int32_t lane;      // 1: computed by the lane-per-pair kernel (short str2), the wave kernels skip it
-    int32_t pad[2];
+    int32_t map_off;   // stripe-parallel traceback: word offset of the pair's stripe exit map
+    int32_t pad;
 };
 
 // Per-pair result (16 bytes).
@@ -106,6 +107,8 @@ hipError_t sed_launch_lane_i32x2(const sed_launch &L, const int32_t *idx, int nl
 hipError_t sed_launch_lane_f64(const sed_launch &L, const int32_t *idx, int nidx, const double *gtab, double ins,
                                double del, int K);
 hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops);
+// stripe-parallel traceback of few long pairs (per-cell codes): map[pd.map_off ...] per pair, ops zeroed first
+hipError_t sed_launch_traceback_stripes(const sed_launch &L, uint32_t *ops, uint32_t *map, int items, int kmax);
 // Checkpoint layout of the CK forward kernels (R = 4, 8 or 16 rows per lane, G = 64/R steps per group):
 //   column checkpoints, per stripe [nchunks][R + 1][64 lanes]: each lane's R row values and its top_prev
 //   at every 64-step chunk end;

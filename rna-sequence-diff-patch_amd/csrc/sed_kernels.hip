@@ -1296,38 +1296,39 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
 // the window covers NT = G lanes x NS = R step-groups, i.e. the next ~50-64 steps of any path
 // direction, so one load latency serves them all.  Blocks move from the window's VGPRs to SGPRs
 // with v_readlane when the walk enters them.
-template <int R>
-__global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair_desc *__restrict__ pd,
-                                                                  int npairs, const uint32_t *__restrict__ tb,
-                                                                  sed_result *__restrict__ res,
-                                                                  uint32_t *__restrict__ ops, const uint64_t pat) {
+// The window walk of one pair from cell (i, j), emitting script positions q-1 down, until it reaches row istop
+// (0: the origin, with the trailing border runs).  SEG: one segment of the stripe-parallel traceback, whose
+// script words go through atomicOr (the buffer is zeroed; the first and last words are shared with the
+// neighbouring segments), the last partial word included.  Returns the final q.
+template <int R, bool SEG>
+__device__ __forceinline__ uint32_t window_walk(const sed_pair_desc &d, int i, int j, const int istop, uint32_t q,
+                                                const int lane, const uint32_t *__restrict__ tb,
+                                                uint32_t *__restrict__ out, const uint64_t pat, uint32_t &bad) {
     constexpr int G = Grp<R>::G, NT = G, NS = R;  // NT * NS = 64 blocks
     constexpr int P = Ladder<R>::P;
     constexpr int LR = R == 4 ? 2 : R == 8 ? 3 : R == 16 ? 4 : 5, LG = 6 - LR;
     static_assert((1 << LR) == R, "R must be a power of two in 4..32");
-    const int lane = threadIdx.x;
-    const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x);
-    if (pair >= npairs) return;
-    const sed_pair_desc d = pd[pair];
-    if (d.lane) return;  // scripted by sed_lane.hip
-    const int n = d.n, m = d.m;
+    const int m = d.m;
     const int SG = (m + 63 + G - 1) / G * G;
     const uint64_t stripe_words = (uint64_t)(SG / G) * 256u;
-    uint32_t *out = ops + d.ops_off;
     // ops are emitted sink -> origin, i.e. from position q-1 down; acc = acc<<2 | op leaves the op of
     // position q in bits 1:0 and position q+p in bits 2p+1:2p when a word [q, q+16) completes
-    uint32_t q = (uint32_t)__builtin_amdgcn_readfirstlane(res[pair].len);
-    uint32_t acc = 0, bad = 0;
+    uint32_t acc = 0;
     auto emit = [&](uint32_t op) {
         if (q == 0) {  // longer than the sink's L (integer flag: a wave-uniform walk)
             bad = 1;
             return;
         }
         acc = (acc << 2) | op;
-        if ((--q & 15u) == 0) out[q >> 4] = acc;  // every lane stores the same word (no exec switching)
+        if ((--q & 15u) == 0) {
+            if constexpr (SEG) {
+                if (lane == 0) atomicOr(out + (q >> 4), acc);
+            } else {
+                out[q >> 4] = acc;  // every lane stores the same word (no exec switching)
+            }
+        }
     };
-    int i = n, j = m;
-    if (i > 0 && j > 0) {
+    if (i > istop && j > 0) {
         const int rr = i - 1;
         int k = rr >> (6 + LR);
         int t = (rr >> LR) & 63;
@@ -1361,7 +1362,7 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
             const uint32_t di = (op + 1u) >> 1, dj = (5u >> op) & 1u;  // row move (del, upd), column move (ins, upd)
             i -= (int)di;
             j -= (int)dj;
-            if (min(i, j) == 0) break;
+            if (i == istop || j == 0) break;
             const uint32_t wrap = di & ((r - 1u) >> 31);  // moved up out of the lane's rows (r was 0)
             r = (r - di) & (R - 1);
             const int s_old = s;
@@ -1378,10 +1379,256 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
             }
         }
     }
-    while (j > 0) { emit(0u); --j; }
-    while (i > 0) { emit(1u); --i; }
+    if (istop == 0) {
+        while (j > 0) { emit(0u); --j; }
+        while (i > 0) { emit(1u); --i; }
+    } else {
+        while (i > istop) { emit(1u); --i; }  // the column-0 border inside the segment
+    }
+    if constexpr (SEG) {
+        if ((q & 15u) != 0 && lane == 0) atomicOr(out + (q >> 4), acc << (2u * (q & 15u)));  // last partial word
+    }
+    return q;
+}
+
+template <int R>
+__global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair_desc *__restrict__ pd,
+                                                                  int npairs, const uint32_t *__restrict__ tb,
+                                                                  sed_result *__restrict__ res,
+                                                                  uint32_t *__restrict__ ops, const uint64_t pat) {
+    const int lane = threadIdx.x;
+    const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x);
+    if (pair >= npairs) return;
+    const sed_pair_desc d = pd[pair];
+    if (d.lane) return;  // scripted by sed_lane.hip
+    const uint32_t q0 = (uint32_t)__builtin_amdgcn_readfirstlane(res[pair].len);
+    uint32_t bad = 0;
+    const uint32_t q = window_walk<R, false>(d, d.n, d.m, 0, q0, lane, tb, ops + d.ops_off, pat, bad);
     if ((bad | q) && lane == 0) res[pair].err = SED_ERR_TB_LENGTH;
 }
+
+
+// ---------------------------------------------------------------------------
+// Stripe-parallel traceback for few pairs (per-cell codes; config 2, the GUI: one 4096^2 pair, SPLIT at
+// R = 4, 16 stripes).  The window walk above is one dependent chain of ~4200 steps.  Instead:
+//   map kernel: one lane per (stripe k in 1 .. K-2, column x): walk the codes from cell (last row of stripe
+//     k, x) until the path steps into stripe k-1; record that column and the ops taken.  One more lane walks
+//     the sink's stripe from the sink.  A path through a cell continues the same way whatever led to it (each
+//     code is the cell's canonical op), so these maps compose;
+//   emit kernel: one wave per (pair, stripe): compose the maps from the sink down to its stripe (its entry
+//     column and the script positions of its segment), then walk that segment with the window walk, storing
+//     script words with atomicOr (the two words a segment shares with its neighbours; the buffer is zeroed).
+// ---------------------------------------------------------------------------
+template <int R> struct CodeCursor {  // per-lane reader of one pair's per-cell codes, one 16-byte block cached
+    static constexpr int G = Grp<R>::G, LR = R == 4 ? 2 : R == 8 ? 3 : R == 16 ? 4 : 5, LG = 6 - LR;
+    static constexpr int P = Ladder<R>::P;
+    const uint32_t *base;
+    uint64_t stripe_words;
+    uint4 blk;
+    uint64_t key;
+    __device__ CodeCursor(const uint32_t *b, uint64_t sw) : base(b), stripe_words(sw), blk(make_uint4(0, 0, 0, 0)), key(~0ull) {}
+    // canonical op (0 insert, 1 delete, 2 update) of cell (i, j), 1 <= i, 1 <= j
+    __device__ __forceinline__ uint32_t op(int i, int j, uint64_t pat) {
+        const int rr = i - 1, k = rr >> (6 + LR), t = (rr >> LR) & 63, r = rr & (R - 1);
+        const int s = j - 1 + t;  // the step at which lane t computed column j
+        const uint64_t kk = ((uint64_t)k << 40) | ((uint64_t)(s >> LG) << 6) | (uint64_t)t;
+        if (kk != key) {
+            key = kk;
+            blk = *reinterpret_cast<const uint4 *>(base + (uint64_t)k * stripe_words + ((uint64_t)(s >> LG) * 64u + t) * 4u);
+        }
+        const uint32_t c = ((uint32_t)(s & (G - 1)) << LR) | (uint32_t)r;
+        const uint32_t w = (c & 32u) ? ((c & 16u) ? blk.w : blk.z) : ((c & 16u) ? blk.y : blk.x);
+        return ((w >> (2u * (c & 15u))) - (uint32_t)(pat >> (4 * (i & (P - 1))))) & 3u;
+    }
+};
+
+// map[pd.map_off + 2 * (k * (m + 1) + x)] = {exit column, ops} for stripes 1 .. K-2; the sink's stripe at x = 0.
+// A workgroup takes 256 consecutive columns x0 .. x0+255 of one stripe.  Paths near the diagonal stay in the
+// stripe's 64R rows and within SED_TBMAP_LEFT columns left of x0: the code groups of those steps are one
+// contiguous run of 1 KiB groups (layout [group][64 lanes][16 B]), copied to LDS once, so a step reads LDS
+// instead of waiting on a global load (a wave's lanes need new blocks at different steps: with global loads
+// nearly every step waited on one).  A path that leaves the staged steps (cells far from the diagonal insert
+// first, since ties prefer insert, and can run along the row for thousands of columns) stops: its entry is
+// marked unknown (exit 0xFFFFFFFF) and the emit kernel walks that stripe itself if the real path needs it.
+// The last workgroup of a pair walks the sink's stripe from the sink.  Every workgroup also zeroes its share
+// of the pair's script words, which the emit kernel's segments OR into (lane-kernel pairs wrote theirs already).
+#define SED_TBMAP_LEFT 512
+#define SED_TBMAP_RUN 96
+template <int R>
+__global__ __launch_bounds__(256) void sed_tb_stripemap_kernel(const sed_pair_desc *__restrict__ pd,
+                                                               const uint32_t *__restrict__ tb,
+                                                               uint32_t *__restrict__ map,
+                                                               uint32_t *__restrict__ ops, const uint64_t pat) {
+    constexpr int ROWS = 64 * R, G = Grp<R>::G, LG = CodeCursor<R>::LG, LR = CodeCursor<R>::LR;
+    constexpr int P = Ladder<R>::P;
+    constexpr int NSG = (SED_TBMAP_LEFT + 256 + 64 + 2 * G) / G + 1;  // staged step groups
+    constexpr int NIT = (NSG * 64 + 255) / 256;  // staging trips of the 256 threads
+    __shared__ uint4 stage[NIT * 256];
+    const __attribute__((address_space(3))) uint32_t *stage32 =
+        (const __attribute__((address_space(3))) uint32_t *)(stage);
+    const int p = blockIdx.y;
+    const sed_pair_desc d = pd[p];
+    const int n = d.n, m = d.m;
+    if (d.lane) return;
+    const int tid = threadIdx.x, idx = blockIdx.x * 256 + tid;
+    if (idx < (n + m + 15) / 16) ops[d.ops_off + idx] = 0u;
+    if (n == 0 || m == 0) return;
+    const int K = (n + ROWS - 1) / ROWS;
+    if (K < 3) return;  // walked whole by the emit kernel
+    const int nx = m + 1, nxc = (nx + 255) / 256;
+    const int blk = blockIdx.x;
+    if (blk > (K - 2) * nxc) return;
+    const int SG = (m + 63 + G - 1) / G * G;
+    const uint64_t stripe_words = (uint64_t)(SG / G) * 256u;
+    int k, i, j, slot, x0;
+    bool live;
+    if (blk == (K - 2) * nxc) {  // the sink's stripe, from the sink: the last lane of a block ending at m
+        k = K - 1;
+        x0 = max(0, m - 255);
+        i = n;
+        j = m;
+        slot = k * nx;
+        live = tid == m - x0;
+    } else {
+        k = 1 + blk / nxc;
+        x0 = (blk % nxc) * 256;
+        j = x0 + tid;
+        i = (k + 1) * ROWS;
+        slot = k * nx + j;
+        live = j <= m;
+    }
+    // stage the groups of steps s = j' - 1 + t, j' in [x0 - LEFT, x0 + 255], t in [0, 63]
+    const uint32_t *tbk = tb + d.tb_off + (uint64_t)k * stripe_words;
+    const int s_lo = max(0, x0 - SED_TBMAP_LEFT - 1), s_hi = min(SG - 1, x0 + 255 + 63);
+    const int sg_lo = s_lo >> LG, nsg = min(NSG, (s_hi >> LG) - sg_lo + 1);
+    const uint4 *src = reinterpret_cast<const uint4 *>(tbk) + (uint64_t)sg_lo * 64u;
+    {  // fixed trip count, unguarded stores (clamped loads fill the tail): every load is in flight before the first
+       // wait (guarded stores split the blocks, and the copy ran load, wait, store per trip)
+        uint4 v[NIT];
+#pragma unroll
+        for (int u = 0; u < NIT; ++u) {
+            const int e = tid + 256 * u;
+            v[u] = src[e < nsg * 64 ? e : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < NIT; ++u) stage[tid + 256 * u] = v[u];
+    }
+    __syncthreads();
+    if (!live) return;
+    const int top = k * ROWS;  // row top belongs to stripe k - 1
+    uint32_t cnt = 0, run = 0;  // run: consecutive inserts
+    for (;;) {  // one exit per step (separate exits became nested exec-mask regions); reason decided after
+        const int rr = i - 1, t = (rr >> LR) & 63, r = rr & (R - 1);
+        const int s = j - 1 + t;
+        const uint32_t c = ((uint32_t)(s & (G - 1)) << LR) | (uint32_t)r;
+        // one unconditional ds_read_b32 per step (an LDS-qualified pointer: a generic one became a flat load, and
+        // a uint4 read was split into two branch-guarded halves)
+        const uint32_t rel = (uint32_t)((s >> LG) - sg_lo);
+        const bool inside = rel < (uint32_t)nsg;
+        const uint32_t word = stage32[(inside ? rel : 0u) * 256u + (uint32_t)t * 4u + (c >> 4)];
+        if (!((i > top) & (j > 0) & inside & (run <= SED_TBMAP_RUN))) break;
+        const uint32_t op = ((word >> (2u * (c & 15u))) - (uint32_t)(pat >> (4 * (i & (P - 1))))) & 3u;
+        ++cnt;
+        run = op == 0u ? run + 1u : 0u;
+        i -= (int)(op != 0u);
+        j -= (int)(op != 1u);
+    }
+    if (i > top) {
+        if (j == 0) {  // the column-0 border: deletes up to the stripe above
+            cnt += (uint32_t)(i - top);
+        } else {  // left of the staged steps, or a long run of inserts (a cell far from the diagonal): unknown,
+            j = -1;  // walked by the emit kernel if the real path needs it; the run limit bounds such walks
+            cnt = 0;
+        }
+    }
+    uint32_t *mp = map + (uint32_t)d.map_off + 2u * (uint32_t)slot;
+    mp[0] = (uint32_t)j;  // 0xFFFFFFFF: unknown
+    mp[1] = cnt;
+}
+
+// The exit column and op count of stripe k's segment from cell (i, j), walked here (entries the map kernel left
+// unknown); wave-uniform, codes read one word per step
+template <int R>
+__device__ __forceinline__ uint2 ck_count_walk(const sed_pair_desc &d, const uint32_t *__restrict__ tb, const uint64_t pat,
+                                               const int k, int i, int j) {
+    constexpr int ROWS = 64 * R, G = Grp<R>::G, LG = CodeCursor<R>::LG, LR = CodeCursor<R>::LR, P = Ladder<R>::P;
+    const int SG = (d.m + 63 + G - 1) / G * G;
+    const uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * 256u;
+    const int top = k * ROWS;
+    uint32_t cnt = 0;
+    while (i > top) {
+        if (j == 0) {
+            cnt += (uint32_t)(i - top);
+            break;
+        }
+        const int rr = i - 1, t = (rr >> LR) & 63, r = rr & (R - 1);
+        const int s = j - 1 + t;
+        const uint32_t c = ((uint32_t)(s & (G - 1)) << LR) | (uint32_t)r;
+        const uint32_t word = tbk[((uint64_t)(s >> LG) * 64u + t) * 4u + (c >> 4)];
+        const uint32_t op = ((word >> (2u * (c & 15u))) - (uint32_t)(pat >> (4 * (i & (P - 1))))) & 3u;
+        ++cnt;
+        i -= (int)(op != 0u);
+        j -= (int)(op != 1u);
+    }
+    return make_uint2((uint32_t)j, cnt);
+}
+
+// One wave per (pair, stripe): its segment of the canonical path, from the composed maps (see above; entries the map left unknown are walked here)
+template <int R>
+__global__ __launch_bounds__(64) void sed_tb_stripeemit_kernel(const sed_pair_desc *__restrict__ pd,
+                                                               const uint32_t *__restrict__ tb,
+                                                               sed_result *__restrict__ res,
+                                                               uint32_t *__restrict__ ops,
+                                                               const uint32_t *__restrict__ map, const uint64_t pat) {
+    constexpr int ROWS = 64 * R;
+    const int lane = threadIdx.x;
+    const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x), kme = __builtin_amdgcn_readfirstlane(blockIdx.y);
+    const sed_pair_desc d = pd[pair];
+    if (d.lane) return;
+    const int n = d.n, m = d.m;
+    const int K = n > 0 ? (n + ROWS - 1) / ROWS : 1;
+    const int Keff = (K >= 3 && m > 0) ? K : 1;  // pairs of one or two stripes: one segment, the whole walk
+    if (kme >= Keff) return;
+    const uint32_t L = (uint32_t)__builtin_amdgcn_readfirstlane(res[pair].len);
+    int i0 = n, j0 = m;
+    uint32_t qhi = L, cnt = L;  // cnt: the ops of this segment
+    if (Keff > 1) {
+        const uint32_t nx = (uint32_t)m + 1u;
+        const uint32_t *mp = map + (uint32_t)d.map_off;
+        uint32_t x = mp[2u * ((uint32_t)(K - 1) * nx)];
+        cnt = mp[2u * ((uint32_t)(K - 1) * nx) + 1u];
+        if (x == 0xFFFFFFFFu) {  // the sink's walk left its staged columns
+            const uint2 w = ck_count_walk<R>(d, tb, pat, K - 1, n, m);
+            x = w.x;
+            cnt = w.y;
+        }
+        for (int kk = K - 2; kk >= kme; --kk) {  // down to this stripe: its entry column and script positions
+            qhi -= cnt;
+            const uint32_t e = 2u * ((uint32_t)kk * nx + x);
+            if (kk > 0) {
+                i0 = (kk + 1) * ROWS;
+                j0 = (int)x;
+                uint32_t xn = mp[e];
+                cnt = mp[e + 1u];
+                if (xn == 0xFFFFFFFFu) {
+                    const uint2 w = ck_count_walk<R>(d, tb, pat, kk, i0, j0);
+                    xn = w.x;
+                    cnt = w.y;
+                }
+                x = xn;
+            } else {  // stripe 0: to the origin, whatever is left
+                cnt = qhi;
+                i0 = ROWS;
+                j0 = (int)x;
+            }
+        }
+    }
+    const int istop = (Keff == 1 || kme == 0) ? 0 : kme * ROWS;
+    uint32_t bad = 0;
+    const uint32_t q = window_walk<R, true>(d, i0, j0, istop, qhi, lane, tb, ops + d.ops_off, pat, bad);
+    if ((bad || q != qhi - cnt) && lane == 0) res[pair].err = SED_ERR_TB_LENGTH;
+}
+
 
 // ---------------------------------------------------------------------------
 // Traceback from checkpoints (CK: script batches of the stripe and CHAIN kernels with R = 4, 8 or 16 rows
@@ -1854,6 +2101,27 @@ hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops) {
         CASE(4) CASE(8) CASE(16) CASE(32)
 #undef CASE
     default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// stripe-parallel traceback (few pairs with >= 3 stripes): ops zeroed by the caller; items = the most map lanes
+// of a pair ((K-2)(m+1)+1), kmax = the most stripes of a pair
+hipError_t sed_launch_traceback_stripes(const sed_launch &L, uint32_t *ops, uint32_t *map, int items, int kmax) {
+    // items: map workgroups x 256 of the largest pair, and at least every pair's script words; >= one block
+    const dim3 gmap((max(items, 1) + 255) / 256, L.npairs), gemit(L.npairs, max(kmax, 1));
+    switch (L.R) {
+#define CASE(RR)                                                                                                 \
+    case RR: {                                                                                                   \
+        const uint64_t pat = L.tb_ladder ? Ladder<RR>::pat : 0ull;                                               \
+        hipLaunchKernelGGL((sed_tb_stripemap_kernel<RR>), gmap, dim3(256), 0, L.stream, L.pd, L.tb, map, ops, pat); \
+        hipLaunchKernelGGL((sed_tb_stripeemit_kernel<RR>), gemit, dim3(64), 0, L.stream, L.pd, L.tb, L.res, ops, map, \
+                           pat);                                                                                 \
+        break;                                                                                                   \
+    }
+        CASE(4)
+#undef CASE
+    default: return hipErrorInvalidValue;  // the runtime takes this route at R = 4 only
     }
     return hipGetLastError();
 }

@@ -87,7 +87,9 @@ struct sed_batch {
     std::vector<int32_t> n, m;
     uint64_t tb_words = 0, bnd_words = 0, ops_words = 0;
     double cells = 0, algo_bytes = 0;
-    DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops, d_tasks, d_prog, d_lane, d_chain, d_x2;
+    DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops, d_tasks, d_prog, d_lane, d_chain, d_x2, d_tbmap;
+    bool tbpar = false;        // stripe-parallel traceback (few long pairs, per-cell codes; sed_tb_stripe*_kernel)
+    int tbpar_items = 0, tbpar_kmax = 0;
     bool split = false;
     bool ck = false;           // traceback from checkpoints + recompute (sed_kernels.hip: CK) instead of codes
     int nlane = 0, nwave = 0;  // pairs on the lane-per-pair kernel / on the wave kernels
@@ -118,7 +120,7 @@ struct sed_batch {
 
     int cur() const { return (int)((runs - 1) % nbuf); }
     ~sed_batch() {
-        d_pd.release(); d_seqa.release(); d_seqb.release(); d_bnd.release(); d_ops.release();
+        d_pd.release(); d_seqa.release(); d_seqb.release(); d_bnd.release(); d_ops.release(); d_tbmap.release();
         d_tasks.release(); d_prog.release(); d_lane.release(); d_chain.release(); d_x2.release();
         for (int i = 0; i < 3; ++i) {
             d_tb[i].release();
@@ -288,6 +290,12 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // 20.5-20.8 ms pipelined, profiles/r01_ck/ab_pipeline.jsonl) and saves two traceback buffers.
     static const bool ck_pipe = [] { const char *e = getenv("SED_CK_PIPELINE"); return e && atoi(e) > 0; }();
     if (b->ck && !ck_pipe) b->nbuf = 1;
+    // few pairs with per-cell codes (config 2, the GUI): the traceback walks the stripes of a pair in parallel
+    // (a map of every stripe's exits, then one wave per stripe segment) instead of one ~n+m step chain;
+    // SED_TBPAR=0/1 overrides (A/B)
+    static const int tbpar_env = [] { const char *e = getenv("SED_TBPAR"); return e ? atoi(e) : -1; }();
+    b->tbpar = want_tb && !b->ck && R == 4 && (tbpar_env < 0 ? npairs <= 64 : tbpar_env > 0);
+    b->tbpar_items = b->tbpar_kmax = 0;
 
     // ---- layout ----
     b->pd.assign(npairs, sed_pair_desc{});
@@ -296,7 +304,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // lane-per-pair kernels: integer keys (any flags), or fp64 distance-only in "simple typing" mode
     const bool use_lane = !split && c->opt_lane != 2 &&
                           (mode == SED_MODE_I32 || (mode == SED_MODE_F64 && !want_tb && (flags & SED_NO_LEN)));
-    uint64_t aw = 0, bw = 0, tbw = 0, bndw = 0, opw = 0, progw = 0;
+    uint64_t aw = 0, bw = 0, tbw = 0, bndw = 0, opw = 0, progw = 0, mapw = 0;
     const bool packed = (mode == SED_MODE_I32);
     double cells = 0, in_bytes = 0, tb_bytes = 0, ck_bytes = 0;
     for (int p = 0; p < npairs; ++p) {
@@ -317,6 +325,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         d.bnd_off = bndw;
         d.ops_off = opw;
         d.prog_off = (int32_t)progw;
+        d.map_off = (int32_t)mapw;  // stripe-parallel traceback: this pair's exit map
         if (use_lane && nn >= 1 && nn <= SED_LANE_MAXN && mm >= 1 && mm <= SED_LANE_MAXM) {
             d.lane = 1;
             lane_idx.push_back(p);
@@ -332,12 +341,22 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
                 ck_bytes += 4.0 * (double)w;
             }
             if (nstripes > 1) bndw += (nchunks + 2) * 64 * (packed ? 1 : 4) * (split ? nstripes : 1);
+            if (b->tbpar && nstripes >= 3) {  // {exit column, ops} per stripe and column
+                mapw += nstripes * (uint64_t)(mm + 1) * 2;
+                // workgroups of 256 columns per middle stripe, and one for the sink's stripe
+                b->tbpar_items = std::max<int>(b->tbpar_items, (int)(((nstripes - 2) * ((mm + 256) / 256) + 1) * 256));
+            }
+            b->tbpar_kmax = std::max<int>(b->tbpar_kmax, (int)(nstripes >= 3 ? nstripes : 1));
             if (split) {
                 for (uint64_t k = 0; k < nstripes; ++k) tasks.push_back(make_int2(p, (int)k));
                 progw += nstripes;
             }
         } else if (split) {
             tasks.push_back(make_int2(p, 0));
+        }
+        if (b->tbpar && !d.lane) {
+            b->tbpar_items = std::max<int>(b->tbpar_items, (nn + mm + 15) / 16);  // the map kernel zeroes these
+            b->tbpar_kmax = std::max(b->tbpar_kmax, 1);
         }
         opw += (uint64_t)(nn + mm + 15) / 16;
         cells += (double)nn * mm;
@@ -477,7 +496,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
                    b->d_prog.reserve(4 * std::max<uint64_t>(1, progw)) &&
                    b->d_lane.reserve(4 * std::max<size_t>(1, lane_idx.size())) &&
                    b->d_chain.reserve(4 * (chain_pairs.size() + chain_off.size() + 2)) &&
-                   b->d_x2.reserve(4 * std::max<size_t>(1, x2.size()));
+                   b->d_x2.reserve(4 * std::max<size_t>(1, x2.size())) &&
+                   b->d_tbmap.reserve(4 * std::max<uint64_t>(1, mapw));
     for (int i = 0; i < b->nbuf && okalloc; ++i)
         okalloc = b->d_res[i].reserve(sizeof(sed_result) * std::max(1, npairs)) &&
                   (!want_tb || b->d_tb[i].reserve(4 * std::max<uint64_t>(1, tbw)));
@@ -652,9 +672,14 @@ int run_batch(sed_batch *b) {
         if ((e = hipEventRecord(lg[2], ts)) != hipSuccess) return c->hipfail(e, "event record");
         if (b->nwave > 0) {
             L.stream = ts;
-            if ((e = b->ck ? sed_launch_traceback_ck(L, (uint32_t *)b->d_ops.p, ip)
-                           : sed_launch_traceback(L, (uint32_t *)b->d_ops.p)) != hipSuccess)
-                return c->hipfail(e, "traceback kernel launch");
+            if (b->tbpar) {  // (the map kernel zeroes the scripts the segments OR into)
+                e = sed_launch_traceback_stripes(L, (uint32_t *)b->d_ops.p, (uint32_t *)b->d_tbmap.p, b->tbpar_items,
+                                                 b->tbpar_kmax);
+            } else {
+                e = b->ck ? sed_launch_traceback_ck(L, (uint32_t *)b->d_ops.p, ip)
+                          : sed_launch_traceback(L, (uint32_t *)b->d_ops.p);
+            }
+            if (e != hipSuccess) return c->hipfail(e, "traceback kernel launch");
         }
         if ((e = hipEventRecord(lg[3], ts)) != hipSuccess) return c->hipfail(e, "event record");
     }
@@ -845,7 +870,7 @@ int sed_batch_lane_pairs(const sed_batch *b) { return b ? b->nlane : SED_E_ARG; 
 int sed_batch_chains(const sed_batch *b) { return b ? b->nchains : SED_E_ARG; }
 int sed_batch_traceback_mode(const sed_batch *b) {
     if (!b || !(b->flags & SED_WANT_SCRIPT)) return 0;
-    return b->ck ? 2 : 1;
+    return b->ck ? 2 : (b->tbpar ? 3 : 1);
 }
 
 int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave) {

@@ -177,3 +177,35 @@ def test_repeated_runs_reuse_the_context(gpu, tables):
     for _ in range(300):
         d, ii, ln, ops = gpu.run(packed, True)
     assert np.array_equal(d, first[0]) and np.array_equal(ops, first[3])
+
+
+@pytest.mark.parametrize("R,split", [(4, 0), (4, 2), (8, 2), (16, 2)])
+def test_stripe_parallel_traceback(gpu, tables, R, split):
+    """Few pairs (<= 64) with per-cell codes at R = 4 (config 2's SPLIT route): the traceback maps every stripe's
+    exits (one lane per stripe and column, codes staged in LDS), composes them from the sink and walks the stripe
+    segments in parallel (sed_tb_stripe*_kernel); other R keep the one-chain window walk.
+    Ragged pairs of 1..12 stripes with empty strings, lane-kernel pairs, exits through the column-0 border
+    (n >> m) and segment boundaries inside script words; every op vs the oracle and vs the one-chain walk."""
+    rows = 64 * R
+    A, B = _ragged(5200 + R + split, 9, 1, 12 * rows if R == 4 else 4 * rows, 1, 2600)
+    rng = np.random.default_rng(5300 + R)
+    # (3 rows, 3000) and (4 rows, 4000): insert-heavy paths that leave the map kernel's staged columns
+    for n, m in ((0, 40), (60, 0), (700, 20), (3 * rows, 3), (3 * rows + 1, 2 * rows), (2 * rows, 500), (5 * rows - 1, 17),
+                 (3 * rows, 3000), (4 * rows, 4000)):
+        A.append(rng.integers(0, 4, size=n).astype(np.uint8))
+        B.append(rng.integers(0, 4, size=m).astype(np.uint8))
+    plan = _plan(tables[True])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs(A, B)
+    gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, R)
+    gpu.set_option(sedgpu.SED_OPT_SPLIT, split)
+    try:
+        b, (d, ii, ln, ops) = _batch_run(gpu, packed, True, runs=2)
+        try:
+            assert b.traceback_mode == (3 if R == 4 else 1) and b.rows_per_lane == R  # stripe route at R = 4
+        finally:
+            b.close()
+        _check_all(plan, packed, d, ii, ln, ops, script=True)
+    finally:
+        gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
+        gpu.set_option(sedgpu.SED_OPT_SPLIT, 0)
