@@ -13,10 +13,9 @@ struct sed_pair_desc {
     uint64_t bnd_off;  // stripe bottom-row buffer: uint32 word offset
     uint64_t ops_off;  // packed script: uint32 word offset
     int32_t n, m;
-    int32_t prog_off;  // SPLIT mode: index of stripe 0's progress word
     int32_t lane;      // 1: computed by the lane-per-pair kernel (short str2), the wave kernels skip it
     int32_t map_off;   // stripe-parallel traceback: word offset of the pair's stripe exit map
-    int32_t pad;
+    int32_t pad[2];
 };
 
 // Per-pair result (16 bytes).
@@ -46,7 +45,7 @@ struct sed_i32_params {
     uint32_t costrow16[4];
     uint32_t kins, kdel;
     uint32_t ins, del;
-    uint32_t epoch;  // SPLIT hand-off counters: 1..32767 per run (sed_kernels.hip: wait_progress)
+    uint32_t epoch;  // SPLIT hand-off words' tag: 1..32767 per run (sed_kernels.hip: store_tagged)
     uint32_t pad;
 };
 
@@ -77,7 +76,6 @@ struct sed_launch {
     bool tb_ladder;     // traceback codes of the integer kernels carry the row's ladder rung (sed_kernels.hip)
     bool ck;            // integer R = 16 wave kernel: tb holds checkpoints, the traceback recomputes tiles
     const int2 *tasks;  // SPLIT mode: (pair, stripe) per workgroup, else nullptr
-    uint32_t *prog;     // SPLIT mode: per-stripe published-column counters (zeroed before each run)
     int ntasks;         // 0 -> one wave per pair
     // CHAIN mode: chain c runs pairs chain_pairs[chain_off[c] .. chain_off[c+1]) back to back;
     // with chain_counter set, nchains persistent waves take list entries [0, chain_list) from it

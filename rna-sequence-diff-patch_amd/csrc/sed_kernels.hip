@@ -306,38 +306,25 @@ template <int R> struct I32Waves { static constexpr int value = R >= 32 ? 4 : (R
 #else
 #define SED_I32_WAVES(R) I32Waves<R>::value
 #endif
-// Inter-workgroup hand-off of stripe bottom rows (SPLIT mode; cdna_hip_programming.md §6 G16):
-// producer = every lane's plain stores -> s_waitcnt vmcnt(0) -> lane 0 agent release fence ->
-// s_waitcnt -> relaxed agent store of the published column count; consumer = relaxed agent
-// poll (bounded, s_sleep) -> agent acquire fence -> L1-bypassing sc1 loads.
-// Counter word = poison << 31 | epoch << 16 | columns.  The run's epoch (1..32767, prm.epoch)
-// makes the previous run's counts read as "nothing yet", so the counters need no reset between
-// runs (the host zeroes them when the epoch wraps).  A stripe that gave up waiting publishes
-// with the poison bit; its consumer then stops waiting too, and the last stripe reports err.
+// Inter-workgroup hand-off of stripe bottom rows (SPLIT mode), per 16-step group and self-validating: every
+// bottom-row cell travels as one 64-bit word {tag, value}, stored with a relaxed agent-scope 64-bit atomic
+// (single-copy atomic, so a reader sees the tag and the value of one store together), tag = the run's epoch
+// (1..32767, prm.epoch) | poison << 31.  The consumer loads its next group's words one group ahead (sc1, past
+// its L1) and re-polls any whose tag is not this run's.  No counter, fence or s_waitcnt on the producer side:
+// with the per-chunk counter hand-off (stores, s_waitcnt, release fence, counter; the consumer prefetching a
+// chunk ahead) each stripe ran 3 chunks (192 steps) behind the one above.
+// The previous run's words carry another epoch; the host zeroes the buffer on a batch's first run and when the
+// epoch wraps.  A stripe that gave up waiting publishes with the poison bit, so its consumer stops waiting too,
+// and the last stripe reports err.
 #define SED_PROG_POISON 0x80000000u
-__device__ __forceinline__ void publish_progress(uint32_t *prog, uint32_t tag, uint32_t cols, int lane) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(prog, tag | cols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-__device__ __forceinline__ bool wait_progress(const uint32_t *prog, uint32_t epoch_tag, uint32_t need) {
-    uint32_t spins = 0, v;
-    while (((v = __hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & ~SED_PROG_POISON) <
-           (epoch_tag | need)) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1u << 24)) return false;  // producer never came: give up, flag the pair
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    return !(v & SED_PROG_POISON);
+__device__ __forceinline__ void store_tagged(uint64_t *p, uint32_t tag, uint32_t v) {
+    __hip_atomic_store(p, ((uint64_t)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // SPLIT = false: one wave per pair walks all of its stripes (batches).
 // SPLIT = true : one wave (one 64-thread workgroup) per stripe, all stripes of
-//                a pair run concurrently, each one 3 chunks (192 steps) behind the
-//                stripe above it (single long pairs: config 2, the GUI).
+//                a pair run concurrently, each a few groups behind the stripe
+//                above it (single long pairs: config 2, the GUI; hand-off above).
 // CK (not SPLIT): instead of per-cell codes, tb receives checkpoints for the recompute traceback
 // (sed_traceback_ck_kernel; layout in sed_internal.h): per stripe, at every chunk end each lane's R row values
 // and its top_prev ("column checkpoints", [chunk][R+1][64 lanes]), and every step the bottom row of the lanes
@@ -349,7 +336,7 @@ __device__ __forceinline__ bool wait_progress(const uint32_t *prog, uint32_t epo
 template <int R, bool TB, bool SPLIT, bool LEN = true, bool CK = false>
 __global__ __launch_bounds__(SPLIT ? 64 : 256) __attribute__((amdgpu_waves_per_eu(CK ? SED_CK_WAVES : SED_I32_WAVES(R))))
 void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *__restrict__ tasks,
-                  uint32_t *__restrict__ prog, const uint32_t *__restrict__ seqa, const uint32_t *__restrict__ seqb,
+                  const uint32_t *__restrict__ seqa, const uint32_t *__restrict__ seqb,
                   uint32_t *__restrict__ tb, uint32_t *__restrict__ bnd, sed_result *__restrict__ res,
                   sed_i32_params prm) {
     constexpr int ROWS = 64 * R;
@@ -382,7 +369,7 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
     const int klast = SPLIT ? kfirst : nstripes - 1;
     const int SG = (m + 63 + G - 1) / G * G;  // steps per stripe, rounded to whole groups
     const int nchunks = (SG + 63) >> 6;
-    const uint32_t bstride = (uint32_t)(nchunks + 2) * 64u;  // bottom-row buffer of one stripe (SPLIT)
+    const uint32_t bstride = (uint32_t)(nchunks + 2) * 64u;  // bottom-row buffer of one stripe (SPLIT: 64-bit words)
     const uint32_t *pa = seqa + d.a_off;
     const uint32_t *pb = seqb + d.b_off;
     // the sink cell (n, m): last stripe, lane (n-1)%ROWS / R, row (n-1)%R, computed at step m-1+lane
@@ -400,8 +387,10 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
 
     for (int k = kfirst; k <= klast; ++k) {
         // in-place single buffer per pair when one wave does all stripes; one buffer per stripe otherwise
-        const uint32_t *bnd_in = bnd + d.bnd_off + (SPLIT ? (uint32_t)(k - 1) * bstride : 0u);
-        uint32_t *bnd_out = bnd + d.bnd_off + (SPLIT ? (uint32_t)k * bstride : 0u);
+        const uint32_t *bnd_in = bnd + d.bnd_off;
+        uint32_t *bnd_out = bnd + d.bnd_off;
+        const uint64_t *bin64 = reinterpret_cast<const uint64_t *>(bnd + d.bnd_off) + (uint32_t)(k - 1) * bstride;
+        uint64_t *bout64 = reinterpret_cast<uint64_t *>(bnd + d.bnd_off) + (uint32_t)k * bstride;
         const int row0 = k * ROWS + lane * R;  // 0-based str1 index of this lane's first row
         uint32_t cv[R], V[R];
 #pragma unroll
@@ -423,17 +412,42 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
             const int j = 64 * c + lane + 1;
             if (k == 0) return i32_row0<LEN>();
             if constexpr (CK) return load_sc1(bnd + d.bnd_off + (uint32_t)(j + 62));
-            if constexpr (SPLIT) {  // after one timeout stop waiting: the kernel must still drain quickly
-                if (ok) ok = wait_progress(prog + d.prog_off + k - 1, prm.epoch << 16, (uint32_t)min(m, 64 * c + 64));
-            }
             return load_sc1(bnd_in + j + 64);
+        };
+        // SPLIT: lane u < G loads the tagged word of column s0 + u + 1 for the group starting at step s0 (issued a
+        // group ahead), then every word is checked and re-polled until it carries this run's epoch; the values go
+        // to the LDS ring of lane 0's tops (slot = step & 63).  Columns past m are never stored nor waited for.
+        uint64_t pre = 0;
+        auto fetch_issue = [&](int s0n) {
+            if (lane < G) pre = load_sc1_u64(bin64 + (uint32_t)(s0n + lane + 1 + 64));
+        };
+        auto fetch_finish = [&](int s0n) {
+            const int col = s0n + lane + 1;
+            auto good = [&]() { return lane >= G || col > m || ((uint32_t)(pre >> 32) & ~SED_PROG_POISON) == prm.epoch; };
+            uint32_t spins = 0;
+            while (!__all(good())) {  // after one timeout stop waiting: the kernel must still drain quickly
+                if (!ok || ++spins > (1u << 24)) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                if (!good()) pre = load_sc1_u64(bin64 + (uint32_t)(col + 64));
+            }
+            if (__any(lane < G && col <= m && (pre >> 63))) ok = false;  // poisoned upstream
+            if (lane < G) lch[(s0n + lane) & 63] = (uint32_t)pre;
         };
         auto load_sel = [&](int c) -> uint32_t {
             const int ci = 64 * c + lane;
             return i32_sel((pb[ci >> 4] >> ((ci & 15) * 2)) & 3u);
         };
-        uint32_t tch = load_top(0), sch = load_sel(0);
-        lch[lane] = tch;
+        uint32_t tch = (SPLIT && k > 0) ? 0u : load_top(0), sch = load_sel(0);
+        lch[lane] = tch;  // SPLIT: stripe 0's constant row; the others fetch group by group
+        if constexpr (SPLIT) {
+            if (k > 0) {
+                fetch_issue(0);
+                fetch_finish(0);
+            }
+        }
         ring[lane] = ring[lane + 128] = sch;
         ring[lane + 64] = ring[lane + 192] = i32_sent<LEN>();
         uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * 256u;
@@ -454,7 +468,10 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         int s = 0;
         for (int c = 0; c < nchunks; ++c) {
             uint32_t tnx = 0, snx = 0;
-            if (c + 1 < nchunks) { tnx = load_top(c + 1); snx = load_sel(c + 1); }
+            if (c + 1 < nchunks) {
+                if (!SPLIT) tnx = load_top(c + 1);
+                snx = load_sel(c + 1);
+            }
             const uint32_t *lsel = ring + ((64 * c - lane) & 127);  // this lane's column at the chunk's first step
             auto stores = [&](const int s0) {
                 if constexpr (TB) {
@@ -477,6 +494,8 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                 s = 64 * (c + 1);  // lane 63's bottom cells of the whole chunk are in outc (!CK)
             } else {
                 for (int g = 0; g < 64 / G && s < SG; ++g, s += G, lsel += G) {
+                    const bool fetch = SPLIT && k > 0 && s + G < SG;
+                    if (fetch) fetch_issue(s + G);
                     const bool capg = cap_step >= s && cap_step < s + G;
                     if (capg)
                         i32_group<R, TB, LEN, true, CK>(V, cv, top_prev, bottom, selv, lch, lsel, outc, W, s, lane,
@@ -485,6 +504,13 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                         i32_group<R, TB, LEN, false, CK>(V, cv, top_prev, bottom, selv, lch, lsel, outc, W, s, lane,
                                                          cap_step, cap_lane, cap_row, cap, rcv);
                     stores(s);
+                    if constexpr (SPLIT) {
+                        // lanes 64-G+u hold lane 63's bottom cell of step s+u, column s+u-62 (word col + 64)
+                        if (!last && lane >= 64 - G)
+                            store_tagged(bout64 + (uint32_t)(s + lane - (64 - G) - 62 + 64),
+                                         prm.epoch | (ok ? 0u : SED_PROG_POISON), outc);
+                        if (fetch) fetch_finish(s + G);
+                    }
                 }
             }
             if constexpr (CK) {  // column checkpoint: state after the chunk's last step
@@ -494,15 +520,10 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                 cp[R * 64] = top_prev;
             }
             // lane i holds lane 63's bottom cell of step s-64+i, i.e. column s-126+i at bnd index col+64
-            if (!CK && !last) {
-                bnd_out[s - 62 + lane] = outc;
-                if constexpr (SPLIT)
-                    publish_progress(prog + d.prog_off + k, (prm.epoch << 16) | (ok ? 0u : SED_PROG_POISON),
-                                     (uint32_t)min(m, max(0, s - 63)), lane);
-            }
+            if (!CK && !SPLIT && !last) bnd_out[s - 62 + lane] = outc;
             tch = tnx;
             sch = snx;
-            lch[lane] = tch;  // after the chunk's last LDS read (in order)
+            if (!SPLIT) lch[lane] = tch;  // after the chunk's last LDS read (in order)
             const uint32_t slot = (uint32_t)(64 * (c + 1) + lane) & 127u;  // replaces column 64(c-1) + lane
             ring[slot] = ring[slot + 128] = sch;
         }
@@ -1962,14 +1983,14 @@ template <int R, bool TB, bool LEN = true, bool CK = false>
 static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
     if (L.ntasks > 0) {  // SPLIT: one 64-thread workgroup per (pair, stripe)
         hipLaunchKernelGGL((sed_wf_i32_kernel<R, TB, true, LEN>), dim3(L.ntasks), dim3(64), 0, L.stream, L.pd, L.npairs,
-                           L.tasks, L.prog, (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res,
+                           L.tasks, (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res,
                            prm);
     } else {
         const int grid = (L.npairs + 3) / 4;
         // SED_OCC_LDS (tuning/A-B only): dynamic LDS bytes per workgroup, which caps the resident waves
         static const int occ_lds = [] { const char *e = getenv("SED_OCC_LDS"); return e ? atoi(e) : 0; }();
         hipLaunchKernelGGL((sed_wf_i32_kernel<R, TB, false, LEN, CK>), dim3(grid), dim3(256), occ_lds, L.stream, L.pd, L.npairs,
-                           L.tasks, L.prog, (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res,
+                           L.tasks, (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res,
                            prm);
     }
     return hipGetLastError();

@@ -87,7 +87,7 @@ struct sed_batch {
     std::vector<int32_t> n, m;
     uint64_t tb_words = 0, bnd_words = 0, ops_words = 0;
     double cells = 0, algo_bytes = 0;
-    DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops, d_tasks, d_prog, d_lane, d_chain, d_x2, d_tbmap;
+    DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops, d_tasks, d_lane, d_chain, d_x2, d_tbmap;
     bool tbpar = false;        // stripe-parallel traceback (few long pairs, per-cell codes; sed_tb_stripe*_kernel)
     int tbpar_items = 0, tbpar_kmax = 0;
     bool split = false;
@@ -99,7 +99,6 @@ struct sed_batch {
     size_t chain_npairs = 0;   // d_chain = [chain_pairs (chain_npairs) | chain_off (nchains + 1) | counter]
     bool chain_dyn = false;    // persistent waves + device counter instead of static chains
     int ntasks = 0;
-    uint64_t prog_words = 0;
     // SED_PIPELINE: run k uses traceback/result buffer k%3 and its traceback runs on a second
     // stream, overlapping the DP of run k+1.  Three buffers, so the DP of run k+3 is the first
     // to wait for that traceback: with two, a traceback starved of CUs during the next DP
@@ -121,7 +120,7 @@ struct sed_batch {
     int cur() const { return (int)((runs - 1) % nbuf); }
     ~sed_batch() {
         d_pd.release(); d_seqa.release(); d_seqb.release(); d_bnd.release(); d_ops.release(); d_tbmap.release();
-        d_tasks.release(); d_prog.release(); d_lane.release(); d_chain.release(); d_x2.release();
+        d_tasks.release(); d_lane.release(); d_chain.release(); d_x2.release();
         for (int i = 0; i < 3; ++i) {
             d_tb[i].release();
             d_res[i].release();
@@ -304,7 +303,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // lane-per-pair kernels: integer keys (any flags), or fp64 distance-only in "simple typing" mode
     const bool use_lane = !split && c->opt_lane != 2 &&
                           (mode == SED_MODE_I32 || (mode == SED_MODE_F64 && !want_tb && (flags & SED_NO_LEN)));
-    uint64_t aw = 0, bw = 0, tbw = 0, bndw = 0, opw = 0, progw = 0, mapw = 0;
+    uint64_t aw = 0, bw = 0, tbw = 0, bndw = 0, opw = 0, mapw = 0;
     const bool packed = (mode == SED_MODE_I32);
     double cells = 0, in_bytes = 0, tb_bytes = 0, ck_bytes = 0;
     for (int p = 0; p < npairs; ++p) {
@@ -324,7 +323,6 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         d.tb_off = tbw;
         d.bnd_off = bndw;
         d.ops_off = opw;
-        d.prog_off = (int32_t)progw;
         d.map_off = (int32_t)mapw;  // stripe-parallel traceback: this pair's exit map
         if (use_lane && nn >= 1 && nn <= SED_LANE_MAXN && mm >= 1 && mm <= SED_LANE_MAXM) {
             d.lane = 1;
@@ -340,7 +338,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
                 tbw += w;
                 ck_bytes += 4.0 * (double)w;
             }
-            if (nstripes > 1) bndw += (nchunks + 2) * 64 * (packed ? 1 : 4) * (split ? nstripes : 1);
+            // SPLIT: 64-bit {epoch tag, value} words per column and stripe (the tagged hand-off, sed_kernels.hip)
+            if (nstripes > 1) bndw += (nchunks + 2) * 64 * (packed ? (split ? 2 : 1) : 4) * (split ? nstripes : 1);
             if (b->tbpar && nstripes >= 3) {  // {exit column, ops} per stripe and column
                 mapw += nstripes * (uint64_t)(mm + 1) * 2;
                 // workgroups of 256 columns per middle stripe, and one for the sink's stripe
@@ -349,7 +348,6 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
             b->tbpar_kmax = std::max<int>(b->tbpar_kmax, (int)(nstripes >= 3 ? nstripes : 1));
             if (split) {
                 for (uint64_t k = 0; k < nstripes; ++k) tasks.push_back(make_int2(p, (int)k));
-                progw += nstripes;
             }
         } else if (split) {
             tasks.push_back(make_int2(p, 0));
@@ -462,7 +460,6 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         }
     }
     b->ntasks = (int)tasks.size();
-    b->prog_words = progw;
     b->ops_words = opw;
     b->cells = cells;
     b->algo_bytes = in_bytes + (want_tb ? tb_bytes : 0) + 16.0 * npairs;
@@ -493,7 +490,6 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
                    b->d_seqb.reserve(sb) && b->d_ops.reserve(4 * std::max<uint64_t>(1, opw)) &&
                    b->d_bnd.reserve(4 * std::max<uint64_t>(1, bndw)) &&
                    b->d_tasks.reserve(sizeof(int2) * std::max<size_t>(1, tasks.size())) &&
-                   b->d_prog.reserve(4 * std::max<uint64_t>(1, progw)) &&
                    b->d_lane.reserve(4 * std::max<size_t>(1, lane_idx.size())) &&
                    b->d_chain.reserve(4 * (chain_pairs.size() + chain_off.size() + 2)) &&
                    b->d_x2.reserve(4 * std::max<size_t>(1, x2.size())) &&
@@ -601,7 +597,6 @@ int run_batch(sed_batch *b) {
     L.tb_ladder = b->mode == SED_MODE_I32;
     L.ck = b->ck;
     L.tasks = b->split ? (const int2 *)b->d_tasks.p : nullptr;
-    L.prog = (uint32_t *)b->d_prog.p;
     L.ntasks = b->split ? b->ntasks : 0;
     // buffer k was last read by the traceback of run runs-2
     if (b->nbuf > 1 && want_tb && b->runs >= b->nbuf &&
@@ -610,13 +605,14 @@ int run_batch(sed_batch *b) {
     // Only the event-log records sit between kernels: each record is a packet on the queue, and for
     // the ~50 us lane kernel (config 5) every avoided record is measurable.
     if ((e = hipEventRecord(lg[0], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
-    // SPLIT hand-off counters carry the run's epoch (1..32767), so they are zeroed only when it wraps;
-    // every kernel writes all result fields, err included
+    // SPLIT hand-off words carry the run's epoch (1..32767), so the buffer is zeroed only on a batch's first run
+    // (runs restarts at 0 on every fill) and when the epoch wraps; every kernel writes all result fields, err
+    // included
     sed_i32_params ip = b->ip;
     ip.epoch = (uint32_t)(b->runs % 32767u) + 1u;
-    if (b->split && b->prog_words && ip.epoch == 1 &&
-        (e = hipMemsetAsync(b->d_prog.p, 0, 4 * b->prog_words, c->stream)) != hipSuccess)
-        return c->hipfail(e, "memset progress");
+    if (b->split && b->bnd_words && ip.epoch == 1 &&
+        (e = hipMemsetAsync(b->d_bnd.p, 0, 4 * b->bnd_words, c->stream)) != hipSuccess)
+        return c->hipfail(e, "memset hand-off words");
     const bool len = want_tb || !(b->flags & SED_NO_LEN);
     if (b->nwave_x2 > 0 && (e = sed_launch_i32x2(L, (const int32_t *)b->d_x2.p, b->nwave_x2, ip)) != hipSuccess)
         return c->hipfail(e, "packed DP kernel launch");
@@ -1077,7 +1073,6 @@ int sed_full_matrix(sed_ctx *c, const uint8_t *codes_a, int32_t n, const uint8_t
     L.res = (sed_result *)tmp.d_res[0].p;
     L.R = 4;
     L.tasks = nullptr;
-    L.prog = nullptr;
     L.ntasks = 0;
     L.stream = c->stream;
     sed_full_out fo{(double *)fD.p, (uint8_t *)fM.p, n, m};

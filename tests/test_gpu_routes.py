@@ -209,3 +209,51 @@ def test_stripe_parallel_traceback(gpu, tables, R, split):
     finally:
         gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
         gpu.set_option(sedgpu.SED_OPT_SPLIT, 0)
+
+
+def _same(out, ref, ops_off):
+    """Identical results; scripts compared op by op (words past a script's length are unused padding)."""
+    for name, x, y in zip(("dist", "is_int", "len"), out, ref):
+        assert np.array_equal(x, y), (name, np.flatnonzero(x != y)[:8])
+    bad = [p for p in range(len(ref[2]))
+           if not np.array_equal(sedgpu.unpack_ops(out[3], ops_off, p, int(ref[2][p])),
+                                 sedgpu.unpack_ops(ref[3], ops_off, p, int(ref[2][p])))]
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("R,pipeline", [(4, False), (4, True), (16, False)])
+def test_split_handoff_repeated_runs(gpu, tables, R, pipeline):
+    """SPLIT's stripes hand their bottom rows over as 64-bit {epoch tag, value} words (sed_kernels.hip): words of
+    an earlier run carry another epoch and must never be taken for this run's.  One batch run 40 times (results
+    after each run), and the one-shot path (its scratch batch refilled per call, epoch restarting at 1), must
+    match the oracle every time; the 4096^2 pair is config 2's shape."""
+    A, B = _ragged(5400 + R, 3, 700, 3000, 1, 2600)
+    rng = np.random.default_rng(5410)
+    A.append(rng.integers(0, 4, size=4096).astype(np.uint8))
+    B.append(rng.integers(0, 4, size=4096).astype(np.uint8))
+    plan = _plan(tables[True])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs(A, B)
+    gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, R)
+    gpu.set_option(sedgpu.SED_OPT_SPLIT, 1)
+    try:
+        b = sedgpu.Batch(gpu, packed, True, pipeline=pipeline)
+        try:
+            first = None
+            for _ in range(40):
+                b.run()
+                out = b.results()
+                if first is None:
+                    first = out
+                    _check_all(plan, packed, *out, script=True)
+                else:
+                    _same(out, first, packed.ops_off)
+        finally:
+            b.close()
+        for _ in range(3):
+            out = gpu.run(packed, True)
+            _check_all(plan, packed, *out, script=True)
+            _same(out, first, packed.ops_off)
+    finally:
+        gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
+        gpu.set_option(sedgpu.SED_OPT_SPLIT, 0)
