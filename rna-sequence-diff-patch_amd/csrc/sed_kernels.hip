@@ -12,10 +12,11 @@
 // consecutive rows and sweeps the columns one step behind lane t-1
 // (a systolic anti-diagonal wavefront).  Per step a lane receives the cell
 // above its band from lane t-1 through a DPP wave_shr:1 move, so there is no
-// LDS traffic and no barrier in the inner loop.  Lane 0 takes its "above"
-// value from a 64-entry chunk register that is rotated by DPP wave_rol:1 each
-// step; lane 63's bottom row is collected the same way (wave_shl:1) and written
-// once per 64 steps as the next stripe's top row.
+// barrier in the inner loop.  Lane 0 takes its "above" value (the stripe's top
+// row) and every lane its str2 selector from small per-wave LDS rings, read as
+// broadcasts; lane 63's bottom row is collected by DPP wave_shl:1 and stored as
+// the next stripe's top row (per 64-step chunk in one wave, per 16-step group
+// through tagged words between SPLIT workgroups, below).
 //
 // Integer kernels (the exact fast path).  When every cost is
 // an integral positive Python float (or the int 0 of a match), the reference's
@@ -30,7 +31,8 @@
 //  - distance keys D << 16 - U (U = updates on the path, so at a fixed cell the
 //    low half orders by the path length L = i + j - U): v_perm, v_add, v_min3
 //    = 3 VALU.  Distance-only batches and the checkpoint forward kernel (CK),
-//    whose traceback recomputes tiles in ladder keys converted from them;
+//    whose traceback recomputes tiles in traceback keys (D << 16 | L << 2 | op
+//    in offset space) converted from them;
 //  - 16-bit packed distance keys, two pairs per word (distance only).
 //
 // fp64 kernel (the general path): fp64 candidates added exactly as the
