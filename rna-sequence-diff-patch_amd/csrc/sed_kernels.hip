@@ -1675,7 +1675,7 @@ __global__ __launch_bounds__(64) void sed_tb_stripeemit_kernel(const sed_pair_de
 // goes up and left), and the entry cell's key must carry the path length still to emit: a mismatch (a
 // corrupted checkpoint, SED_OPT_DEBUG_CORRUPT) sets res.err instead of writing a wrong script.  Codes stay
 // in registers, 16 steps per word.  The walk is scalar: one v_readlane per step and the state packed as
-// S = row + (step << 7), 12 SALU per step (a step moves S by 128 / 129 / 257 for insert / delete /
+// S = row + (step << 7), 10 SALU per step (a step moves S by 128 / 129 / 257 for insert / delete /
 // update; one masked compare catches leaving the word, the tile (bit 6 = above it) and the window (code
 // 3)), one unrolled copy per code word since the step only decreases.
 // ---------------------------------------------------------------------------
@@ -1694,31 +1694,38 @@ __device__ __forceinline__ uint32_t ck_walk(const uint32_t (&W)[8], uint32_t S, 
     for (int w = 7; w >= 0; --w) {
         const uint32_t tag = (uint32_t)w << 11;
         if ((S & SED_TB_WORD) == tag) {
-            // Every op moves the walk at least one step left, so one word yields at most 16 ops: acc (the last 32
-            // ops, position q in bits 1:0) never overflows inside the loop, and the script words completed in it
-            // are stored after it.  A step is then one v_readlane and 12 SALU.
+            // Every op moves the walk at least one step left, so one word yields at most 16 ops.  Inside the loop
+            // the state is carried as T = S - tag (same low 11 bits: lane and shift), so leaving the word, the tile or
+            // the window is (T & SED_TB_WORD) != 0, one s_and that sets SCC; the codes collect in a 32-bit lo
+            // (s_lshl2_add_u32), which holds all of them, and go onto the 64-bit acc (the last 32 ops) after the
+            // loop, where the script word completed in it, if any, is stored.  A step is one v_readlane and 10 SALU.
             const uint32_t qs = q;
-            uint32_t code;
+            uint32_t T = S - tag, lo = 0, code;
             do {
-                // s_lshr takes the low 5 bits of S >> 6: 2 * (step & 15), bit 6 of S being clear inside the tile
-                code = ((uint32_t)__builtin_amdgcn_readlane((int)W[w], (int)S) >> ((S >> 6) & 31u)) & 3u;
+                // s_lshr takes the low 5 bits of T >> 6: 2 * (step & 15), bit 6 being clear inside the tile
+                code = ((uint32_t)__builtin_amdgcn_readlane((int)W[w], (int)T) >> ((T >> 6) & 31u)) & 3u;
                 if (C0 && jcol == 0) code = 3u;
-                acc = (acc << 2) | code;  // the marker too: taken back below
+                // the marker too: taken back below (asm: the compiler emits s_lshl + s_or; the op writes SCC)
+                asm("s_lshl2_add_u32 %0, %1, %2" : "=s"(lo) : "s"(lo), "s"(code) : "scc");
                 if constexpr (C0) jcol -= (int)((5u >> code) & 1u);
-                S -= (uint32_t)(SED_TB_MOVES >> (code << 4));
+                T -= (uint32_t)(SED_TB_MOVES >> (code << 4));
                 --q;
-            } while ((S & SED_TB_WORD) == tag);
+            } while ((T & SED_TB_WORD) == 0u);
+            S = T + tag;
             const bool marker = code == 3u;
-            // opaque: otherwise the compiler keeps the previous acc and q alive through the loop for the undo
-            asm volatile("" : "+s"(acc), "+s"(q));
+            // opaque: otherwise the compiler keeps the previous lo and q alive through the loop for the undo
+            asm volatile("" : "+s"(lo), "+s"(q));
             if (marker) {  // not an op: the walk stays at the cell before it
-                acc >>= 2;
+                lo >>= 2;
                 ++q;
             }
+            // lo started at 0 and holds exactly this word's ops (at most 16)
+            const uint32_t nw = qs - q;
+            acc = (acc << (2u * nw)) | lo;
             // the script word [p, p + 16) completed in this word, if any: [q, qs) holds at most 16 positions, so at most
             // one p = 16k with q <= p < qs
             const uint32_t p = (q + 15u) & ~15u;
-            if (q > qs) err = SED_ERR_TB_LENGTH;  // ran past the sink's L (q wrapped; the tile still bounds the walk)
+            if ((int32_t)nw < 0) err = SED_ERR_TB_LENGTH;  // ran past the sink's L (q wrapped; the tile bounds the walk)
             else if (p < qs) out[p >> 4] = (uint32_t)(acc >> (2u * (p - q)));
             if (marker) return (S + 0x8000u) & 0xFFFFu;
         }
