@@ -63,6 +63,11 @@ struct sed_full_out {
     int32_t n, m;
 };
 
+// a kernel launch of a sed_launch phase, carrying its events (see sed_launch::ev0 / ev1); the .hip files that
+// use it include <hip/hip_ext.h> (the host-compiled runtime does not)
+#define SED_LAUNCH(kernel, grid, block, shmem, L, ...) \
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, (L).stream, (L).ev0, (L).ev1, 0, __VA_ARGS__)
+
 struct sed_launch {
     const sed_pair_desc *pd;
     int npairs;
@@ -75,6 +80,10 @@ struct sed_launch {
     hipStream_t stream;
     bool tb_ladder;     // traceback codes of the integer kernels carry the row's ladder rung (sed_kernels.hip)
     bool ck;            // integer R = 16 wave kernel: tb holds checkpoints, the traceback recomputes tiles
+    // timing events carried by the launches themselves (hipExtLaunchKernelGGL: timestamps on the dispatch
+    // packet, no marker packet between kernels): the launcher's first kernel records ev0 at its start, its last
+    // kernel ev1 at its end; nullptr = none
+    hipEvent_t ev0, ev1;
     const int2 *tasks;  // SPLIT mode: (pair, stripe) per workgroup, else nullptr
     int ntasks;         // 0 -> one wave per pair
     // CHAIN mode: chain c runs pairs chain_pairs[chain_off[c] .. chain_off[c+1]) back to back;

@@ -42,6 +42,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <type_traits>
+#include <hip/hip_ext.h>
 #include "sed_internal.h"
 
 #define DPP_WAVE_SHL1 0x130  // lane i <- lane i+1, lane 63 keeps `old`
@@ -1991,14 +1992,14 @@ __global__ void sed_selftest_kernel(uint32_t *out) {
 template <int R, bool TB, bool LEN = true, bool CK = false>
 static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
     if (L.ntasks > 0) {  // SPLIT: one 64-thread workgroup per (pair, stripe)
-        hipLaunchKernelGGL((sed_wf_i32_kernel<R, TB, true, LEN>), dim3(L.ntasks), dim3(64), 0, L.stream, L.pd, L.npairs,
+        SED_LAUNCH((sed_wf_i32_kernel<R, TB, true, LEN>), dim3(L.ntasks), dim3(64), 0, L, L.pd, L.npairs,
                            L.tasks, (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res,
                            prm);
     } else {
         const int grid = (L.npairs + 3) / 4;
         // SED_OCC_LDS (tuning/A-B only): dynamic LDS bytes per workgroup, which caps the resident waves
         static const int occ_lds = [] { const char *e = getenv("SED_OCC_LDS"); return e ? atoi(e) : 0; }();
-        hipLaunchKernelGGL((sed_wf_i32_kernel<R, TB, false, LEN, CK>), dim3(grid), dim3(256), occ_lds, L.stream, L.pd, L.npairs,
+        SED_LAUNCH((sed_wf_i32_kernel<R, TB, false, LEN, CK>), dim3(grid), dim3(256), occ_lds, L, L.pd, L.npairs,
                            L.tasks, (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res,
                            prm);
     }
@@ -2007,7 +2008,7 @@ static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
 
 template <int R, bool TB, bool LEN, bool CK = false>
 static hipError_t launch_chain_R(const sed_launch &L, const sed_i32_params &prm) {
-    hipLaunchKernelGGL((sed_wf_i32_chain_kernel<R, TB, LEN, CK>), dim3((L.nchains + 3) / 4), dim3(256), 0, L.stream, L.pd,
+    SED_LAUNCH((sed_wf_i32_chain_kernel<R, TB, LEN, CK>), dim3((L.nchains + 3) / 4), dim3(256), 0, L, L.pd,
                        L.chain_pairs, L.chain_off, L.nchains, L.chain_counter, L.chain_list,
                        (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.res, prm);
     return hipGetLastError();
@@ -2039,10 +2040,10 @@ hipError_t sed_launch_i32x2(const sed_launch &L, const int32_t *list, int nwaves
     const dim3 grid((nwaves + 3) / 4), block(256);
     const uint32_t *a = (const uint32_t *)L.seqa, *b = (const uint32_t *)L.seqb;
     switch (L.R) {
-    case 4: hipLaunchKernelGGL((sed_wf_i32x2_kernel<4>), grid, block, 0, L.stream, L.pd, list, nwaves, a, b, L.bnd, L.res, prm); break;
-    case 8: hipLaunchKernelGGL((sed_wf_i32x2_kernel<8>), grid, block, 0, L.stream, L.pd, list, nwaves, a, b, L.bnd, L.res, prm); break;
-    case 16: hipLaunchKernelGGL((sed_wf_i32x2_kernel<16>), grid, block, 0, L.stream, L.pd, list, nwaves, a, b, L.bnd, L.res, prm); break;
-    case 32: hipLaunchKernelGGL((sed_wf_i32x2_kernel<32>), grid, block, 0, L.stream, L.pd, list, nwaves, a, b, L.bnd, L.res, prm); break;
+    case 4: SED_LAUNCH((sed_wf_i32x2_kernel<4>), grid, block, 0, L, L.pd, list, nwaves, a, b, L.bnd, L.res, prm); break;
+    case 8: SED_LAUNCH((sed_wf_i32x2_kernel<8>), grid, block, 0, L, L.pd, list, nwaves, a, b, L.bnd, L.res, prm); break;
+    case 16: SED_LAUNCH((sed_wf_i32x2_kernel<16>), grid, block, 0, L, L.pd, list, nwaves, a, b, L.bnd, L.res, prm); break;
+    case 32: SED_LAUNCH((sed_wf_i32x2_kernel<32>), grid, block, 0, L, L.pd, list, nwaves, a, b, L.bnd, L.res, prm); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -2074,7 +2075,7 @@ template <int R, bool TB, bool TYPED, bool FULL = false>
 static hipError_t launch_f64_R(const sed_launch &L, const double *gtab, const sed_f64_params &prm,
                                const sed_full_out &fo = sed_full_out{}) {
     const int grid = (L.npairs + 3) / 4;
-    hipLaunchKernelGGL((sed_wf_f64_kernel<R, TB, TYPED, FULL>), dim3(grid), dim3(256), 0, L.stream, L.pd, L.npairs,
+    SED_LAUNCH((sed_wf_f64_kernel<R, TB, TYPED, FULL>), dim3(grid), dim3(256), 0, L, L.pd, L.npairs,
                        (const uint8_t *)L.seqa, (const uint8_t *)L.seqb, L.tb, L.bnd, L.res, gtab, prm, fo);
     return hipGetLastError();
 }
@@ -2104,9 +2105,9 @@ hipError_t sed_launch_traceback_ck(const sed_launch &L, uint32_t *ops, const sed
     const dim3 grid(L.npairs), block(64);
     const uint32_t *a = (const uint32_t *)L.seqa, *b = (const uint32_t *)L.seqb;
     switch (L.R) {
-    case 4: hipLaunchKernelGGL(sed_traceback_ck_kernel<4>, grid, block, 0, L.stream, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
-    case 8: hipLaunchKernelGGL(sed_traceback_ck_kernel<8>, grid, block, 0, L.stream, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
-    case 16: hipLaunchKernelGGL(sed_traceback_ck_kernel<16>, grid, block, 0, L.stream, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
+    case 4: SED_LAUNCH(sed_traceback_ck_kernel<4>, grid, block, 0, L, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
+    case 8: SED_LAUNCH(sed_traceback_ck_kernel<8>, grid, block, 0, L, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
+    case 16: SED_LAUNCH(sed_traceback_ck_kernel<16>, grid, block, 0, L, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -2121,10 +2122,10 @@ hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops) {
     case RR: {                                                                                                   \
         const uint64_t pat = L.tb_ladder ? Ladder<RR>::pat : 0ull;                                               \
         if (uni)                                                                                                 \
-            hipLaunchKernelGGL((sed_traceback_window_kernel<RR>), dim3(grid), dim3(64), 0, L.stream, L.pd,       \
+            SED_LAUNCH((sed_traceback_window_kernel<RR>), dim3(grid), dim3(64), 0, L, L.pd,       \
                                L.npairs, L.tb, L.res, ops, pat);                                                \
         else                                                                                                     \
-            hipLaunchKernelGGL((sed_traceback_kernel<RR>), dim3(grid), dim3(64), 0, L.stream, L.pd,              \
+            SED_LAUNCH((sed_traceback_kernel<RR>), dim3(grid), dim3(64), 0, L, L.pd,              \
                                L.npairs, L.tb, L.res, ops, pat);                                                \
         break;                                                                                                   \
     }
@@ -2144,8 +2145,8 @@ hipError_t sed_launch_traceback_stripes(const sed_launch &L, uint32_t *ops, uint
 #define CASE(RR)                                                                                                 \
     case RR: {                                                                                                   \
         const uint64_t pat = L.tb_ladder ? Ladder<RR>::pat : 0ull;                                               \
-        hipLaunchKernelGGL((sed_tb_stripemap_kernel<RR>), gmap, dim3(256), 0, L.stream, L.pd, L.tb, map, ops, pat); \
-        hipLaunchKernelGGL((sed_tb_stripeemit_kernel<RR>), gemit, dim3(64), 0, L.stream, L.pd, L.tb, L.res, ops, map, \
+        hipExtLaunchKernelGGL((sed_tb_stripemap_kernel<RR>), gmap, dim3(256), 0, L.stream, L.ev0, nullptr, 0, L.pd, L.tb, map, ops, pat); \
+        hipExtLaunchKernelGGL((sed_tb_stripeemit_kernel<RR>), gemit, dim3(64), 0, L.stream, nullptr, L.ev1, 0, L.pd, L.tb, L.res, ops, map, \
                            pat);                                                                                 \
         break;                                                                                                   \
     }

@@ -14,6 +14,7 @@
 //   !LEN: distance only, no L/op field: left, up, diag + perm(costrow, -1, sel)      (3 VALU)
 // TB (implies LEN): the op of every cell (2 bits, 32 per row = one uint2) is stored per pair,
 // row-major, and the same lane walks it back from (n, m) to write the canonical script.
+#include <hip/hip_ext.h>
 #include "sed_internal.h"
 
 namespace {
@@ -288,14 +289,14 @@ __global__ __launch_bounds__(256) void sed_lane_f64_kernel(const sed_pair_desc *
 hipError_t sed_launch_lane_f64(const sed_launch &L, const int32_t *idx, int nidx, const double *gtab, double ins,
                                double del, int K) {
     if (nidx <= 0) return hipSuccess;
-    hipLaunchKernelGGL((sed_lane_f64_kernel<SED_LANE_MAXM>), dim3((nidx + 255) / 256), dim3(256), 0, L.stream, L.pd,
+    SED_LAUNCH((sed_lane_f64_kernel<SED_LANE_MAXM>), dim3((nidx + 255) / 256), dim3(256), 0, L, L.pd,
                        idx, nidx, (const uint8_t *)L.seqa, (const uint8_t *)L.seqb, L.res, gtab, ins, del, K);
     return hipGetLastError();
 }
 
 hipError_t sed_launch_lane_i32x2(const sed_launch &L, const int32_t *idx, int nlanes, const sed_i32_params &prm) {
     if (nlanes <= 0) return hipSuccess;
-    hipLaunchKernelGGL(sed_lane_i32x2_kernel, dim3((nlanes + 255) / 256), dim3(256), 0, L.stream, L.pd, idx, nlanes,
+    SED_LAUNCH(sed_lane_i32x2_kernel, dim3((nlanes + 255) / 256), dim3(256), 0, L, L.pd, idx, nlanes,
                        (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.res, prm);
     return hipGetLastError();
 }
@@ -306,13 +307,13 @@ hipError_t sed_launch_lane_i32(const sed_launch &L, const int32_t *idx, int nidx
     const dim3 grid((nidx + 255) / 256), block(256);
     const uint32_t *a = (const uint32_t *)L.seqa, *b = (const uint32_t *)L.seqb;
     if (L.tb)
-        hipLaunchKernelGGL((sed_lane_i32_kernel<true, true>), grid, block, 0, L.stream, L.pd, idx, nidx, a, b, L.tb,
+        SED_LAUNCH((sed_lane_i32_kernel<true, true>), grid, block, 0, L, L.pd, idx, nidx, a, b, L.tb,
                            L.ops, L.res, prm);
     else if (len)
-        hipLaunchKernelGGL((sed_lane_i32_kernel<true, false>), grid, block, 0, L.stream, L.pd, idx, nidx, a, b,
+        SED_LAUNCH((sed_lane_i32_kernel<true, false>), grid, block, 0, L, L.pd, idx, nidx, a, b,
                            nullptr, nullptr, L.res, prm);
     else
-        hipLaunchKernelGGL((sed_lane_i32_kernel<false, false>), grid, block, 0, L.stream, L.pd, idx, nidx, a, b,
+        SED_LAUNCH((sed_lane_i32_kernel<false, false>), grid, block, 0, L, L.pd, idx, nidx, a, b,
                            nullptr, nullptr, L.res, prm);
     return hipGetLastError();
 }

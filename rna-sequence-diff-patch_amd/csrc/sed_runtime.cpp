@@ -598,13 +598,24 @@ int run_batch(sed_batch *b) {
     L.ck = b->ck;
     L.tasks = b->split ? (const int2 *)b->d_tasks.p : nullptr;
     L.ntasks = b->split ? b->ntasks : 0;
-    // buffer k was last read by the traceback of run runs-2
-    if (b->nbuf > 1 && want_tb && b->runs >= b->nbuf &&
+    // buffer k was last read by the traceback of run runs-3: wait for it unless it has finished already (a
+    // cross-queue wait is a barrier packet between this run's kernel and the previous one)
+    if (b->nbuf > 1 && want_tb && b->runs >= b->nbuf && hipEventQuery(b->evk[k][3]) != hipSuccess &&
         (e = hipStreamWaitEvent(c->stream, b->evk[k][3], 0)) != hipSuccess)
         return c->hipfail(e, "stream wait");
-    // Only the event-log records sit between kernels: each record is a packet on the queue, and for
-    // the ~50 us lane kernel (config 5) every avoided record is measurable.
-    if ((e = hipEventRecord(lg[0], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
+    // The event log's timestamps ride on the kernels' own dispatch packets (SED_LAUNCH: the DP phase's first
+    // kernel records lg[0] at its start and its last kernel lg[1] at its end; the same for the traceback phase
+    // with lg[2] / lg[3]).  An event record is a marker packet on the queue: with records around the kernels,
+    // consecutive config-2 DP kernels were ~18 us apart, and for the ~25 us lane kernel (config 5) every
+    // avoided packet is measurable.  A phase that launches nothing records its events directly.
+    const int ndp = (b->nwave_x2 > 0) + (b->nwave > 0) + (b->nlane > 0);
+    int idp = 0;
+    auto dp_events = [&]() {
+        L.ev0 = idp == 0 ? lg[0] : nullptr;
+        L.ev1 = idp == ndp - 1 ? lg[1] : nullptr;
+        ++idp;
+    };
+    if (ndp == 0 && (e = hipEventRecord(lg[0], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
     // SPLIT hand-off words carry the run's epoch (1..32767), so the buffer is zeroed only on a batch's first run
     // (runs restarts at 0 on every fill) and when the epoch wraps; every kernel writes all result fields, err
     // included
@@ -614,9 +625,13 @@ int run_batch(sed_batch *b) {
         (e = hipMemsetAsync(b->d_bnd.p, 0, 4 * b->bnd_words, c->stream)) != hipSuccess)
         return c->hipfail(e, "memset hand-off words");
     const bool len = want_tb || !(b->flags & SED_NO_LEN);
-    if (b->nwave_x2 > 0 && (e = sed_launch_i32x2(L, (const int32_t *)b->d_x2.p, b->nwave_x2, ip)) != hipSuccess)
-        return c->hipfail(e, "packed DP kernel launch");
+    if (b->nwave_x2 > 0) {
+        dp_events();
+        if ((e = sed_launch_i32x2(L, (const int32_t *)b->d_x2.p, b->nwave_x2, ip)) != hipSuccess)
+            return c->hipfail(e, "packed DP kernel launch");
+    }
     if (b->nwave > 0) {
+        dp_events();
         if (b->mode == SED_MODE_I32 && b->nchains) {
             L.chain_pairs = (const int32_t *)b->d_chain.p;
             L.chain_off = (const int32_t *)b->d_chain.p + b->chain_npairs;
@@ -636,6 +651,7 @@ int run_batch(sed_batch *b) {
         if (e != hipSuccess) return c->hipfail(e, "DP kernel launch");
     }
     if (b->nlane > 0) {
+        dp_events();
         if (b->nlane_x2 > 0)
             e = sed_launch_lane_i32x2(L, (const int32_t *)b->d_lane.p, b->nlane_x2, ip);
         else if (b->mode == SED_MODE_I32)
@@ -645,7 +661,8 @@ int run_batch(sed_batch *b) {
                                     c->del, c->K);
         if (e != hipSuccess) return c->hipfail(e, "lane kernel launch");
     }
-    if ((e = hipEventRecord(lg[1], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
+    if (ndp == 0 && (e = hipEventRecord(lg[1], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
+    L.ev0 = L.ev1 = nullptr;
     if (want_tb && b->ck && c->opt_debug_corrupt > 0 && c->opt_debug_corrupt <= b->npairs) {
         // SED_OPT_DEBUG_CORRUPT: overwrite the column checkpoint of the sink's row in the chunk before the
         // sink's tile with the smallest distance key (D offset 0, no updates), which the recompute then
@@ -665,9 +682,11 @@ int run_batch(sed_batch *b) {
     }
     if (want_tb) {
         if (ts != c->stream && (e = hipStreamWaitEvent(ts, lg[1], 0)) != hipSuccess) return c->hipfail(e, "stream wait");
-        if ((e = hipEventRecord(lg[2], ts)) != hipSuccess) return c->hipfail(e, "event record");
+        if (b->nwave == 0 && (e = hipEventRecord(lg[2], ts)) != hipSuccess) return c->hipfail(e, "event record");
         if (b->nwave > 0) {
             L.stream = ts;
+            L.ev0 = lg[2];
+            L.ev1 = lg[3];
             if (b->tbpar) {  // (the map kernel zeroes the scripts the segments OR into)
                 e = sed_launch_traceback_stripes(L, (uint32_t *)b->d_ops.p, (uint32_t *)b->d_tbmap.p, b->tbpar_items,
                                                  b->tbpar_kmax);
@@ -677,7 +696,7 @@ int run_batch(sed_batch *b) {
             }
             if (e != hipSuccess) return c->hipfail(e, "traceback kernel launch");
         }
-        if ((e = hipEventRecord(lg[3], ts)) != hipSuccess) return c->hipfail(e, "event record");
+        if (b->nwave == 0 && (e = hipEventRecord(lg[3], ts)) != hipSuccess) return c->hipfail(e, "event record");
     }
     b->evk[k] = lg;
     ++b->runs;
