@@ -91,6 +91,7 @@ struct sed_launch {
     const int32_t *chain_pairs, *chain_off;
     int nchains;
     uint32_t *chain_counter;
+    uint32_t chain_base;  // the counter's value when this run starts (it is never reset between runs)
     int chain_list;
 };
 

@@ -805,7 +805,7 @@ template <int R, bool TB, bool LEN, bool CK = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainWaves<R>::value))) void
 sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restrict__ chain_pairs,
                         const int32_t *__restrict__ chain_off, int nchains, uint32_t *__restrict__ counter,
-                        int nlist, const uint32_t *__restrict__ seqa, const uint32_t *__restrict__ seqb,
+                        uint32_t cbase, int nlist, const uint32_t *__restrict__ seqa, const uint32_t *__restrict__ seqb,
                         uint32_t *__restrict__ tb, sed_result *__restrict__ res, sed_i32_params prm) {
     constexpr int G = Grp<R>::G;
     static_assert(!CK || (!TB && !LEN), "checkpoints: distance keys, no codes");
@@ -814,10 +814,12 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
     if (chain >= nchains) return;
     // Static chains: list entries [chain_off[c], chain_off[c+1]).  Dynamic (counter != null):
     // persistent waves take the next list entry from a device counter whenever lane 0 reaches
-    // the end of a pair, so every wave stays busy until the list is exhausted.
+    // the end of a pair, so every wave stays busy until the list is exhausted.  A run takes exactly
+    // nlist + nchains values (every wave ends with one failed grab), so the counter is never reset:
+    // this run's values start at cbase (no fill kernel per run).
     auto grab = [&]() -> int {
         uint32_t v = 0;
-        if (lane == 0) v = atomicAdd(counter, 1u);
+        if (lane == 0) v = atomicAdd(counter, 1u) - cbase;
         return (int)__builtin_amdgcn_readfirstlane(v);
     };
     int c0, c1;
@@ -2009,7 +2011,7 @@ static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
 template <int R, bool TB, bool LEN, bool CK = false>
 static hipError_t launch_chain_R(const sed_launch &L, const sed_i32_params &prm) {
     SED_LAUNCH((sed_wf_i32_chain_kernel<R, TB, LEN, CK>), dim3((L.nchains + 3) / 4), dim3(256), 0, L, L.pd,
-                       L.chain_pairs, L.chain_off, L.nchains, L.chain_counter, L.chain_list,
+                       L.chain_pairs, L.chain_off, L.nchains, L.chain_counter, L.chain_base, L.chain_list,
                        (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.res, prm);
     return hipGetLastError();
 }

@@ -638,9 +638,10 @@ int run_batch(sed_batch *b) {
             L.nchains = b->nchains;
             L.chain_list = (int)b->chain_npairs;
             L.chain_counter = nullptr;
-            if (b->chain_dyn) {
+            if (b->chain_dyn) {  // zeroed on a batch's first run only: a run takes list + waves values
                 L.chain_counter = (uint32_t *)b->d_chain.p + b->chain_npairs + 1;
-                if ((e = hipMemsetAsync(L.chain_counter, 0, 4, c->stream)) != hipSuccess)
+                L.chain_base = (uint32_t)((uint64_t)b->runs * (uint64_t)(b->chain_npairs + b->nchains));
+                if (b->runs == 0 && (e = hipMemsetAsync(L.chain_counter, 0, 4, c->stream)) != hipSuccess)
                     return c->hipfail(e, "reset chain counter");
             }
             e = sed_launch_i32_chain(L, ip, len);
@@ -898,12 +899,13 @@ int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave)
     int32_t f = 0, mx = 0;
     if (b->nchains > 0 && b->npairs > 0) {
         hipError_t e;
-        if (b->chain_dyn) {  // every persistent wave ends with one failed grab: counter = list + waves
+        if (b->chain_dyn && b->runs > 0) {  // every persistent wave ends with one failed grab: a run takes list + waves
             uint32_t cnt = 0;
             if ((e = hipMemcpy(&cnt, (uint32_t *)b->d_chain.p + b->chain_npairs + 1, 4, hipMemcpyDeviceToHost)) !=
                 hipSuccess)
                 return c->hipfail(e, "download chain counter");
-            f = (int32_t)cnt - b->nchains;
+            const uint32_t base = (uint32_t)((uint64_t)(b->runs - 1) * (uint64_t)(b->chain_npairs + b->nchains));
+            f = (int32_t)(cnt - base) - b->nchains;
         }
         std::vector<sed_result> h(b->npairs);
         if ((e = hipMemcpy(h.data(), b->d_res[b->cur()].p, sizeof(sed_result) * b->npairs, hipMemcpyDeviceToHost)) !=

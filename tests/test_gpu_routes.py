@@ -96,7 +96,8 @@ def test_dynamic_chain_config3_route(gpu, tables, user):
 
 def test_dynamic_chain_capped_waves(gpu, tables):
     """The same route with the persistent waves capped (SED_OPT_CHAIN_WAVES = 300): ~30 fetched pairs per
-    wave, so every wave crosses many pair switches; scripts and lengths vs the oracle."""
+    wave, so every wave crosses many pair switches; scripts and lengths vs the oracle.  Each batch runs three
+    times (the pair counter is not reset between runs: a run's values start at runs * (list + waves))."""
     A, B = _ragged(3100, 9000, 1, 512, 33, 700)
     plan = _plan(tables[True])
     gpu.set_costs(plan)
@@ -106,7 +107,7 @@ def test_dynamic_chain_capped_waves(gpu, tables):
     try:
         for tb in (0, 2):  # per-cell codes, then checkpoints
             gpu.set_option(sedgpu.SED_OPT_TB, tb)
-            b, (d, ii, ln, ops) = _batch_run(gpu, packed, True)
+            b, (d, ii, ln, ops) = _batch_run(gpu, packed, True, pipeline=tb == 0, runs=3)
             try:
                 assert b.chains == 300 and b.traceback_mode == (2 if tb else 1)
                 fetched, per_wave = b.chain_stats()
