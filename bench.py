@@ -43,7 +43,7 @@ SIMDS, CLOCK = 1024, 2.4e9
 # keys: perm + pk_add + 2 pk_min per 2 cells.  Checkpoint script batches (traceback mode 2) run the distance
 # keys (D << 16 - U carries the path length; the traceback recomputes the op tie-break): "nolen".
 VALU_CYCLES_PER_OP = 4.0
-CELL_OPS = {"script": 5 + 3 / 16, "len": 4 + 3 / 16, "nolen": 3, "nolen_x2": 2}
+CELL_OPS = {"script": 5 + 3 / 16, "len": 4 + 3 / 16, "nolen": 3, "nolen_x2": 2, "dot": 2}
 
 WORKLOADS = {
     # name: (pairs per GPU, n, m, cost table, description)
@@ -443,9 +443,11 @@ def main():
     wave_x2 = npk - (nl if lane_x2 else 0)  # wave pairs computed two per wave
     ops_cell = None
     if batch.mode == "i32":
-        # checkpoint batches (SED_OPT_TB 2): the forward kernel runs distance keys (3 ops/cell); the
-        # traceback's recompute runs after it on the same SIMDs and is not in this model (kernel_ms is the DP)
-        ops_cell = CELL_OPS[("nolen" if batch.traceback_mode == 2 else "script") if want_script
+        # checkpoint batches (SED_OPT_TB 2): the forward kernel runs dot keys (v_dot4 + v_max3, 2 ops/cell) or
+        # distance keys (3 ops/cell); the traceback's recompute runs after it on the same SIMDs and is not in
+        # this model (kernel_ms is the DP)
+        ck_ops = "dot" if batch.dot_keys else "nolen"
+        ops_cell = CELL_OPS[(ck_ops if batch.traceback_mode == 2 else "script") if want_script
                             else ("nolen_x2" if npk == P else "nolen")]
     valu_peak = SIMDS * CLOCK * 64 / (VALU_CYCLES_PER_OP * ops_cell) if ops_cell else None
     rate = cells / (dp_avg * 1e-3)
@@ -474,7 +476,7 @@ def main():
         "config": {"workload": desc, "pairs_per_gpu": P, "n": n, "m": m, "costs": costs_file,
                    "script": want_script, "pipeline": pipeline and batch.traceback_mode != 2, "mode": batch.mode,
                    "rows_per_lane": batch.rows_per_lane, "lane_pairs": nl, "packed_pairs": npk,
-                   "chains": batch.chains,
+                   "chains": batch.chains, "dot_keys": batch.dot_keys,
                    "traceback": {0: None, 1: "per-cell codes", 2: "checkpoints + recompute",
                                  3: "per-cell codes, stripe-parallel walk"}[batch.traceback_mode],
                    "parallelism": "dp%d" % world},

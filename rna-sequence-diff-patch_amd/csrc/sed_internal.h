@@ -40,13 +40,20 @@ struct sed_result {
 //   kins = (insert << 16) + 4, kdel = (delete << 16) + 5: the lane kernels' key increments (op included;
 //   their offsets per column / row are kins and kdel - 1).  The wave kernels derive their own from ins/del.
 #define SED_KB 0xFFFFFFFCu  // bias of the 32-bit distance-only offset keys (sed_kernels.hip)
+#define SED_KB_DOT 0u       // border of the dot keys (every border cell is X = U = 0)
 struct sed_i32_params {
     uint32_t costrow[4];
     uint32_t costrow16[4];
     uint32_t kins, kdel;
     uint32_t ins, del;
     uint32_t epoch;  // SPLIT hand-off words' tag: 1..32767 per run (sed_kernels.hip: store_tagged)
-    uint32_t pad;
+    // Dot keys (checkpoint batches of the stripe kernel, sed_kernels.hip: i32_step DOT): the update addend
+    // A*kappa(a, b) + 1, kappa = insert + delete - cost(a -> b), as a signed byte dot product
+    // dot4(dotrow[a], dotcol[b]); keys W = A*X + U (X = sum of kappa on the path, U = its updates), maximised.
+    // Decode: X = ((k*dotkmax) * dotM) >> dotS (= floor(k*kmax / (A*kmax + 1))), U = k - A*X.
+    uint32_t dot;  // 1: the CK forward kernel runs dot keys, the CK traceback converts them
+    uint32_t dotA, dotkmax, dotM, dotS;
+    uint32_t dotrow[4], dotcol[4];
 };
 
 struct sed_f64_params {

@@ -83,6 +83,21 @@ __device__ __forceinline__ double dpp_rol1_f64(double src) {
 }
 
 __device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) { return min(min(a, b), c); }
+__device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) { return max(max(a, b), c); }
+// the dot keys' update candidate: diag + dot4(row vector, column vector) over signed bytes (v_dot4_i32_i8)
+// (the VOP3P form with its own destination: the builtin picks v_dot4c_i32_i8, which accumulates in place and made
+// the register allocator copy every diagonal first, 186 instead of 111 v_mov per 256 cells).  The hardware needs
+// wait states between a v_dot4 and a VALU op reading its result, which the compiler cannot see through the asm
+// (tools/ubench/dot_sem.hip: the next op reads a stale value), so the asm is volatile (issued in program order)
+// and the caller keeps every consumer 4 dots behind its producer (dot_fence).
+__device__ __forceinline__ uint32_t dot_add(uint32_t rowv, uint32_t colv, uint32_t diag) {
+    uint32_t r;
+    asm volatile("v_dot4_i32_i8 %0, %1, %2, %3" : "=v"(r) : "v"(rowv), "v"(colv), "v"(diag));
+    return r;
+}
+// an empty volatile asm on a dot result, placed after the dots that must separate it from its consumer: the
+// consumer cannot be scheduled above it
+__device__ __forceinline__ void dot_fence(uint32_t &x) { asm volatile("" : "+v"(x)); }
 // An opaque v_min3_u32: over three selects (tie keys of the fp64 kernel) the compiler rewrites
 // min(min(a, b), c) into select-of-min chains that cost one op more per cell.
 __device__ __forceinline__ uint32_t umin3_op(uint32_t a, uint32_t b, uint32_t c) {
@@ -175,7 +190,7 @@ template <int R> struct Ladder {
 // sed_wf_i32_kernel), instead of flowing from lane 0 through a DPP move (one DPP + one copy per step).
 // TOPC: lane 0's top is the row-0 constant, which its top_prev already holds (single-stripe pairs: the CHAIN
 // kernel), so the DPP move writes over top_prev in place instead of over a copy of tv.x.
-template <int R, bool TB, bool LEN, bool COLLECT = true, bool SELL = false, bool TOPC = false>
+template <int R, bool TB, bool LEN, bool COLLECT = true, bool SELL = false, bool TOPC = false, bool DOT = false>
 __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                          uint32_t &bottom, uint32_t &selv, const uint2 tv, uint32_t &outc,
                                          uint32_t (&W)[4], const int u) {
@@ -185,6 +200,28 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
     constexpr int d0 = Lad::rung(1) - Lad::rung(0);
     // row 0's update candidate from top_prev, before the DPP move overwrites top_prev in place (TOPC): the
     // empty asm makes the move's `old` depend on it, so top_prev needs no copy
+    if constexpr (DOT) {  // dot keys: maximise, the update addend is one v_dot4 of signed bytes
+        // candidates run 4 rows ahead of the max chain (the dot's result hazard, dot_add): row r + 4's diagonal is
+        // still the old value of row r + 3 when row r is updated
+        constexpr int AH = R < 4 ? R : 4;
+        uint32_t cand[R];
+        cand[0] = dot_add(cv[0], selv, top_prev);
+#pragma unroll
+        for (int r = 1; r < AH; ++r) cand[r] = dot_add(cv[r], selv, V[r - 1]);
+        const uint32_t topv = dpp_shr1(TOPC ? top_prev : tv.x, bottom);
+        uint32_t up = topv;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (r + AH < R) cand[r + AH] = dot_add(cv[r + AH], selv, V[r + AH - 1]);
+            dot_fence(cand[r]);
+            up = umax3(V[r], up, cand[r]);
+            V[r] = up;
+        }
+        top_prev = topv;
+        bottom = V[R - 1];
+        if constexpr (COLLECT) outc = dpp_shl1(bottom, outc);
+        return;
+    }
     uint32_t dg0 = top_prev + __builtin_amdgcn_perm(cv[0], LEN ? (uint32_t)(d0 - 6) : 0xFFFFFFFFu, selv);
     if constexpr (TOPC) asm("" : "+v"(top_prev) : "v"(dg0));
     const uint32_t topv = dpp_shr1(TOPC ? top_prev : tv.x, bottom);  // cell above the band, this column
@@ -218,19 +255,31 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
 
 // Column-0 state of rows row0+1 .. row0+R (row0 = multiple of P) and of row0, the diagonal of the
 // first column.
-template <int R, bool LEN>
+template <int R, bool LEN, bool DOT = false>
 __device__ __forceinline__ void i32_reset(uint32_t (&V)[R], uint32_t &top_prev) {
-    top_prev = LEN ? SED_KB3 : SED_KB;
+    top_prev = LEN ? SED_KB3 : DOT ? SED_KB_DOT : SED_KB;
 #pragma unroll
-    for (int r = 0; r < R; ++r) V[r] = LEN ? SED_KB3 + (uint32_t)Ladder<R>::rung(r + 1) : SED_KB;
+    for (int r = 0; r < R; ++r) V[r] = LEN ? SED_KB3 + (uint32_t)Ladder<R>::rung(r + 1) : DOT ? SED_KB_DOT : SED_KB;
 }
 // row 0 (D = j*insert, L = j) in offset keys
-template <bool LEN> __device__ __forceinline__ uint32_t i32_row0() { return LEN ? SED_KB3 : SED_KB; }
+template <bool LEN, bool DOT = false> __device__ __forceinline__ uint32_t i32_row0() {
+    return LEN ? SED_KB3 : DOT ? SED_KB_DOT : SED_KB;
+}
 
 // The sink cell (n, m) back to V space; returns {D, L} (without LEN, L = n + m - U when WANT_L, else -1).
-template <int R, bool LEN, bool WANT_L = false>
+// Dot key k = A*X + U -> {X, U}: X = floor(k*kmax / (A*kmax + 1)) by a multiply-shift (the host checks k*kmax
+// < 2^29 and picks dotM, dotS so the product is exact), U = k - A*X.
+__device__ __forceinline__ uint2 dot_split(uint32_t w, const sed_i32_params &prm) {
+    const uint32_t k = w - SED_KB_DOT;
+    const uint32_t X = (uint32_t)(((uint64_t)(k * prm.dotkmax) * prm.dotM) >> prm.dotS);
+    return make_uint2(X, k - prm.dotA * X);
+}
+template <int R, bool LEN, bool WANT_L = false, bool DOT = false>
 __device__ __forceinline__ int2 i32_decode(uint32_t w, int n, int m, const sed_i32_params &prm) {
-    if constexpr (LEN) {
+    if constexpr (DOT) {  // D = n*delete + m*insert - X, L = n + m - U
+        const uint2 xu = dot_split(w, prm);
+        return make_int2((int)((uint32_t)n * prm.del + (uint32_t)m * prm.ins - xu.x), n + m - (int)xu.y);
+    } else if constexpr (LEN) {
         const uint32_t v = w - SED_KB3 - (uint32_t)Ladder<R>::rung(n) + (uint32_t)n * ((prm.del << 16) + 8u) +
                            (uint32_t)m * ((prm.ins << 16) + 8u);
         const uint32_t lo = (uint32_t)max(n, m);
@@ -253,6 +302,14 @@ __device__ __forceinline__ uint32_t i32_dist_to_tb(uint32_t w) {
     const uint32_t U = (SED_KB - w) & 0xFFFFu;
     return w - 3u * U;
 }
+// either forward key format -> traceback key: T = SED_KB - (X << 16) - 4U (X = i*delete + j*insert - D)
+__device__ __forceinline__ uint32_t ck_to_tb(uint32_t w, const sed_i32_params &prm) {
+    if (prm.dot) {
+        const uint2 xu = dot_split(w, prm);
+        return SED_KB - (xu.x << 16) - 4u * xu.y;
+    }
+    return i32_dist_to_tb(w);
+}
 
 // Ramp for free.  Every lane starts a stripe at its column-0 state and lane t begins real work
 // at step t.  Before that it runs "virtual" columns, which leave its state unchanged: their str2
@@ -264,7 +321,9 @@ __device__ __forceinline__ uint32_t i32_dist_to_tb(uint32_t w) {
 // The lane's first real column then sees exactly D[row][0], D[row-1][0] and the cell above.
 #define SED_SEL_SENT 0x0C0C0C0Cu
 #define SED_SEL_SENT3 0x0C0C0C0Du
-template <bool LEN> __device__ __forceinline__ uint32_t i32_sent() { return LEN ? SED_SEL_SENT3 : SED_SEL_SENT; }
+template <bool LEN, bool DOT = false> __device__ __forceinline__ uint32_t i32_sent() {
+    return LEN ? SED_SEL_SENT3 : DOT ? 0u : SED_SEL_SENT;  // dot keys: the zero column vector adds 0
+}
 // perm selector of str2 symbol b: byte3 <- 0xFF, byte2 <- cost byte b, bytes 1:0 <- the constant
 __device__ __forceinline__ uint32_t i32_sel(uint32_t b) { return 0x0D000100u | ((4u + b) << 16); }
 
@@ -273,7 +332,7 @@ __device__ __forceinline__ uint32_t i32_sel(uint32_t b) { return 0x0D000100u | (
 // The stripe kernel's group: lane 0's top values from the chunk's LDS slots (ltop, broadcast reads),
 // each lane's str2 selectors from the wave's LDS selector ring at its own column (lsel: this group's
 // first step for this lane, doubled ring so the G reads never wrap).
-template <int R, bool TB, bool LEN, bool CAP, bool CK = false>
+template <int R, bool TB, bool LEN, bool CAP, bool CK = false, bool DOT = false>
 __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                           uint32_t &bottom, uint32_t &selv, const uint32_t *__restrict__ ltop,
                                           const uint32_t *__restrict__ lsel, uint32_t &outc, uint32_t (&W)[4],
@@ -287,7 +346,7 @@ __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         const int s = s0 + u;
-        i32_step<R, TB, LEN, !CK, true>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u);
+        i32_step<R, TB, LEN, !CK, true, false, DOT>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u);
         if constexpr (CK) rcv[u] = V[R - 1];  // the band's bottom row, step s (row checkpoints)
         if constexpr (CAP) {
             const bool hit = (s == cap_step) && (lane == cap_lane);
@@ -336,7 +395,7 @@ __device__ __forceinline__ void store_tagged(uint64_t *p, uint32_t tag, uint32_t
 // (D, L), which is all the checkpoints need; the traceback recomputes the op tie-break.
 // The CK kernel (distance keys, no codes) would fit 80 VGPRs (6 waves per SIMD, spills per chunk only) but
 // ran slower: 12.45 against 12.11 ms at 5 waves (profiles/r02/ab_ck_waves.txt).
-template <int R, bool TB, bool SPLIT, bool LEN = true, bool CK = false>
+template <int R, bool TB, bool SPLIT, bool LEN = true, bool CK = false, bool DOT = false>
 __global__ __launch_bounds__(SPLIT ? 64 : 256) __attribute__((amdgpu_waves_per_eu(CK ? SED_CK_WAVES : SED_I32_WAVES(R))))
 void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *__restrict__ tasks,
                   const uint32_t *__restrict__ seqa, const uint32_t *__restrict__ seqb,
@@ -345,6 +404,7 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
     constexpr int ROWS = 64 * R;
     constexpr int G = Grp<R>::G;
     static_assert(!CK || (R <= 16 && !SPLIT && !TB && !LEN), "checkpoints: R <= 16, distance keys, one wave per pair");
+    static_assert(!DOT || CK, "dot keys: checkpoint batches only");
     const int lane = threadIdx.x & 63;
     int pair, kfirst = 0;
     if constexpr (SPLIT) {
@@ -400,12 +460,13 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         for (int r = 0; r < R; ++r) {
             const int ri = row0 + r;
             const uint32_t a = (pa[ri >> 4] >> ((ri & 15) * 2)) & 3u;
-            cv[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
+            if constexpr (DOT) cv[r] = a == 0 ? prm.dotrow[0] : a == 1 ? prm.dotrow[1] : a == 2 ? prm.dotrow[2] : prm.dotrow[3];
+            else cv[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
         }
         uint32_t top_prev;
-        i32_reset<R, LEN>(V, top_prev);
+        i32_reset<R, LEN, DOT>(V, top_prev);
         // column-0 state for every lane; virtual columns until the lane's first real one (see above)
-        uint32_t bottom = V[R - 1], selv = i32_sent<LEN>(), outc = 0;
+        uint32_t bottom = V[R - 1], selv = i32_sent<LEN, DOT>(), outc = 0;
         uint32_t W[4] = {0, 0, 0, 0};
 
         // CK: the previous stripe's lane 63 stored its bottom row contiguously by step into the pair's
@@ -413,7 +474,7 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         // steps >= s + 64; past SG the columns are beyond m and never read)
         auto load_top = [&](int c) -> uint32_t {
             const int j = 64 * c + lane + 1;
-            if (k == 0) return i32_row0<LEN>();
+            if (k == 0) return i32_row0<LEN, DOT>();
             if constexpr (CK) return load_sc1(bnd + d.bnd_off + (uint32_t)(j + 62));
             return load_sc1(bnd_in + j + 64);
         };
@@ -441,7 +502,9 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         };
         auto load_sel = [&](int c) -> uint32_t {
             const int ci = 64 * c + lane;
-            return i32_sel((pb[ci >> 4] >> ((ci & 15) * 2)) & 3u);
+            const uint32_t b = (pb[ci >> 4] >> ((ci & 15) * 2)) & 3u;
+            if constexpr (DOT) return b == 0 ? prm.dotcol[0] : b == 1 ? prm.dotcol[1] : b == 2 ? prm.dotcol[2] : prm.dotcol[3];
+            return i32_sel(b);
         };
         uint32_t tch = (SPLIT && k > 0) ? 0u : load_top(0), sch = load_sel(0);
         lch[lane] = tch;  // SPLIT: stripe 0's constant row; the others fetch group by group
@@ -452,7 +515,7 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
             }
         }
         ring[lane] = ring[lane + 128] = sch;
-        ring[lane + 64] = ring[lane + 192] = i32_sent<LEN>();
+        ring[lane + 64] = ring[lane + 192] = i32_sent<LEN, DOT>();
         uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * 256u;
         // CK: column checkpoints of stripe k at ccb[(chunk * (R+1) + v) * 64 + lane], row checkpoints at
         // rcb[group * 64 + (lane / G) * G + step % G] (sed_ck_*_word, the layout sed_traceback_ck_kernel reads)
@@ -490,7 +553,7 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
 #pragma unroll 2
                 for (int g = 0; g < 64 / G; ++g) {
                     const int s0 = 64 * c + g * G;  // (s0 & 63 folds to g * G)
-                    i32_group<R, TB, LEN, false, CK>(V, cv, top_prev, bottom, selv, lch, lsel + g * G, outc, W, s0, lane,
+                    i32_group<R, TB, LEN, false, CK, DOT>(V, cv, top_prev, bottom, selv, lch, lsel + g * G, outc, W, s0, lane,
                                                      cap_step, cap_lane, cap_row, cap, rcv);
                     if (s0 < SG) stores(s0);
                 }
@@ -501,10 +564,10 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                     if (fetch) fetch_issue(s + G);
                     const bool capg = cap_step >= s && cap_step < s + G;
                     if (capg)
-                        i32_group<R, TB, LEN, true, CK>(V, cv, top_prev, bottom, selv, lch, lsel, outc, W, s, lane,
+                        i32_group<R, TB, LEN, true, CK, DOT>(V, cv, top_prev, bottom, selv, lch, lsel, outc, W, s, lane,
                                                         cap_step, cap_lane, cap_row, cap, rcv);
                     else
-                        i32_group<R, TB, LEN, false, CK>(V, cv, top_prev, bottom, selv, lch, lsel, outc, W, s, lane,
+                        i32_group<R, TB, LEN, false, CK, DOT>(V, cv, top_prev, bottom, selv, lch, lsel, outc, W, s, lane,
                                                          cap_step, cap_lane, cap_row, cap, rcv);
                     stores(s);
                     if constexpr (SPLIT) {
@@ -533,7 +596,7 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         if (!last) __builtin_amdgcn_s_waitcnt(0);  // own bottom-row stores done before the next stripe reads them
     }
     if (klast == nstripes - 1 && lane == cap_lane) {
-        const int2 dl = i32_decode<R, LEN, CK>(cap, n, m, prm);
+        const int2 dl = i32_decode<R, LEN, CK, DOT>(cap, n, m, prm);
         res[pair].dist = (double)dl.x;
         res[pair].len = dl.y;
         res[pair].is_int = (dl.x == 0);
@@ -1835,8 +1898,8 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
             uint32_t V = SED_KB, tp = SED_KB;  // c = 0: the column-0 borders
             if (c >= 1) {
                 const uint32_t *cp = ccp + sed_ck_col_word(R, k, nchunks, c - 1, lane & (R - 1), G * Q + band);
-                V = i32_dist_to_tb(cp[0]);
-                tp = i32_dist_to_tb(cp[(R - (lane & (R - 1))) * 64]);
+                V = ck_to_tb(cp[0], prm);
+                tp = ck_to_tb(cp[(R - (lane & (R - 1))) * 64], prm);
             }
             tp += 1u;  // diagonals carry the +1 of the delete candidate they were taken from
             {
@@ -1849,9 +1912,9 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
                 uint32_t v = SED_KB;
                 if (J0 - G + x >= 1) {
                     if (Q >= 1)
-                        v = i32_dist_to_tb(rcp[sed_ck_row_word(R, k, ngroups, min(64 * c - G - 1 + x, SG - 1), G * Q - 1)]);
+                        v = ck_to_tb(rcp[sed_ck_row_word(R, k, ngroups, min(64 * c - G - 1 + x, SG - 1), G * Q - 1)], prm);
                     else if (k >= 1)
-                        v = i32_dist_to_tb(rcp[sed_ck_row_word(R, k - 1, ngroups, min(64 * c + 63 - G + x, SG - 1), 63)]);
+                        v = ck_to_tb(rcp[sed_ck_row_word(R, k - 1, ngroups, min(64 * c + 63 - G + x, SG - 1), 63)], prm);
                 }
                 topb[x] = v + 1u;
                 const int col = J0 - (G - 1) + x;  // column of lane 0 at step x
@@ -1991,7 +2054,7 @@ __global__ void sed_selftest_kernel(uint32_t *out) {
 // ---------------------------------------------------------------------------
 // Launchers (host side, called from sed_runtime.cpp)
 // ---------------------------------------------------------------------------
-template <int R, bool TB, bool LEN = true, bool CK = false>
+template <int R, bool TB, bool LEN = true, bool CK = false, bool DOT = false>
 static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
     if (L.ntasks > 0) {  // SPLIT: one 64-thread workgroup per (pair, stripe)
         SED_LAUNCH((sed_wf_i32_kernel<R, TB, true, LEN>), dim3(L.ntasks), dim3(64), 0, L, L.pd, L.npairs,
@@ -2001,7 +2064,7 @@ static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
         const int grid = (L.npairs + 3) / 4;
         // SED_OCC_LDS (tuning/A-B only): dynamic LDS bytes per workgroup, which caps the resident waves
         static const int occ_lds = [] { const char *e = getenv("SED_OCC_LDS"); return e ? atoi(e) : 0; }();
-        SED_LAUNCH((sed_wf_i32_kernel<R, TB, false, LEN, CK>), dim3(grid), dim3(256), occ_lds, L, L.pd, L.npairs,
+        SED_LAUNCH((sed_wf_i32_kernel<R, TB, false, LEN, CK, DOT>), dim3(grid), dim3(256), occ_lds, L, L.pd, L.npairs,
                            L.tasks, (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res,
                            prm);
     }
@@ -2055,6 +2118,14 @@ hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm, bool l
     const bool tb = L.tb != nullptr;
     if (tb && L.ck) {  // distance keys + checkpoints
         if (L.ntasks > 0) return hipErrorInvalidValue;
+        if (prm.dot) {  // dot keys (the host found a byte factorisation of the update addends)
+            switch (L.R) {
+            case 4: return launch_i32_R<4, false, false, true, true>(L, prm);
+            case 8: return launch_i32_R<8, false, false, true, true>(L, prm);
+            case 16: return launch_i32_R<16, false, false, true, true>(L, prm);
+            default: return hipErrorInvalidValue;
+            }
+        }
         switch (L.R) {
         case 4: return launch_i32_R<4, false, false, true>(L, prm);
         case 8: return launch_i32_R<8, false, false, true>(L, prm);

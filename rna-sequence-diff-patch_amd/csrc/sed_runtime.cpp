@@ -59,7 +59,8 @@ struct sed_ctx {
     DevBuf gtab;  // fp64 kernel table: per entry {value bits, is-int flag}
     // options
     int opt_mode = 0, opt_R = 0, opt_split = 0, opt_lane = 0, opt_chain = 0, opt_pack = 0, opt_tb = 0;
-    int opt_chain_waves = 0;    // SED_OPT_CHAIN_WAVES: cap on the persistent waves of dynamic CHAIN mode
+    int opt_chain_waves = 0;
+    int opt_dot = 0;            // SED_OPT_DOT: 0 auto, 2 never (checkpoint batches keep the perm-based distance keys)    // SED_OPT_CHAIN_WAVES: cap on the persistent waves of dynamic CHAIN mode
     int opt_debug_corrupt = 0;  // SED_OPT_DEBUG_CORRUPT: pair + 1 whose sink-tile checkpoint is overwritten
     DevBuf selftest;
     sed_batch *scratch = nullptr;
@@ -92,6 +93,7 @@ struct sed_batch {
     int tbpar_items = 0, tbpar_kmax = 0;
     bool split = false;
     bool ck = false;           // traceback from checkpoints + recompute (sed_kernels.hip: CK) instead of codes
+    bool dot = false;          // CK forward kernel on dot keys (dot_keys below)
     int nlane = 0, nwave = 0;  // pairs on the lane-per-pair kernel / on the wave kernels
     int nlane_x2 = 0;          // > 0: lane pairs run two per lane (distance only), in this many lanes
     int nwave_x2 = 0;          // distance-only wave pairs of equal shape run two per wave, in this many waves
@@ -133,6 +135,168 @@ struct sed_batch {
 };
 
 namespace {
+
+// ---- dot keys ----
+// The CK forward kernel's update candidate can be one signed-byte dot product v_dot4_i32_i8(row vector of str1's
+// symbol a, column vector of str2's symbol b, diagonal) when the addends H(a, b) = A*kappa(a, b) + 1 (kappa =
+// insert + delete - cost(a -> b)) factor as sum_k r_k(a) c_k(b) over bytes in [-127, 127]: keys W = A*X + U
+// (X = sum of kappa over the path's updates, U = its number of updates) are maximised with v_max3, so the cell is
+// v_dot4 + v_max3 (2 VALU) instead of v_perm + v_add + v_min3.  Ordering: at a fixed cell a candidate with a larger
+// X must win whatever the U's, i.e. A > the U spread of two candidates, which is below min(i, j) (kmax - kmin) /
+// kmin because every update contributes kappa in [kmin, kmax]; the same bound makes X = floor(k kmax / (A kmax +
+// 1)) recover X from k = A*X + U.
+// Construction (rank 3 + one constant slot): with det/S = num/den (S = 1^T adj(K) 1), N = den*K - num*J has rank 3
+// and left null vector v = 1^T adj(K); if some |v_g| = 1, row g of N is an integer combination of the other three.
+// Slot 0 is the constant x*y = num*a + 1, slots 1..3 are a*N's rank-3 factorisation (coordinates P0 scaled by a1,
+// rows of N scaled by a2, a1*a2 = a), so sum_k r_k c_k = num*a + 1 + a*(den K - num) = A K + 1 with A = den*a.
+struct DotKeys {
+    bool ok = false;
+    uint32_t A = 0, kmax = 0, kmin = 0, M = 0, S = 0;
+    uint32_t row[4] = {0, 0, 0, 0}, col[4] = {0, 0, 0, 0};
+};
+int64_t det3(const int64_t m[3][3]) {
+    return m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) - m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
+           m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
+}
+int64_t gcd64(int64_t a, int64_t b) {
+    a = a < 0 ? -a : a;
+    b = b < 0 ? -b : b;
+    while (b) {
+        const int64_t t = a % b;
+        a = b;
+        b = t;
+    }
+    return a;
+}
+// kap: kappa[a][b] (>= 1); maxmin: the largest min(n, m) of the batch's wave pairs
+DotKeys dot_keys(const int64_t kap[4][4], int64_t maxmin) {
+    DotKeys dk;
+    int64_t kmax = 0, kmin = INT64_MAX;
+    for (int a = 0; a < 4; ++a)
+        for (int b = 0; b < 4; ++b) {
+            kmax = std::max(kmax, kap[a][b]);
+            kmin = std::min(kmin, kap[a][b]);
+        }
+    if (kmin < 1 || kmax > 255) return dk;
+    // adjugate (adj[b][a] = cofactor(a, b)) and determinant
+    int64_t adj[4][4], det = 0;
+    for (int a = 0; a < 4; ++a)
+        for (int b = 0; b < 4; ++b) {
+            int64_t m3[3][3];
+            for (int i = 0, ii = 0; i < 4; ++i) {
+                if (i == a) continue;
+                for (int j = 0, jj = 0; j < 4; ++j) {
+                    if (j == b) continue;
+                    m3[ii][jj++] = kap[i][j];
+                }
+                ++ii;
+            }
+            adj[b][a] = (((a + b) & 1) ? -1 : 1) * det3(m3);
+        }
+    for (int b = 0; b < 4; ++b) det += kap[0][b] * adj[b][0];
+    int64_t S = 0, v[4] = {0, 0, 0, 0};
+    for (int a = 0; a < 4; ++a)
+        for (int b = 0; b < 4; ++b) {
+            S += adj[a][b];
+            v[b] += adj[a][b];  // v = 1^T adj(K)
+        }
+    if (S == 0) return dk;
+    int64_t num = det, den = S;
+    if (den < 0) { num = -num; den = -den; }
+    const int64_t gd = gcd64(num, den);
+    if (gd > 1) { num /= gd; den /= gd; }
+    int64_t gv = 0;
+    for (int a = 0; a < 4; ++a) gv = gcd64(gv, v[a]);
+    if (gv == 0) return dk;
+    for (int a = 0; a < 4; ++a) v[a] /= gv;
+    int g = -1;
+    for (int a = 0; a < 4; ++a)
+        if (v[a] == 1 || v[a] == -1) { g = a; break; }
+    if (g < 0) return dk;
+    int64_t N[4][4];
+    for (int a = 0; a < 4; ++a)
+        for (int b = 0; b < 4; ++b) N[a][b] = den * kap[a][b] - num;
+    // slots 1..3 <-> rows s[0..2] != g: P0[a][k] = [a == s_k] (a != g), P0[g][k] = -v[s_k] / v[g]
+    int sr[3], ns = 0;
+    for (int a = 0; a < 4; ++a)
+        if (a != g) sr[ns++] = a;
+    int64_t P0[4][3], pmax[3], qmax[3];
+    for (int k = 0; k < 3; ++k) {
+        pmax[k] = qmax[k] = 0;
+        for (int a = 0; a < 4; ++a) {
+            P0[a][k] = a == g ? -v[sr[k]] * v[g] : (a == sr[k] ? 1 : 0);  // v[g] = +-1: 1/v[g] = v[g]
+            pmax[k] = std::max(pmax[k], P0[a][k] < 0 ? -P0[a][k] : P0[a][k]);
+        }
+        for (int b = 0; b < 4; ++b) qmax[k] = std::max(qmax[k], N[sr[k]][b] < 0 ? -N[sr[k]][b] : N[sr[k]][b]);
+    }
+    // the rank-3 identity must hold exactly
+    for (int a = 0; a < 4; ++a)
+        for (int b = 0; b < 4; ++b) {
+            int64_t t = 0;
+            for (int k = 0; k < 3; ++k) t += P0[a][k] * N[sr[k]][b];
+            if (t != N[a][b]) return dk;
+        }
+    // the largest a with every slot within bytes (larger A leaves more room for long pairs)
+    const int64_t a_hi = num != 0 ? (127 * 127 + 127) / (num < 0 ? -num : num) : 127 * 127;  // |num a + 1| <= 127^2
+    for (int64_t a = a_hi; a >= 1; --a) {
+        const int64_t A = den * a;
+        if (A * kmin <= maxmin * (kmax - kmin)) break;  // the ordering bound fails for every smaller a too
+        const int64_t J = num * a + 1;
+        int64_t x = 0, y = 0;
+        for (int64_t t = 1; t <= 127 && !x; ++t)
+            if (J % t == 0 && (J / t >= -127 && J / t <= 127)) { x = t; y = J / t; }
+        if (!x) continue;
+        int64_t a1[3], a2[3];
+        bool fit = true;
+        for (int k = 0; k < 3 && fit; ++k) {
+            a1[k] = 0;
+            for (int64_t t = 1; t <= 127; ++t)
+                if (a % t == 0 && t * pmax[k] <= 127 && (a / t) * qmax[k] <= 127) { a1[k] = t; break; }
+            if (!a1[k]) fit = false;
+            else a2[k] = a / a1[k];
+        }
+        if (!fit) continue;
+        // decode: k * kmax < 2^29 over every real cell (k <= A * kmax * maxmin + maxmin)
+        if ((A * kmax * maxmin + maxmin) * kmax >= (int64_t)1 << 29) continue;
+        int8_t R[4][4], C[4][4];
+        for (int i = 0; i < 4; ++i) {
+            R[i][0] = (int8_t)x;
+            C[i][0] = (int8_t)y;
+            for (int k = 0; k < 3; ++k) {
+                R[i][k + 1] = (int8_t)(a1[k] * P0[i][k]);
+                C[i][k + 1] = (int8_t)(a2[k] * N[sr[k]][i]);
+            }
+        }
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) {
+                int64_t t = 0;
+                for (int k = 0; k < 4; ++k) t += (int64_t)R[i][k] * C[j][k];
+                if (t != A * kap[i][j] + 1) return dk;
+            }
+        dk.A = (uint32_t)A;
+        dk.kmax = (uint32_t)kmax;
+        dk.kmin = (uint32_t)kmin;
+        const uint64_t Dd = (uint64_t)A * kmax + 1;
+        int lg = 0;
+        while (((uint64_t)1 << lg) < Dd) ++lg;
+        dk.S = (uint32_t)(29 + lg);
+        const uint64_t M = (((uint64_t)1 << dk.S) / Dd) + 1;
+        if (M >> 32) return dk;
+        dk.M = (uint32_t)M;
+        for (int i = 0; i < 4; ++i) {
+            uint32_t rw = 0, cw = 0;
+            for (int k = 0; k < 4; ++k) {
+                rw |= (uint32_t)(uint8_t)R[i][k] << (8 * k);
+                cw |= (uint32_t)(uint8_t)C[i][k] << (8 * k);
+            }
+            dk.row[i] = rw;
+            dk.col[i] = cw;
+        }
+        dk.ok = true;
+        return dk;
+    }
+    return dk;
+}
 
 int next_pow2(int x) {
     int p = 1;
@@ -549,6 +713,28 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         }
         ip.kins = (ip.ins << 16) + 4u;
         ip.kdel = (ip.del << 16) + 5u;
+        // dot keys: checkpoint batches of the stripe kernel (CHAIN batches share the traceback's key format)
+        b->dot = false;
+        if (b->ck && b->nchains == 0 && c->K == 4 && c->opt_dot != 2) {
+            int64_t kap[4][4], maxmin = 0;
+            for (int a = 0; a < 4; ++a)
+                for (int bb = 0; bb < 4; ++bb) kap[a][bb] = (int64_t)ip.ins + ip.del - (int64_t)c->sub[a * 4 + bb];
+            for (int p = 0; p < npairs; ++p)
+                if (!b->pd[p].lane) maxmin = std::max<int64_t>(maxmin, std::min(len_a[p], len_b[p]));
+            const DotKeys dk = dot_keys(kap, maxmin);
+            if (dk.ok) {
+                ip.dot = 1;
+                ip.dotA = dk.A;
+                ip.dotkmax = dk.kmax;
+                ip.dotM = dk.M;
+                ip.dotS = dk.S;
+                for (int a = 0; a < 4; ++a) {
+                    ip.dotrow[a] = dk.row[a];
+                    ip.dotcol[a] = dk.col[a];
+                }
+                b->dot = true;
+            }
+        }
         b->ip = ip;
     } else {
         sed_f64_params fp{};
@@ -676,12 +862,17 @@ int run_batch(sed_batch *b) {
             const int t = ((d.n - 1) % ROWS) / R, r = (d.n - 1) % R, cs = (d.m - 1 + t) >> 6;
             if (cs >= 1) {
                 uint32_t *w = (uint32_t *)b->d_tb[k].p + d.tb_off + sed_ck_col_word(R, nstripes - 1, nchunks, cs - 1, r, t);
-                if ((e = hipMemsetD32Async((hipDeviceptr_t)w, 0x0000FFFCu, 1, c->stream)) != hipSuccess)
+                // (dot keys are maximised: the largest key there instead)
+                if ((e = hipMemsetD32Async((hipDeviceptr_t)w, b->dot ? 0x3FFFFFFFu : 0x0000FFFCu, 1, c->stream)) !=
+                    hipSuccess)
                     return c->hipfail(e, "debug corrupt");
             }
         }
     }
-    if (want_tb) {
+    // SED_DEBUG_NOTB=1 (debugging only): skip the traceback kernels, so a script batch reports the forward kernel's
+    // distances and lengths (its scripts are left as they were)
+    static const bool no_tb = [] { const char *e = getenv("SED_DEBUG_NOTB"); return e && atoi(e) > 0; }();
+    if (want_tb && !no_tb) {
         if (ts != c->stream && (e = hipStreamWaitEvent(ts, lg[1], 0)) != hipSuccess) return c->hipfail(e, "stream wait");
         if (b->nwave == 0 && (e = hipEventRecord(lg[2], ts)) != hipSuccess) return c->hipfail(e, "event record");
         if (b->nwave > 0) {
@@ -811,6 +1002,10 @@ int sed_set_option(sed_ctx *c, int key, int value) {
         c->opt_pack = value;
         return SED_OK;
     }
+    if (key == SED_OPT_DOT && (value == 0 || value == 2)) {
+        c->opt_dot = value;
+        return SED_OK;
+    }
     if (key == SED_OPT_CHAIN_WAVES && value >= 0) {
         c->opt_chain_waves = value;
         return SED_OK;
@@ -888,6 +1083,8 @@ int sed_batch_traceback_mode(const sed_batch *b) {
     if (!b || !(b->flags & SED_WANT_SCRIPT)) return 0;
     return b->ck ? 2 : (b->tbpar ? 3 : 1);
 }
+
+int sed_batch_dot_keys(const sed_batch *b) { return b ? (b->dot ? 1 : 0) : SED_E_ARG; }
 
 int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave) {
     if (!b) return SED_E_ARG;

@@ -38,6 +38,7 @@ SED_OPT_PACK = 6
 SED_OPT_TB = 7
 SED_OPT_CHAIN_WAVES = 8
 SED_OPT_DEBUG_CORRUPT = 9
+SED_OPT_DOT = 10
 MODE_NAMES = {1: "i32", 2: "f64", 3: "f64-typed"}
 
 _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
@@ -63,6 +64,7 @@ SIGNATURES = [
     ("sed_batch_rows_per_lane", C.c_int, [C.c_void_p]),
     ("sed_batch_lane_pairs", C.c_int, [C.c_void_p]),
     ("sed_batch_chains", C.c_int, [C.c_void_p]),
+    ("sed_batch_dot_keys", C.c_int, [C.c_void_p]),
     ("sed_batch_packed_pairs", C.c_int, [C.c_void_p]),
     ("sed_batch_traceback_mode", C.c_int, [C.c_void_p]),
     ("sed_batch_chain_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
@@ -281,6 +283,11 @@ class Batch:
     @property
     def chains(self):
         return self._lib.sed_batch_chains(self.ptr)
+
+    @property
+    def dot_keys(self):
+        """True when the checkpoint forward kernel runs dot keys (v_dot4 + v_max3 per cell, SED_OPT_DOT)."""
+        return self._lib.sed_batch_dot_keys(self.ptr) == 1
 
     @property
     def traceback_mode(self):

@@ -144,6 +144,67 @@ def test_checkpoint_default_route_with_lane_pairs_and_pipeline(gpu, tables):
     assert np.array_equal(d2, d) and np.array_equal(ln2, ln) and np.array_equal(ops2, ops)
 
 
+@pytest.mark.parametrize("user", [False, True])
+def test_checkpoint_dot_keys_route(gpu, tables, user):
+    """Dot keys (SED_OPT_DOT): the checkpoint forward kernel's cell is one v_dot4_i32_i8 (row vector of str1's
+    symbol . column vector of str2's symbol, added to the diagonal) and one v_max3 when the table's update addends
+    A*kappa + 1 factor over signed bytes (both shipped tables do).  300 ragged pairs (1..2600, related and
+    unrelated) at R = 16, 8 and 4: every pair vs the oracle, op by op, and identical to the perm-based distance
+    keys (SED_OPT_DOT = 2)."""
+    A, B = _ragged(3400 + user, 300, 1, 2600, 1, 2600)
+    plan = _plan(tables[user])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs(A, B)
+    gpu.set_option(sedgpu.SED_OPT_TB, 2)
+    gpu.set_option(sedgpu.SED_OPT_CHAIN, 2)
+    try:
+        for R in (16, 8, 4):
+            gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, R)
+            b, (d, ii, ln, ops) = _batch_run(gpu, packed, True)
+            try:
+                assert b.dot_keys and b.traceback_mode == 2 and b.rows_per_lane == R and b.chains == 0
+            finally:
+                b.close()
+            _check_all(plan, packed, d, ii, ln, ops)
+            gpu.set_option(sedgpu.SED_OPT_DOT, 2)
+            try:
+                b, (d2, ii2, ln2, ops2) = _batch_run(gpu, packed, True)
+                try:
+                    assert not b.dot_keys and b.traceback_mode == 2
+                finally:
+                    b.close()
+            finally:
+                gpu.set_option(sedgpu.SED_OPT_DOT, 0)
+            assert np.array_equal(d2, d) and np.array_equal(ln2, ln) and np.array_equal(ops2, ops)
+    finally:
+        gpu.set_option(sedgpu.SED_OPT_TB, 0)
+        gpu.set_option(sedgpu.SED_OPT_CHAIN, 0)
+        gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
+
+
+def test_dot_keys_fall_back_past_their_bound(gpu, tables):
+    """user_costs' byte factorisation has A = 2880.  Dot keys order the candidates of a cell correctly while
+    A > min(n, m) (kmax - kmin) / kmin (kappa = insert + delete - cost in 3..5), i.e. min(n, m) < 4320: a batch
+    holding a 4400 x 4400 pair keeps the perm-based distance keys, the same batch without it takes dot keys, and
+    both match the oracle."""
+    A, B = _ragged(3500, 259, 100, 1500, 100, 1500)
+    a, b = _ragged(3501, 1, 4400, 4400, 4400, 4400, related=1.0)
+    plan = _plan(tables[True])
+    gpu.set_costs(plan)
+    gpu.set_option(sedgpu.SED_OPT_TB, 2)
+    try:
+        for extra, want in (([], True), (list(zip(a, b)), False)):
+            packed = sedgpu.PackedPairs(A + [x for x, _ in extra], B + [y for _, y in extra])
+            bt, (d, ii, ln, ops) = _batch_run(gpu, packed, True)
+            try:
+                assert bt.dot_keys == want and bt.traceback_mode == 2
+            finally:
+                bt.close()
+            _check_all(plan, packed, d, ii, ln, ops)
+    finally:
+        gpu.set_option(sedgpu.SED_OPT_TB, 0)
+
+
 def test_checkpoint_traceback_reports_a_corrupt_checkpoint(gpu, tables):
     """SED_OPT_DEBUG_CORRUPT overwrites one column-checkpoint word (the sink row's, in the chunk before the
     sink's tile) of one pair with the smallest key between the DP and the traceback: the recomputed tile then contradicts the path
