@@ -50,7 +50,8 @@ struct sed_i32_params {
     // Dot keys (checkpoint batches of the stripe kernel, sed_kernels.hip: i32_step DOT): the update addend
     // A*kappa(a, b) + 1, kappa = insert + delete - cost(a -> b), as a signed byte dot product
     // dot4(dotrow[a], dotcol[b]); keys W = A*X + U (X = sum of kappa on the path, U = its updates), maximised.
-    // Decode: X = ((k*dotkmax) * dotM) >> dotS (= floor(k*kmax / (A*kmax + 1))), U = k - A*X.
+    // Decode: X = (k * dotM) >> dotS (= floor(k*kmax / (A*kmax + 1)); dotM includes kmax, dotS >= 32, so the
+    // kernels take one v_mul_hi_u32), U = k - A*X.
     uint32_t dot;  // 1: the CK forward kernel runs dot keys, the CK traceback converts them
     uint32_t dotA, dotkmax, dotM, dotS;
     uint32_t dotrow[4], dotcol[4];

@@ -96,7 +96,9 @@ __device__ __forceinline__ uint32_t dot_add(uint32_t rowv, uint32_t colv, uint32
     return r;
 }
 // an empty volatile asm on a dot result, placed after the dots that must separate it from its consumer: the
-// consumer cannot be scheduled above it
+// consumer cannot be scheduled above it.  (The compiler treats the asm as a write of x and puts an s_nop 0 between
+// it and the max reading x, 50 per 64-cell group.  Fencing one row earlier drops that to 29 but lets the compiler
+// pair up dependent maxes back to back: config 4's forward 9.19 -> 9.49 ms, so the fence stays next to its max.)
 __device__ __forceinline__ void dot_fence(uint32_t &x) { asm volatile("" : "+v"(x)); }
 // An opaque v_min3_u32: over three selects (tie keys of the fp64 kernel) the compiler rewrites
 // min(min(a, b), c) into select-of-min chains that cost one op more per cell.
@@ -213,7 +215,7 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (r + AH < R) cand[r + AH] = dot_add(cv[r + AH], selv, V[r + AH - 1]);
-            dot_fence(cand[r]);
+            dot_fence(cand[r]);  // row r's candidate was issued 4 dots ago
             up = umax3(V[r], up, cand[r]);
             V[r] = up;
         }
@@ -271,8 +273,8 @@ template <bool LEN, bool DOT = false> __device__ __forceinline__ uint32_t i32_ro
 // < 2^29 and picks dotM, dotS so the product is exact), U = k - A*X.
 __device__ __forceinline__ uint2 dot_split(uint32_t w, const sed_i32_params &prm) {
     const uint32_t k = w - SED_KB_DOT;
-    const uint32_t X = (uint32_t)(((uint64_t)(k * prm.dotkmax) * prm.dotM) >> prm.dotS);
-    return make_uint2(X, k - prm.dotA * X);
+    const uint32_t X = __umulhi(k, prm.dotM) >> (prm.dotS - 32u);  // dotM carries kmax (one v_mul_hi, full-rate rest)
+    return make_uint2(X, k - __umul24(prm.dotA, X));
 }
 template <int R, bool LEN, bool WANT_L = false, bool DOT = false>
 __device__ __forceinline__ int2 i32_decode(uint32_t w, int n, int m, const sed_i32_params &prm) {
@@ -304,9 +306,10 @@ __device__ __forceinline__ uint32_t i32_dist_to_tb(uint32_t w) {
 }
 // either forward key format -> traceback key: T = SED_KB - (X << 16) - 4U (X = i*delete + j*insert - D)
 __device__ __forceinline__ uint32_t ck_to_tb(uint32_t w, const sed_i32_params &prm) {
-    if (prm.dot) {
-        const uint2 xu = dot_split(w, prm);
-        return SED_KB - (xu.x << 16) - 4u * xu.y;
+    if (prm.dot) {  // = SED_KB - 4k + 4A X - (X << 16)
+        const uint32_t k = w - SED_KB_DOT;
+        const uint32_t X = __umulhi(k, prm.dotM) >> (prm.dotS - 32u);
+        return SED_KB - 4u * k + __umul24(4u * prm.dotA, X) - (X << 16);
     }
     return i32_dist_to_tb(w);
 }

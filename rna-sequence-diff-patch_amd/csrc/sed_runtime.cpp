@@ -280,8 +280,8 @@ DotKeys dot_keys(const int64_t kap[4][4], int64_t maxmin) {
         int lg = 0;
         while (((uint64_t)1 << lg) < Dd) ++lg;
         dk.S = (uint32_t)(29 + lg);
-        const uint64_t M = (((uint64_t)1 << dk.S) / Dd) + 1;
-        if (M >> 32) return dk;
+        const uint64_t M = ((((uint64_t)1 << dk.S) / Dd) + 1) * (uint64_t)kmax;  // the kernels multiply k by M
+        if (M >> 32 || dk.S < 32 || 4 * A >= (1 << 24)) return dk;
         dk.M = (uint32_t)M;
         for (int i = 0; i < 4; ++i) {
             uint32_t rw = 0, cw = 0;
