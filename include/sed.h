@@ -73,8 +73,9 @@ enum {
                                    wave (equal n and m) in packed 16-bit cells: 0 auto (on), 2 never */
 #define SED_OPT_CHAIN_WAVES 8   /* dynamic CHAIN mode: persistent waves, 0 auto (every SIMD's resident waves), else a
                                    cap (tests: several counter-fetched pairs per wave) */
-#define SED_OPT_DOT 10          /* checkpoint batches of the stripe kernel: 0 auto (dot keys when the cost table's
-                                   update addends factor over signed bytes and the pairs fit its bound), 2 never */
+#define SED_OPT_DOT 10          /* checkpoint batches of the stripe kernel and CHAIN batches: 0 auto (dot keys when
+                                   the cost table's update addends factor over signed bytes and the pairs fit the
+                                   bound), 2 never */
 #define SED_OPT_DEBUG_CORRUPT 9 /* testing only: p + 1 overwrites one checkpoint word of pair p before its traceback,
                                    which must then fail with SED_E_DEVICE naming the pair; 0 off */
 
@@ -125,7 +126,8 @@ int sed_batch_rows_per_lane(const sed_batch *b);
 int sed_batch_lane_pairs(const sed_batch *b);         /* pairs on the lane-per-pair kernel (short str2) */
 int sed_batch_chains(const sed_batch *b);             /* CHAIN mode: number of chains (0 = not used) */
 int sed_batch_packed_pairs(const sed_batch *b);       /* pairs computed two per lane / wave (SED_OPT_PACK) */
-int sed_batch_dot_keys(const sed_batch *b);           /* 1: the checkpoint forward kernel runs dot keys (SED_OPT_DOT) */
+int sed_batch_dot_keys(const sed_batch *b);           /* bit 0: the checkpoint forward kernel runs dot keys, bit 1: the
+                                                         CHAIN kernel runs ladder dot keys (SED_OPT_DOT) */
 int sed_batch_traceback_mode(const sed_batch *b);     /* 0 no script, 1 per-cell codes, 2 checkpoints (SED_OPT_TB),
                                                          3 per-cell codes walked stripe-parallel (<= 64 pairs, R = 4) */
 /* CHAIN diagnostics of the last run (waits for it): pairs handed out by the dynamic-CHAIN device counter, and

@@ -55,6 +55,10 @@ struct sed_i32_params {
     uint32_t dot;  // 1: the CK forward kernel runs dot keys, the CK traceback converts them
     uint32_t dotA, dotkmax, dotM, dotS;
     uint32_t dotrow[4], dotcol[4];
+    // Ladder dot keys (CHAIN kernel with the L field): V = D*ladA + 8L over the ladder, the update addend of a d = -1
+    // row -(ladA*kappa + 7) = dot4(ladrow[a], ladcol[b]) (sed_kernels.hip: i32_step LDOT)
+    uint32_t lad, ladA, ladsent;
+    uint32_t ladrow[4], ladcol[4];
 };
 
 struct sed_f64_params {

@@ -192,7 +192,8 @@ template <int R> struct Ladder {
 // sed_wf_i32_kernel), instead of flowing from lane 0 through a DPP move (one DPP + one copy per step).
 // TOPC: lane 0's top is the row-0 constant, which its top_prev already holds (single-stripe pairs: the CHAIN
 // kernel), so the DPP move writes over top_prev in place instead of over a copy of tv.x.
-template <int R, bool TB, bool LEN, bool COLLECT = true, bool SELL = false, bool TOPC = false, bool DOT = false>
+template <int R, bool TB, bool LEN, bool COLLECT = true, bool SELL = false, bool TOPC = false, bool DOT = false,
+          bool LDOT = false>
 __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                          uint32_t &bottom, uint32_t &selv, const uint2 tv, uint32_t &outc,
                                          uint32_t (&W)[4], const int u) {
@@ -202,6 +203,39 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
     constexpr int d0 = Lad::rung(1) - Lad::rung(0);
     // row 0's update candidate from top_prev, before the DPP move overwrites top_prev in place (TOPC): the
     // empty asm makes the move's `old` depend on it, so top_prev needs no copy
+    if constexpr (LEN && LDOT) {
+        // ladder keys with the update addend as one v_dot4 (ladder dot keys, sed_runtime.cpp: dot_ladder): the
+        // addend of a row whose rung steps down by one (d = -1, 13 of 16 rows) is -(A*kappa + 7) = the dot of the
+        // row's and the column's byte vectors (column vectors negated by the host); a row with another step adds
+        // d + 1 to it, which is where the perm took its inline constant d - 6.  Candidates run 4 rows ahead of the
+        // min chain (dot_add).  Per cell: v_dot4, v_min3, v_and_or, v_alignbit = 4 VALU (5 with the perm).
+        using Lad = Ladder<R>;
+        constexpr int AH = R < 4 ? R : 4;
+        uint32_t cand[R];
+        cand[0] = dot_add(cv[0], selv, top_prev);
+#pragma unroll
+        for (int r = 1; r < AH; ++r) cand[r] = dot_add(cv[r], selv, V[r - 1]);
+        const uint32_t topv = dpp_shr1(TOPC ? top_prev : tv.x, bottom);
+        uint32_t up = topv;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (r + AH < R) cand[r + AH] = dot_add(cv[r + AH], selv, V[r + AH - 1]);
+            dot_fence(cand[r]);
+            const int c = Lad::rung(r + 1), d = c - Lad::rung(r);  // compile-time after unrolling
+            const uint32_t upd = d == -1 ? cand[r] : cand[r] + (uint32_t)(d + 1);
+            const uint32_t mm = umin3(V[r], d == -1 ? up : up + (uint32_t)(d + 1), upd);
+            if constexpr (TB) {
+                const int k = u * R + r;
+                W[k >> 4] = __builtin_amdgcn_alignbit(mm, W[k >> 4], 2);
+            }
+            up = (mm & ~7u) | (uint32_t)c;
+            V[r] = up;
+        }
+        top_prev = topv;
+        bottom = V[R - 1];
+        if constexpr (COLLECT) outc = dpp_shl1(bottom, outc);
+        return;
+    }
     if constexpr (DOT) {  // dot keys: maximise, the update addend is one v_dot4 of signed bytes
         // candidates run 4 rows ahead of the max chain (the dot's result hazard, dot_add): row r + 4's diagonal is
         // still the old value of row r + 3 when row r is updated
@@ -276,9 +310,14 @@ __device__ __forceinline__ uint2 dot_split(uint32_t w, const sed_i32_params &prm
     const uint32_t X = __umulhi(k, prm.dotM) >> (prm.dotS - 32u);  // dotM carries kmax (one v_mul_hi, full-rate rest)
     return make_uint2(X, k - __umul24(prm.dotA, X));
 }
-template <int R, bool LEN, bool WANT_L = false, bool DOT = false>
+template <int R, bool LEN, bool WANT_L = false, bool DOT = false, bool LDOT = false>
 __device__ __forceinline__ int2 i32_decode(uint32_t w, int n, int m, const sed_i32_params &prm) {
-    if constexpr (DOT) {  // D = n*delete + m*insert - X, L = n + m - U
+    if constexpr (LEN && LDOT) {  // V = D*A + 8L (the host keeps 8 (n + m) + 7 < A): one division per pair
+        const uint32_t v = w - SED_KB3 - (uint32_t)Ladder<R>::rung(n) + (uint32_t)n * (prm.del * prm.ladA + 8u) +
+                           (uint32_t)m * (prm.ins * prm.ladA + 8u);
+        const uint32_t D = v / prm.ladA;
+        return make_int2((int)D, (int)((v - D * prm.ladA) >> 3));
+    } else if constexpr (DOT) {  // D = n*delete + m*insert - X, L = n + m - U
         const uint2 xu = dot_split(w, prm);
         return make_int2((int)((uint32_t)n * prm.del + (uint32_t)m * prm.ins - xu.x), n + m - (int)xu.y);
     } else if constexpr (LEN) {
@@ -813,7 +852,7 @@ __device__ __forceinline__ chain_pair_state chain_load(const sed_pair_desc *__re
 // Lane 0's top value is row 0 (single-stripe pairs); every lane reads its str2 selector from the wave's
 // selector ring by global column s - t (lsel: this lane's column at the group's first step), which always
 // belongs to the pair the lane is working on: lane t is on the pair starting at T exactly when s - t >= T.
-template <int R, bool TB, bool LEN, bool SW, bool GEN, bool CK>
+template <int R, bool TB, bool LEN, bool SW, bool GEN, bool CK, bool LDOT = false>
 __device__ __forceinline__ void i32_chain_group(uint32_t (&V)[R], uint32_t (&cv)[R], const uint32_t (&cvn)[R],
                                                 const uint32_t (&Vb)[R], const uint32_t tpb, uint32_t &top_prev,
                                                 uint32_t &bottom, uint32_t &selv, const uint32_t *__restrict__ lsel,
@@ -828,7 +867,7 @@ __device__ __forceinline__ void i32_chain_group(uint32_t (&V)[R], uint32_t (&cv)
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         const int s = s0 + u;
-        i32_step<R, TB, LEN, false, true, true>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u);
+        i32_step<R, TB, LEN, false, true, true, false, LDOT>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u);
         if constexpr (CK) rcv[u] = V[R - 1];  // the band's bottom row (row checkpoints), before any switch
         if constexpr (GEN) {
             const bool hA = (s == csA) && (lane == clA), hB = (s == csB) && (lane == clB);
@@ -850,10 +889,10 @@ __device__ __forceinline__ void i32_chain_group(uint32_t (&V)[R], uint32_t (&cv)
     }
 }
 
-template <int R, bool TB, bool LEN, bool CK>
+template <int R, bool TB, bool LEN, bool CK, bool LDOT = false>
 __device__ __forceinline__ void chain_store_result(sed_result *__restrict__ res, int pair, uint32_t cap, int n,
                                                    int m, int seq, const sed_i32_params &prm) {
-    const int2 dl = i32_decode<R, LEN, CK>(cap, n, m, prm);
+    const int2 dl = i32_decode<R, LEN, CK, false, LDOT>(cap, n, m, prm);
     res[pair].dist = (double)dl.x;
     res[pair].len = dl.y;
     res[pair].is_int = (dl.x == 0);
@@ -867,7 +906,7 @@ template <int R> struct ChainWaves { static constexpr int value = R >= 16 ? 4 : 
 // CK: distance keys, and checkpoints instead of codes (the stripe kernel's layout, one stripe per pair).  At every
 // chunk end all lanes are on the pair lane 0 is on (a lane switches at most 63 steps after lane 0), so the column
 // checkpoints go to that pair; a row-checkpoint group of a switch window goes to both pairs, like the codes.
-template <int R, bool TB, bool LEN, bool CK = false>
+template <int R, bool TB, bool LEN, bool CK = false, bool LDOT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainWaves<R>::value))) void
 sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restrict__ chain_pairs,
                         const int32_t *__restrict__ chain_off, int nchains, uint32_t *__restrict__ counter,
@@ -912,14 +951,20 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
         for (int r = 0; r < R; ++r) {
             const int ri = row0 + r;
             const uint32_t a = (pa[ri >> 4] >> ((ri & 15) * 2)) & 3u;
-            out[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
+            if constexpr (LDOT) out[r] = a == 0 ? prm.ladrow[0] : a == 1 ? prm.ladrow[1] : a == 2 ? prm.ladrow[2] : prm.ladrow[3];
+            else out[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
         }
     };
     auto chunk_of = [&](const chain_pair_state &c, int cl) -> uint2 {  // lane 0's inputs, local chunk cl
         const int j = 64 * cl + lane;
         const uint32_t b = (c.pb[j >> 4] >> ((j & 15) * 2)) & 3u;
+        if constexpr (LDOT)
+            return make_uint2(i32_row0<LEN>(), b == 0 ? prm.ladcol[0] : b == 1 ? prm.ladcol[1] : b == 2 ? prm.ladcol[2] : prm.ladcol[3]);
         return make_uint2(i32_row0<LEN>(), i32_sel(b));  // row 0, str2 selector
     };
+    // ladder dot keys: the host's column vector {s, 0, 0, 0} adds s*x in [8, 490] (above any jump, and the border
+    // SED_KB3 + c(i) plus it stays below 2^32)
+    const uint32_t sent = LDOT ? prm.ladsent : i32_sent<LEN>();
 
     chain_pair_state cur = chain_load<R>(pd, seqb, chain_pairs[c0], 0), prv = cur;
     bool have_cur = true, have_prv = false;
@@ -932,11 +977,11 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
         V[r] = Vb[r];
         cvn[r] = cv[r];
     }
-    uint32_t top_prev = tpb, bottom = V[R - 1], selv = i32_sent<LEN>(), outc = 0, capA = 0, capB = 0;
+    uint32_t top_prev = tpb, bottom = V[R - 1], selv = sent, outc = 0, capA = 0, capB = 0;
     uint32_t W[4] = {0, 0, 0, 0};
     uint32_t rcv[G];
     ring[lane] = ring[lane + 128] = chunk_of(cur, 0).y;
-    ring[lane + 64] = ring[lane + 192] = i32_sent<LEN>();
+    ring[lane + 64] = ring[lane + 192] = sent;
 
     for (int s0 = 0;; s0 += 64) {
         // prefetch the next chunk's lane-0 inputs (this pair's next chunk, or the next pair's first)
@@ -964,7 +1009,7 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
             // wave-uniform: which body; Tsw never matches a lane outside a switch window
             const int Tsw = win ? cur.T : -(1 << 30);
 #define SED_CGROUP(SW, GEN)                                                                               \
-    i32_chain_group<R, TB, LEN, SW, GEN, CK>(V, cv, cvn, Vb, tpb, top_prev, bottom, selv, lsel, outc, W, s, lane, \
+    i32_chain_group<R, TB, LEN, SW, GEN, CK, LDOT>(V, cv, cvn, Vb, tpb, top_prev, bottom, selv, lsel, outc, W, s, lane, \
                                              Tsw, prv.cap_step, prv.cap_lane, prv.cap_row, capA, cur.cap_step,    \
                                              cur.cap_lane, cur.cap_row, capB, rcv)
             if (capg) SED_CGROUP(false, true);
@@ -1000,9 +1045,9 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
             }
             if (capg) {
                 if (have_prv && prv.cap_step >= s && prv.cap_step < s + G && lane == prv.cap_lane)
-                    chain_store_result<R, TB, LEN, CK>(res, prv.pair, capA, prv.n, prv.m, ord_prv, prm);
+                    chain_store_result<R, TB, LEN, CK, LDOT>(res, prv.pair, capA, prv.n, prv.m, ord_prv, prm);
                 if (have_cur && cur.cap_step >= s && cur.cap_step < s + G && lane == cur.cap_lane)
-                    chain_store_result<R, TB, LEN, CK>(res, cur.pair, capB, cur.n, cur.m, ord, prm);
+                    chain_store_result<R, TB, LEN, CK, LDOT>(res, cur.pair, capB, cur.n, cur.m, ord, prm);
             }
         }
         if constexpr (CK) {  // column checkpoint of cur's local chunk: every lane is on cur at a chunk end
@@ -2074,9 +2119,9 @@ static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
     return hipGetLastError();
 }
 
-template <int R, bool TB, bool LEN, bool CK = false>
+template <int R, bool TB, bool LEN, bool CK = false, bool LDOT = false>
 static hipError_t launch_chain_R(const sed_launch &L, const sed_i32_params &prm) {
-    SED_LAUNCH((sed_wf_i32_chain_kernel<R, TB, LEN, CK>), dim3((L.nchains + 3) / 4), dim3(256), 0, L, L.pd,
+    SED_LAUNCH((sed_wf_i32_chain_kernel<R, TB, LEN, CK, LDOT>), dim3((L.nchains + 3) / 4), dim3(256), 0, L, L.pd,
                        L.chain_pairs, L.chain_off, L.nchains, L.chain_counter, L.chain_base, L.chain_list,
                        (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.res, prm);
     return hipGetLastError();
@@ -2095,6 +2140,9 @@ hipError_t sed_launch_i32_chain(const sed_launch &L, const sed_i32_params &prm, 
     switch (L.R) {
 #define CASE(RR)                                                                                   \
     case RR:                                                                                       \
+        if (prm.lad && len)                                                                        \
+            return tb ? launch_chain_R<RR, true, true, false, true>(L, prm)                       \
+                      : launch_chain_R<RR, false, true, false, true>(L, prm);                      \
         return tb ? launch_chain_R<RR, true, true>(L, prm)                                         \
                   : (len ? launch_chain_R<RR, false, true>(L, prm) : launch_chain_R<RR, false, false>(L, prm));
         CASE(4) CASE(8) CASE(16)

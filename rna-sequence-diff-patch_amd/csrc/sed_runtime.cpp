@@ -94,6 +94,7 @@ struct sed_batch {
     bool split = false;
     bool ck = false;           // traceback from checkpoints + recompute (sed_kernels.hip: CK) instead of codes
     bool dot = false;          // CK forward kernel on dot keys (dot_keys below)
+    bool lad = false;          // CHAIN kernel with the L field on ladder dot keys (dot_keys ladder mode)
     int nlane = 0, nwave = 0;  // pairs on the lane-per-pair kernel / on the wave kernels
     int nlane_x2 = 0;          // > 0: lane pairs run two per lane (distance only), in this many lanes
     int nwave_x2 = 0;          // distance-only wave pairs of equal shape run two per wave, in this many waves
@@ -168,8 +169,12 @@ int64_t gcd64(int64_t a, int64_t b) {
     }
     return a;
 }
-// kap: kappa[a][b] (>= 1); maxmin: the largest min(n, m) of the batch's wave pairs
-DotKeys dot_keys(const int64_t kap[4][4], int64_t maxmin) {
+// kap: kappa[a][b] (>= 1); maxmin: the largest min(n, m) of the batch's wave pairs.
+// Ladder mode (lad_amin > 0, lad_beta): the factorisation of A*K + lad_beta*J for the per-cell-code kernels'
+// ladder keys with A >= lad_amin and A < 2^16 (dot_ladder below); no ordering bound or decode constants.
+DotKeys dot_keys(const int64_t kap[4][4], int64_t maxmin, int64_t lad_amin = 0, int64_t lad_beta = 0) {
+    const bool lad = lad_amin > 0;
+    const int64_t beta = lad ? lad_beta : 1;
     DotKeys dk;
     int64_t kmax = 0, kmin = INT64_MAX;
     for (int a = 0; a < 4; ++a)
@@ -240,8 +245,9 @@ DotKeys dot_keys(const int64_t kap[4][4], int64_t maxmin) {
     const int64_t a_hi = num != 0 ? (127 * 127 + 127) / (num < 0 ? -num : num) : 127 * 127;  // |num a + 1| <= 127^2
     for (int64_t a = a_hi; a >= 1; --a) {
         const int64_t A = den * a;
-        if (A * kmin <= maxmin * (kmax - kmin)) break;  // the ordering bound fails for every smaller a too
-        const int64_t J = num * a + 1;
+        if (lad ? A < lad_amin : A * kmin <= maxmin * (kmax - kmin)) break;  // fails for every smaller a too
+        if (lad && A >= 65536) continue;
+        const int64_t J = num * a + beta;
         int64_t x = 0, y = 0;
         for (int64_t t = 1; t <= 127 && !x; ++t)
             if (J % t == 0 && (J / t >= -127 && J / t <= 127)) { x = t; y = J / t; }
@@ -257,7 +263,7 @@ DotKeys dot_keys(const int64_t kap[4][4], int64_t maxmin) {
         }
         if (!fit) continue;
         // decode: k * kmax < 2^29 over every real cell (k <= A * kmax * maxmin + maxmin)
-        if ((A * kmax * maxmin + maxmin) * kmax >= (int64_t)1 << 29) continue;
+        if (!lad && (A * kmax * maxmin + maxmin) * kmax >= (int64_t)1 << 29) continue;
         int8_t R[4][4], C[4][4];
         for (int i = 0; i < 4; ++i) {
             R[i][0] = (int8_t)x;
@@ -271,11 +277,28 @@ DotKeys dot_keys(const int64_t kap[4][4], int64_t maxmin) {
             for (int j = 0; j < 4; ++j) {
                 int64_t t = 0;
                 for (int k = 0; k < 4; ++k) t += (int64_t)R[i][k] * C[j][k];
-                if (t != A * kap[i][j] + 1) return dk;
+                if (t != A * kap[i][j] + beta) return dk;
             }
         dk.A = (uint32_t)A;
         dk.kmax = (uint32_t)kmax;
         dk.kmin = (uint32_t)kmin;
+        if (lad) {  // min-form ladder keys add -(A*kappa + beta): the column vectors are negated
+            for (int i = 0; i < 4; ++i) {
+                uint32_t rw = 0, cw = 0;
+                for (int k = 0; k < 4; ++k) {
+                    rw |= (uint32_t)(uint8_t)R[i][k] << (8 * k);
+                    cw |= (uint32_t)(uint8_t)(int8_t)(-C[i][k]) << (8 * k);
+                }
+                dk.row[i] = rw;
+                dk.col[i] = cw;
+            }
+            // the virtual-column sentinel {s, 0, 0, 0} adds s x in [8, 490]: above every ladder jump, and below the
+            // 512 the border leaves to 2^32 (sed_kernels.hip: SED_KB3)
+            const int64_t sx = x > 0 ? (8 + x - 1) / x : 0;
+            dk.ok = x > 0 && sx * x <= 490;
+            dk.S = (uint32_t)sx;
+            return dk;
+        }
         const uint64_t Dd = (uint64_t)A * kmax + 1;
         int lg = 0;
         while (((uint64_t)1 << lg) < Dd) ++lg;
@@ -735,6 +758,28 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
                 b->dot = true;
             }
         }
+        // ladder dot keys: the CHAIN kernel's ladder keys (L field, with or without codes) with the update addend
+        // as one v_dot4.  V = D*A + 8L needs 8 (n + m) + 7 < A < 2^16 (the L field below the D unit), and the
+        // factorisation of A*K + 7J (the d = -1 rows' constant -6 + d = -7) must fit bytes.
+        b->lad = false;
+        if (b->nchains > 0 && !b->ck && (want_tb || !(flags & SED_NO_LEN)) && c->K == 4 && c->opt_dot != 2) {
+            int64_t kap[4][4], maxsum = 0;
+            for (int a = 0; a < 4; ++a)
+                for (int bb = 0; bb < 4; ++bb) kap[a][bb] = (int64_t)ip.ins + ip.del - (int64_t)c->sub[a * 4 + bb];
+            for (int p = 0; p < npairs; ++p)
+                if (!b->pd[p].lane) maxsum = std::max<int64_t>(maxsum, (int64_t)len_a[p] + len_b[p]);
+            const DotKeys lk = dot_keys(kap, 0, 8 * maxsum + 8, 7);
+            if (lk.ok) {
+                ip.lad = 1;
+                ip.ladA = lk.A;
+                ip.ladsent = lk.S;  // (ladder mode: the sentinel's byte 0)
+                for (int a = 0; a < 4; ++a) {
+                    ip.ladrow[a] = lk.row[a];
+                    ip.ladcol[a] = lk.col[a];
+                }
+                b->lad = true;
+            }
+        }
         b->ip = ip;
     } else {
         sed_f64_params fp{};
@@ -1084,7 +1129,7 @@ int sed_batch_traceback_mode(const sed_batch *b) {
     return b->ck ? 2 : (b->tbpar ? 3 : 1);
 }
 
-int sed_batch_dot_keys(const sed_batch *b) { return b ? (b->dot ? 1 : 0) : SED_E_ARG; }
+int sed_batch_dot_keys(const sed_batch *b) { return b ? (b->dot ? 1 : 0) | (b->lad ? 2 : 0) : SED_E_ARG; }
 
 int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave) {
     if (!b) return SED_E_ARG;

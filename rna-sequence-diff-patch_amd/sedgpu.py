@@ -287,7 +287,12 @@ class Batch:
     @property
     def dot_keys(self):
         """True when the checkpoint forward kernel runs dot keys (v_dot4 + v_max3 per cell, SED_OPT_DOT)."""
-        return self._lib.sed_batch_dot_keys(self.ptr) == 1
+        return (self._lib.sed_batch_dot_keys(self.ptr) & 1) == 1
+
+    @property
+    def ladder_dot_keys(self):
+        """True when the CHAIN kernel runs ladder keys with the update addend as one v_dot4 (SED_OPT_DOT)."""
+        return (self._lib.sed_batch_dot_keys(self.ptr) & 2) == 2
 
     @property
     def traceback_mode(self):

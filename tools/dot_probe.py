@@ -10,7 +10,9 @@ import oracle, sedcost, sedgpu
 
 ctx = sedgpu.Context(0)
 rng = np.random.default_rng(5)
-cases = [(100, 100), (64, 64), (1, 1), (5, 70), (300, 200), (1024, 1024), (1030, 700), (2000, 2600)]
+CHAIN = len(sys.argv) > 1 and sys.argv[1] == "chain"
+cases = ([(100, 100), (64, 64), (1, 1), (5, 70), (256, 200), (250, 700), (3, 3), (200, 64)] if CHAIN else
+         [(100, 100), (64, 64), (1, 1), (5, 70), (300, 200), (1024, 1024), (1030, 700), (2000, 2600)])
 pairs = []
 for n, m in cases:
     a = "".join(rng.choice(list("ACGU"), size=n))
@@ -23,15 +25,16 @@ for user in (False, True):
     ctx.set_costs(plan)
     packed = sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs], [plan.encode(b) for _, b in pairs])
     for dot in (0, 2):
-        ctx.set_option(sedgpu.SED_OPT_TB, 2)
-        ctx.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 16)
+        ctx.set_option(sedgpu.SED_OPT_TB, 1 if CHAIN else 2)
+        ctx.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 4 if CHAIN else 16)
+        ctx.set_option(sedgpu.SED_OPT_CHAIN, 1 if CHAIN else 0)
         ctx.set_option(sedgpu.SED_OPT_SPLIT, 2)
         ctx.set_option(sedgpu.SED_OPT_LANE, 2)
         ctx.set_option(sedgpu.SED_OPT_DOT, dot)
         b = sedgpu.Batch(ctx, packed, True)
         b.run()
         dist, is_int, ln, ops = b.results()
-        print("user", user, "dot_keys", b.dot_keys)
+        print("user", user, "dot_keys", b.dot_keys, "ladder", b.ladder_dot_keys, "chains", b.chains)
         b.close()
         for p, (x, y) in enumerate(pairs):
             o = oracle.pair(cs, plan.encode(x), plan.encode(y))
