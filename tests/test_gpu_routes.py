@@ -89,9 +89,24 @@ def test_dynamic_chain_config3_route(gpu, tables, user):
                 assert b.traceback_mode == (0 if not script else 2 if tb == 2 else 1)
                 fetched, per_wave = b.chain_stats()
                 assert fetched == nwave and per_wave >= 2, (fetched, nwave, per_wave)
+                # costs.json's addends factor over bytes with A > 8 (n + m): the ladder keys run on v_dot4
+                # (user_costs' would need A > 8 * 1212 with kappa up to 5: no byte factorisation that large)
+                assert b.ladder_dot_keys == (not user and tb != 2)
         finally:
             b.close()
         _check_all(plan, packed, d, ii, ln, ops, script=script, no_len=no_len)
+    # the ladder dot keys against the perm ladder on the same batch (SED_OPT_DOT = 2)
+    if not user:
+        gpu.set_option(sedgpu.SED_OPT_DOT, 2)
+        try:
+            b, (d2, ii2, ln2, ops2) = _batch_run(gpu, packed, True)
+            try:
+                assert not b.ladder_dot_keys and b.chains == 5120
+            finally:
+                b.close()
+        finally:
+            gpu.set_option(sedgpu.SED_OPT_DOT, 0)
+        _check_all(plan, packed, d2, ii2, ln2, ops2)  # (the packed buffers' bits past each script may differ)
 
 
 def test_dynamic_chain_capped_waves(gpu, tables):
