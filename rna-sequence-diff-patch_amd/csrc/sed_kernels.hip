@@ -95,6 +95,12 @@ __device__ __forceinline__ uint32_t dot_add(uint32_t rowv, uint32_t colv, uint32
     asm volatile("v_dot4_i32_i8 %0, %1, %2, %3" : "=v"(r) : "v"(rowv), "v"(colv), "v"(diag));
     return r;
 }
+// dots issued ahead of the max / min chain (>= 4: tools/ubench/dot_sem.hip shows the next op reading stale data;
+// the fence then leaves 3 or more instructions between a dot and its reader).  A/B on config 4's forward kernel
+// (tools/ab.sh, profiles/r02_dot/ab_ahead.jsonl): 4 -> 9.24-9.33 ms, 6 same, 8 -> 9.16-9.23 ms, 12 9.29, 16 9.18.
+#ifndef SED_DOT_AHEAD
+#define SED_DOT_AHEAD 8
+#endif
 // an empty volatile asm on a dot result, placed after the dots that must separate it from its consumer: the
 // consumer cannot be scheduled above it.  (The compiler treats the asm as a write of x and puts an s_nop 0 between
 // it and the max reading x, 50 per 64-cell group.  Fencing one row earlier drops that to 29 but lets the compiler
@@ -239,7 +245,7 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
     if constexpr (DOT) {  // dot keys: maximise, the update addend is one v_dot4 of signed bytes
         // candidates run 4 rows ahead of the max chain (the dot's result hazard, dot_add): row r + 4's diagonal is
         // still the old value of row r + 3 when row r is updated
-        constexpr int AH = R < 4 ? R : 4;
+        constexpr int AH = R < SED_DOT_AHEAD ? R : SED_DOT_AHEAD;
         uint32_t cand[R];
         cand[0] = dot_add(cv[0], selv, top_prev);
 #pragma unroll
@@ -249,7 +255,7 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (r + AH < R) cand[r + AH] = dot_add(cv[r + AH], selv, V[r + AH - 1]);
-            dot_fence(cand[r]);  // row r's candidate was issued 4 dots ago
+            dot_fence(cand[r]);  // row r's candidate was issued AH dots ago
             up = umax3(V[r], up, cand[r]);
             V[r] = up;
         }
@@ -901,7 +907,10 @@ __device__ __forceinline__ void chain_store_result(sed_result *__restrict__ res,
 }
 
 // the chain kernel also holds the next pair's cost rows and the column-0 constants
-template <int R> struct ChainWaves { static constexpr int value = R >= 16 ? 4 : 5; };
+#ifndef SED_CHAIN_WAVES
+#define SED_CHAIN_WAVES 5
+#endif
+template <int R> struct ChainWaves { static constexpr int value = R >= 16 ? 4 : SED_CHAIN_WAVES; };
 
 // CK: distance keys, and checkpoints instead of codes (the stripe kernel's layout, one stripe per pair).  At every
 // chunk end all lanes are on the pair lane 0 is on (a lane switches at most 63 steps after lane 0), so the column
