@@ -126,6 +126,12 @@ int sed_batch_rows_per_lane(const sed_batch *b);
 int sed_batch_lane_pairs(const sed_batch *b);         /* pairs on the lane-per-pair kernel (short str2) */
 int sed_batch_chains(const sed_batch *b);             /* CHAIN mode: number of chains (0 = not used) */
 int sed_batch_packed_pairs(const sed_batch *b);       /* pairs computed two per lane / wave (SED_OPT_PACK) */
+/* The byte factorisation behind SED_OPT_DOT, without a device (tests): for the 4 x 4 table sub (a -> b, row-major)
+ * and insert/delete costs, the dot keys for pairs with min(n, m) <= maxmin (ladder_maxsum = 0) or the ladder dot
+ * keys for n + m <= ladder_maxsum.  out[0..3] = row vectors, out[4..7] = column vectors (4 signed bytes each),
+ * out[8] = decode shift / ladder sentinel byte, out[9] = decode multiplier.  Returns A (> 0), 0 when the table has
+ * no such factorisation, or SED_E_ARG. */
+int sed_dot_factor(const double *sub, double ins, double del, int maxmin, int ladder_maxsum, uint32_t *out);
 int sed_batch_dot_keys(const sed_batch *b);           /* bit 0: the checkpoint forward kernel runs dot keys, bit 1: the
                                                          CHAIN kernel runs ladder dot keys (SED_OPT_DOT) */
 int sed_batch_traceback_mode(const sed_batch *b);     /* 0 no script, 1 per-cell codes, 2 checkpoints (SED_OPT_TB),

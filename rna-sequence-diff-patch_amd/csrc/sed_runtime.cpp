@@ -1129,6 +1129,26 @@ int sed_batch_traceback_mode(const sed_batch *b) {
     return b->ck ? 2 : (b->tbpar ? 3 : 1);
 }
 
+int sed_dot_factor(const double *sub, double ins, double del, int maxmin, int ladder_maxsum, uint32_t *out) {
+    if (!sub || !out || maxmin < 0 || ladder_maxsum < 0) return SED_E_ARG;
+    int64_t kap[4][4];
+    for (int a = 0; a < 4; ++a)
+        for (int bb = 0; bb < 4; ++bb) {
+            const double v = ins + del - sub[a * 4 + bb];
+            if (v != (double)(int64_t)v) return 0;  // integer tables only (the packed-integer kernels' domain)
+            kap[a][bb] = (int64_t)v;
+        }
+    const DotKeys dk = ladder_maxsum > 0 ? dot_keys(kap, 0, 8 * (int64_t)ladder_maxsum + 8, 7) : dot_keys(kap, maxmin);
+    if (!dk.ok) return 0;
+    for (int a = 0; a < 4; ++a) {
+        out[a] = dk.row[a];
+        out[4 + a] = dk.col[a];
+    }
+    out[8] = dk.S;  // decode shift (dot keys) or sentinel byte (ladder)
+    out[9] = dk.M;
+    return (int)dk.A;
+}
+
 int sed_batch_dot_keys(const sed_batch *b) { return b ? (b->dot ? 1 : 0) | (b->lad ? 2 : 0) : SED_E_ARG; }
 
 int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave) {

@@ -65,6 +65,7 @@ SIGNATURES = [
     ("sed_batch_lane_pairs", C.c_int, [C.c_void_p]),
     ("sed_batch_chains", C.c_int, [C.c_void_p]),
     ("sed_batch_dot_keys", C.c_int, [C.c_void_p]),
+    ("sed_dot_factor", C.c_int, [_f64p, C.c_double, C.c_double, C.c_int, C.c_int, _u32p]),
     ("sed_batch_packed_pairs", C.c_int, [C.c_void_p]),
     ("sed_batch_traceback_mode", C.c_int, [C.c_void_p]),
     ("sed_batch_chain_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
@@ -528,3 +529,17 @@ def context(device=None):
 
 if __name__ == "__main__" and len(sys.argv) == 5 and sys.argv[1] == "--engine-worker":
     _engine_worker(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))
+
+
+def dot_factor(sub, ins, dele, maxmin=0, ladder_maxsum=0):
+    """The byte factorisation behind SED_OPT_DOT (no device needed): (A, rows, cols, aux) or None.
+    sub: 4 x 4 costs (row symbol -> column symbol); rows/cols: 4 x 4 signed bytes."""
+    out = np.zeros(10, np.uint32)
+    A = load().sed_dot_factor(np.ascontiguousarray(sub, np.float64).ravel(), float(ins), float(dele), int(maxmin),
+                              int(ladder_maxsum), out)
+    if A < 0:
+        raise SedError("sed_dot_factor: bad arguments")
+    if A == 0:
+        return None
+    to_bytes = lambda w: np.frombuffer(np.asarray(w, np.uint32).tobytes(), np.int8).reshape(4, 4).astype(np.int64)
+    return A, to_bytes(out[0:4]), to_bytes(out[4:8]), (int(out[8]), int(out[9]))

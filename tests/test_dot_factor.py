@@ -1,0 +1,54 @@
+"""CPU: the signed-byte factorisations behind the dot keys (sed_runtime.cpp: dot_keys, via sed_dot_factor).
+The checkpoint forward kernel adds dot4(row(a), col(b)) = A*kappa(a, b) + 1 to the diagonal and maximises; the
+CHAIN kernel's ladder keys add -(A*kappa + 7).  Checked here for both shipped tables: exact products, byte ranges,
+the ordering bound A > min(n, m) (kmax - kmin) / kmin, the decode multiply-shift, and the ineligible cases."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+import sedgpu
+
+S = "ACGU"
+
+
+def _table(name):
+    t = load_golden(name)
+    sub = np.array([[0.0 if a == b else t["update"][a][b] for b in S] for a in S])
+    return sub, t["insert"], t["delete"]
+
+
+@pytest.mark.parametrize("name, maxmin, want_A", [("user_costs.json", 4096, 2880), ("costs.json", 4096, 12700)])
+def test_dot_keys_factorisation(name, maxmin, want_A):
+    sub, ins, dele = _table(name)
+    got = sedgpu.dot_factor(sub, ins, dele, maxmin=maxmin)
+    assert got is not None
+    A, rows, cols, (shift, mult) = got
+    assert A == want_A
+    kap = (ins + dele - sub).astype(np.int64)
+    assert np.array_equal(rows @ cols.T, A * kap + 1)  # v_dot4_i32_i8 of row and column vectors
+    assert np.abs(rows).max() <= 127 and np.abs(cols).max() <= 127
+    kmin, kmax = kap.min(), kap.max()
+    assert A * kmin > maxmin * (kmax - kmin)  # candidates' U spread below A
+    # decode X = floor(k kmax / (A kmax + 1)) by (k * mult) >> shift on keys k = A X + U of real paths
+    rng = np.random.default_rng(1)
+    for _ in range(20000):
+        U = int(rng.integers(0, maxmin + 1))
+        X = int(rng.integers(U * kmin, U * kmax + 1))
+        k = A * X + U
+        assert (k * mult) >> shift == X and k - A * X == U
+
+
+def test_dot_keys_bound_and_ladder_eligibility():
+    sub, ins, dele = _table("user_costs.json")
+    assert sedgpu.dot_factor(sub, ins, dele, maxmin=4319) is not None
+    assert sedgpu.dot_factor(sub, ins, dele, maxmin=4320) is None  # 2880 * 3 <= 4320 * 2
+    assert sedgpu.dot_factor(sub, ins, dele, ladder_maxsum=1024) is None  # A > 8 (n + m) does not fit bytes
+    sub, ins, dele = _table("costs.json")
+    A, rows, cols, (sent, _) = sedgpu.dot_factor(sub, ins, dele, ladder_maxsum=1024)
+    kap = (ins + dele - sub).astype(np.int64)
+    assert A >= 8 * 1024 + 8 and A < 65536
+    assert np.array_equal(rows @ cols.T, -(A * kap + 7))  # min-form ladder keys: negated column vectors
+    assert 8 <= sent * rows[0, 0] <= 490 and np.all(rows[:, 0] == rows[0, 0])  # the sentinel column {s, 0, 0, 0}
+    fractional = sub.copy()
+    fractional[0, 1] = 0.5
+    assert sedgpu.dot_factor(fractional, ins, dele, maxmin=100) is None
