@@ -45,6 +45,14 @@ SIMDS, CLOCK = 1024, 2.4e9
 VALU_CYCLES_PER_OP = 4.0
 CELL_OPS = {"script": 5 + 3 / 16, "len": 4 + 3 / 16, "nolen": 3, "nolen_x2": 2, "dot": 2}
 
+
+def lad_ops(R):
+    """Ladder dot keys with per-cell codes (CHAIN kernel): 4 VALU on the ladder's d = -1 rows, 6 on its jump rows
+    (3 of 16 rows at R = 16, 2 of 8 at R = 8, 1 of 4 at R = 4; sed_kernels.hip Ladder<R>)."""
+    jumps = {16: 3, 8: 2, 4: 1}.get(R, 3)
+    period = min(R, 16) if R in (4, 8, 16) else 16
+    return 4.0 + 2.0 * jumps / period
+
 WORKLOADS = {
     # name: (pairs per GPU, n, m, cost table, description)
     "c4": (8192, 4096, 4096, "user_costs.json",
@@ -215,12 +223,9 @@ def cpu_baseline(plan, packed, seconds, threads, want_ops):
             "ops": ops, "ops_off": ops_off}
 
 
-def measure_traffic(kernels):
-    """HBM bytes per launch of `kernels` (summed), measured now: this bench re-run as a child process for one
-    step under rocprofv3, one pass per counter (FETCH_SIZE and WRITE_SIZE do not fit one pass).  Units and the
-    gfx950 correction per MI355X_MICROARCH.md "HBM": both counters in KiB, FETCH_SIZE reports half the bytes of
-    wide streaming reads, so bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.  Returns (bytes, detail) or
-    (None, reason)."""
+def pmc_pass(counters, kernels, timeout=240):
+    """One rocprofv3 --pmc pass over this bench re-run as a child process for one step (no warmup, no CPU legs, no
+    nested measurement).  Returns ({kernel: {counter: value per launch}}, None) or (None, reason)."""
     import csv
     import glob
     import shutil
@@ -231,37 +236,195 @@ def measure_traffic(kernels):
     rp = shutil.which("rocprofv3")
     if rp is None:
         return None, "rocprofv3 not found"
+    d = tempfile.mkdtemp(prefix="sedpmc_", dir="/tmp")
+    # argparse keeps the last occurrence of each flag
+    child = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:] + [
+        "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--traffic", "none"]
+    cmd = ["timeout", "-s", "KILL", str(timeout), rp, "--pmc"] + list(counters) + [
+        "-T", "-d", d, "-o", "pmc", "--output-format", "csv", "--"] + child
+    try:
+        r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                           env=dict(os.environ, TMPDIR="/tmp"), timeout=timeout + 60)
+    except subprocess.TimeoutExpired:
+        return None, "%s pass timed out" % "+".join(counters)
+    vals = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row["Counter_Name"] in counters and row["Kernel_Name"] in kernels:
+                    vals.setdefault(row["Kernel_Name"], {}).setdefault(row["Counter_Name"], []).append(
+                        float(row["Counter_Value"]))
+    shutil.rmtree(d, ignore_errors=True)
+    if r.returncode != 0 or not vals:
+        return None, "%s pass failed (rc %d)" % ("+".join(counters), r.returncode)
+    return {k: {c: sum(v) / len(v) for c, v in cv.items()} for k, cv in vals.items()}, None
+
+
+def measure_traffic(kernels):
+    """HBM bytes per launch of `kernels` (summed), measured now, one pass per counter (FETCH_SIZE and WRITE_SIZE do
+    not fit one pass).  Units and the gfx950 correction per MI355X_MICROARCH.md "HBM": both counters in KiB,
+    FETCH_SIZE reports half the bytes of wide streaming reads, so bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
+    Returns (bytes, detail) or (None, reason)."""
     kib = {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-        d = tempfile.mkdtemp(prefix="sedpmc_", dir="/tmp")
-        # argparse keeps the last occurrence: one untimed-warmup-free step, no CPU legs, no nested measurement
-        child = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:] + [
-            "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--traffic", "none"]
-        cmd = ["timeout", "-s", "KILL", "240", rp, "--pmc", ctr, "-T", "-d", d, "-o", "pmc",
-               "--output-format", "csv", "--"] + child
-        try:
-            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                               env=dict(os.environ, TMPDIR="/tmp"), timeout=300)
-        except subprocess.TimeoutExpired:
-            return None, "%s pass timed out" % ctr
-        vals = {}
-        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-            with open(f) as fh:
-                for row in csv.DictReader(fh):
-                    if row["Counter_Name"] == ctr and row["Kernel_Name"] in kernels:
-                        vals.setdefault(row["Kernel_Name"], []).append(float(row["Counter_Value"]))
-        shutil.rmtree(d, ignore_errors=True)
-        if r.returncode != 0 or not vals:
-            return None, "%s pass failed (rc %d)" % (ctr, r.returncode)
-        kib[ctr] = sum(sum(v) / len(v) for v in vals.values())  # per launch, summed over the kernels
+        got, why = pmc_pass([ctr], kernels)
+        if got is None:
+            return None, why
+        kib[ctr] = sum(v.get(ctr, 0.0) for v in got.values())
     total = 2.0 * kib["FETCH_SIZE"] * 1024.0 + kib["WRITE_SIZE"] * 1024.0
     return total, {"FETCH_SIZE_KiB": kib["FETCH_SIZE"], "WRITE_SIZE_KiB": kib["WRITE_SIZE"],
                    "correction": "KiB; FETCH_SIZE x2 on gfx950 (MI355X_MICROARCH.md HBM)"}
 
 
+def measure_issue(kernels):
+    """VALU / SALU issue per kernel from one SQ pass: SQ_INSTS_VALU and SQ_INSTS_SALU (wave-instructions per launch)
+    and GRBM_GUI_ACTIVE (cycles, summed over the 8 XCDs).  A wave64 VALU instruction occupies its SIMD's issue
+    port 4 cycles (tools/ubench/valu_mix.hip), so valu_issue = SQ_INSTS_VALU * 4 / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8);
+    the scalar unit issues one instruction per CU per cycle, so salu_issue = SQ_INSTS_SALU / 256 CUs / (GRBM / 8)."""
+    got, why = pmc_pass(["SQ_INSTS_VALU", "SQ_INSTS_SALU", "GRBM_GUI_ACTIVE"], kernels)
+    if got is None:
+        return None, why
+    out = {}
+    for k, c in got.items():
+        cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+        if cyc <= 0:
+            continue
+        out[k] = {"SQ_INSTS_VALU": c.get("SQ_INSTS_VALU"), "SQ_INSTS_SALU": c.get("SQ_INSTS_SALU"),
+                  "GRBM_GUI_ACTIVE": c.get("GRBM_GUI_ACTIVE"),
+                  "valu_issue": c.get("SQ_INSTS_VALU", 0.0) * 4.0 / SIMDS / cyc,
+                  "salu_issue": c.get("SQ_INSTS_SALU", 0.0) / (SIMDS / 4) / cyc}
+    return out, None
+
+
+def s8d_bytes(len_a, len_b, script):
+    """SURVEY.md §8(d)'s algorithmic HBM bytes of one launch: 2-bit packed inputs (n+m)/4 + an 8-byte distance per
+    pair; script mode adds the 2-bit traceback choice of every cell (0.25 B/cell), the path's (n+m) sparse reads of
+    it and the (n+m) 2-bit ops out."""
+    n = np.asarray(len_a, np.float64)
+    m = np.asarray(len_b, np.float64)
+    per_pair = (n + m) / 4.0 + 8.0
+    if script:
+        per_pair = per_pair + 0.25 * n * m + (n + m) + (n + m) / 4.0
+    return float(per_pair.sum())
+
+
+def launcher_cmd(n, argv, port):
+    """The torch.distributed.run command bench.py starts for itself when run as `bench.py --gpus N` (N > 1)
+    outside a launcher: one rank per GPU on this node, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def self_launch(n, argv):
+    """Run this bench as n ranks (a child launcher; this process never touches HIP) and return its exit code.
+    The ranks' rank 0 prints the JSON line on the inherited stdout."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    log("bench.py: launching %d ranks: %s" % (n, " ".join(launcher_cmd(n, argv, port))))
+    return subprocess.call(launcher_cmd(n, argv, port), env=env)
+
+
+def refuse_reason(gpus, environ):
+    """Why this rank must not run (None if it may): a world size that differs from --gpus, or a debug switch of
+    the engine in the environment (SED_DEBUG_*, e.g. one that drops work from the timed region)."""
+    world = int(environ.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        return "--gpus %d but WORLD_SIZE=%d: the line would misreport the GPU count" % (gpus, world)
+    dbg = sorted(k for k in environ if k.startswith("SED_DEBUG"))
+    if dbg:
+        return "debug switch(es) %s set: refusing to time the engine under them" % ", ".join(dbg)
+    return None
+
+
+def shard_inputs(workload, P, n, m, world, r):
+    """Rank r's inputs, regenerated from the seeds: (A, B, None, None) for fixed-shape workloads (pair ids
+    [r*P, (r+1)*P)), (None, None, qa, qb) for the all-vs-all rows of config 5."""
+    if workload in ("c5", "c5n"):
+        import sedshard
+        lo, hi = sedshard.shard_range(P, world, r)  # query rows of this rank
+        qa, qb = gen_all_vs_all(P, n_rate=0.01 if workload == "c5n" else 0.0)
+        return None, None, qa[lo * P:hi * P], qb[lo * P:hi * P]
+    ids = np.arange(r * P, (r + 1) * P, dtype=np.uint64)
+    A, B = gen_codes(ids, n, m, workload == "iupac")
+    return A, B, None, None
+
+
+def valid_scripts(plan, A, B, dist, ln, ops, ops_off, exact_int):
+    """Pairs (of A, B) whose script passes script_costs and whose cost equals the reported distance."""
+    good = 0
+    P = A.shape[0]
+    for s0 in range(0, P, 256):
+        sl = slice(s0, min(P, s0 + 256))
+        ok, cost = script_costs(plan, A[sl], B[sl], ln[sl], ops, ops_off[sl])
+        same = (cost == dist[sl]) if exact_int else np.isclose(cost, dist[sl], rtol=1e-12)
+        good += int((ok & same).sum())
+    return good
+
+
+def oracle_agree(plan, packed, count, dist, ln, ops, ops_off, want_script, threads):
+    """Pairs among the first `count` of `packed` whose distance, length and every op equal the C oracle's."""
+    import oracle
+    cs = oracle.Costs.from_plan(plan)
+    od, _, oln, oops, ooff = oracle.batch(cs, packed.codes_a, packed.off_a, packed.len_a, packed.codes_b,
+                                          packed.off_b, packed.len_b, count, want_ops=want_script, nthreads=threads)
+    exact = (od == dist[:count]) & ((oln == ln[:count]) | (ln[:count] == -1))
+    if want_script:
+        for p in range(count):
+            if exact[p]:
+                g = sedgpu.unpack_ops(ops, ops_off, p, int(ln[p]))
+                exact[p] = np.array_equal(g, oops[ooff[p]: ooff[p] + oln[p]])
+    return int(exact.sum())
+
+
+def verify_gathered(args, plan, P, n, m, world, gdist, glen, gops, want_script, mode, threads, seconds):
+    """Rank 0 after the gather: every rank's results, checked on rank 0 (N > 1).  The script property check over
+    ALL gathered pairs (inputs regenerated from the seeds), and an oracle comparison of each rank's leading pairs
+    within `seconds` of CPU time in total.  Returns the bench line's check fields."""
+    exact_int = mode == "i32"
+    valid = total = agree = sampled = 0
+    base = 0
+    per_rank = []
+    for r in range(world):
+        A, B, qa, qb = shard_inputs(args.workload, P, n, m, world, r)
+        packed = sedgpu.PackedPairs.from_arrays(A, B) if A is not None else sedgpu.PackedPairs(qa, qb)
+        Pr = packed.npairs
+        d = gdist[base:base + Pr]
+        ln = glen[base:base + Pr]
+        if want_script:
+            w0 = (n + m + 15) // 16  # script words per pair (fixed shapes)
+            ops = gops[base * w0:(base + Pr) * w0]
+            valid += valid_scripts(plan, A, B, d, ln, ops, packed.ops_off, exact_int)
+        else:
+            ops = None
+        total += Pr
+        # oracle sample: the rank's leading pairs, about seconds / world of single-thread-equivalent work
+        la, lb = packed.len_a[:Pr].astype(np.float64), packed.len_b[:Pr].astype(np.float64)
+        cum = np.cumsum(la * lb)
+        budget = 1.5e8 * threads * seconds / world  # cells; the C oracle runs ~1e8-2e8 cells/s per thread
+        cnt = int(min(Pr, max(1, np.searchsorted(cum, budget))))
+        agree += oracle_agree(plan, packed, cnt, d, ln, ops, packed.ops_off, want_script, threads)
+        sampled += cnt
+        per_rank.append(cnt)
+        base += Pr
+    out = {"verified_on_rank0": {"pairs": total, "oracle_sample_per_rank": per_rank}}
+    if want_script:
+        out["script_valid_rate"] = valid / max(1, total)
+        out["script_exact_rate"] = agree / max(1, sampled)
+    else:
+        out["dist_exact_rate"] = agree / max(1, sampled)
+    out["exact_sample"] = sampled
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (= ranks).  Outside a launcher, N > 1 starts torch.distributed.run with N ranks")
     ap.add_argument("--steps", type=int, default=20)  # per-cell-code batches pipeline traceback k beside DP k+1 (the last one is not overlapped); checkpoint batches run DP then traceback
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
@@ -286,12 +449,19 @@ def main():
                     help="per-launch HBM traffic of the DP kernel from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                          "(tools/profile_round.sh + tools/summarize_profile.py); used when its workload matches")
     ap.add_argument("--traffic", default="measure", choices=["measure", "file", "none"],
-                    help="roofline.traffic: measure = two rocprofv3 --pmc child runs of this workload (FETCH_SIZE, "
-                         "WRITE_SIZE, one step each) on rank 0 at N = 1; file = --pmc-json; none")
+                    help="roofline.traffic and valu.issue: measure = three rocprofv3 --pmc child runs of this "
+                         "workload (FETCH_SIZE, WRITE_SIZE, SQ issue; one step each) on rank 0 at N = 1; "
+                         "file = --pmc-json; none")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse ranks sharing one GPU")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args.gpus, sys.argv[1:]))  # before anything touches HIP
+    why = refuse_reason(args.gpus, os.environ)
+    if why:
+        log("bench.py: " + why)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -322,18 +492,10 @@ def main():
     alpha = synth.IUPAC if iupac else (synth.ALPHABET + "N" if args.workload == "c5n" else synth.ALPHABET)
     plan = sedcost.build_plan(table, [alpha], [alpha])
     t0 = time.perf_counter()
-    if args.workload in ("c5", "c5n"):
-        import sedshard
-        lo, hi = sedshard.shard_range(P, world, rank)  # query rows of this rank
-        qa, qb = gen_all_vs_all(P, n_rate=0.01 if args.workload == "c5n" else 0.0)
-        qa, qb = qa[lo * P:hi * P], qb[lo * P:hi * P]
-        packed = sedgpu.PackedPairs(qa, qb)
-        A = B = None
-        P = len(qa)
-    else:
-        ids = np.arange(rank * P, (rank + 1) * P, dtype=np.uint64)
-        A, B = gen_codes(ids, n, m, iupac)
-        packed = sedgpu.PackedPairs.from_arrays(A, B)
+    A, B, qa, qb = shard_inputs(args.workload, P, n, m, world, rank)
+    packed = sedgpu.PackedPairs.from_arrays(A, B) if A is not None else sedgpu.PackedPairs(qa, qb)
+    Pw = P  # pairs per GPU as configured (config 5: query rows)
+    P = packed.npairs
     log("rank %d: generated %d pairs in %.1fs" % (rank, P, time.perf_counter() - t0))
 
     ctx = sedgpu.Context(local)
@@ -355,7 +517,8 @@ def main():
     batch = sedgpu.Batch(ctx, packed, want_script, pipeline=pipeline, no_len=not want_script)
     log("rank %d: batch resident in %.1fs (mode %s, R=%d)" % (rank, time.perf_counter() - t0, batch.mode,
                                                              batch.rows_per_lane))
-    cells, algo_bytes = batch.work()
+    cells, design_bytes = batch.work()
+    algo_bytes = s8d_bytes(packed.len_a[:P], packed.len_b[:P], want_script)
 
     for _ in range(args.warmup):
         batch.run()
@@ -369,15 +532,20 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     dp_ms, tb_ms = batch.times()
+    cells_all = cells
     if dist is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+        tc = torch.tensor([cells], dtype=torch.float64, device=tdev)  # shards may differ (config 5's rows)
+        dist.all_reduce(tc, op=dist.ReduceOp.SUM)
+        cells_all = float(tc.item())
     ms_per_step = elapsed * 1e3 / args.steps
-    value = cells * world * args.steps / elapsed
+    value = cells_all * args.steps / elapsed
 
     # ---- results: gather to rank 0 over RCCL (timed separately) ----
     gather_ms = None
+    got = None
     if dist is not None:
         import sedshard
         words = int(packed.ops_off[P])
@@ -394,43 +562,47 @@ def main():
         if rank == 0:
             log("rank 0: gathered %d results + %d script words over %s (%.2f ms)"
                 % (got[0].numel(), got[2].numel(), args.dist_backend, gather_ms))
-            assert got[0].numel() == P * world
 
     # ---- verification (untimed) ----
-    d_gpu, ii_gpu, ln_gpu, ops = batch.results()
     check = {}
-    if want_script and A is not None:
-        good = 0
-        for s0 in range(0, P, 256):
-            sl = slice(s0, min(P, s0 + 256))
-            ok, cost = script_costs(plan, A[sl], B[sl], ln_gpu[sl], ops, packed.ops_off[sl])
-            same = (cost == d_gpu[sl]) if batch.mode == "i32" else np.isclose(cost, d_gpu[sl], rtol=1e-12)
-            good += int((ok & same).sum())
-        check["script_valid_rate"] = good / P
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = cpu_share()
-        cpu = cpu_baseline(plan, packed, args.cpu_seconds, threads, want_script)
-        c = cpu["count"]
-        exact = (cpu["dist"] == d_gpu[:c]) & ((cpu["len"] == ln_gpu[:c]) | (ln_gpu[:c] == -1))
-        if want_script:
-            for p in range(c):
-                if exact[p]:
-                    g = sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln_gpu[p]))
-                    o = cpu["ops"][cpu["ops_off"][p]: cpu["ops_off"][p] + cpu["len"][p]]
-                    exact[p] = np.array_equal(g, o)
-        check["script_exact_rate" if want_script else "dist_exact_rate"] = float(exact.mean())
-        check["exact_sample"] = int(c)
-        shape = "%dx%d" % (n, m) if n else "ragged"
-        cpu_obj = {"value": cpu["value"], "unit": "cells/s", "cores": threads, "kind": "port",
-                   "sample": "first %d of the %d pairs (%s, %s, %s), C oracle sed_oracle.c, %.1f s"
-                             % (c, P, shape, costs_file, "distance + script" if want_script else "distance",
-                                cpu["seconds"]),
-                   "cpu_model": cpu_model()}
-        if not args.no_python_baseline:
-            cpu_obj["python_node_graph"] = cpu_baseline_python(
-                table, alpha, A, B, qa if A is None else None, qb if A is None else None, want_script, threads,
-                args.cpu_seconds)
+    threads = cpu_share()
+    if dist is not None:
+        if rank == 0:
+            gd = got[0].cpu().numpy()
+            gl = got[1].cpu().numpy()
+            go = got[2].cpu().numpy().view(np.uint32)
+            tv = time.perf_counter()
+            check = verify_gathered(args, plan, Pw, n, m, world, gd, gl, go, want_script, batch.mode, threads,
+                                    args.cpu_seconds)
+            log("rank 0: verified %d gathered pairs in %.1fs" % (len(gd), time.perf_counter() - tv))
+    else:
+        d_gpu, ii_gpu, ln_gpu, ops = batch.results()
+        if want_script and A is not None:
+            check["script_valid_rate"] = valid_scripts(plan, A, B, d_gpu, ln_gpu, ops, packed.ops_off,
+                                                       batch.mode == "i32") / P
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(plan, packed, args.cpu_seconds, threads, want_script)
+            c = cpu["count"]
+            exact = (cpu["dist"] == d_gpu[:c]) & ((cpu["len"] == ln_gpu[:c]) | (ln_gpu[:c] == -1))
+            if want_script:
+                for p in range(c):
+                    if exact[p]:
+                        g = sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln_gpu[p]))
+                        o = cpu["ops"][cpu["ops_off"][p]: cpu["ops_off"][p] + cpu["len"][p]]
+                        exact[p] = np.array_equal(g, o)
+            check["script_exact_rate" if want_script else "dist_exact_rate"] = float(exact.mean())
+            check["exact_sample"] = int(c)
+            shape = "%dx%d" % (n, m) if n else "ragged"
+            cpu_obj = {"value": cpu["value"], "unit": "cells/s", "cores": threads, "kind": "port",
+                       "sample": "first %d of the %d pairs (%s, %s, %s), C oracle sed_oracle.c, %.1f s"
+                                 % (c, P, shape, costs_file, "distance + script" if want_script else "distance",
+                                    cpu["seconds"]),
+                       "cpu_model": cpu_model()}
+            if not args.no_python_baseline:
+                cpu_obj["python_node_graph"] = cpu_baseline_python(
+                    table, alpha, A, B, qa if A is None else None, qb if A is None else None, want_script, threads,
+                    args.cpu_seconds)
 
     if rank != 0:
         if dist is not None:
@@ -442,13 +614,18 @@ def main():
     lane_x2 = batch.mode == "i32" and not want_script and nl > 0 and not args.no_pack
     wave_x2 = npk - (nl if lane_x2 else 0)  # wave pairs computed two per wave
     ops_cell = None
+    R = batch.rows_per_lane
     if batch.mode == "i32":
         # checkpoint batches (SED_OPT_TB 2): the forward kernel runs dot keys (v_dot4 + v_max3, 2 ops/cell) or
         # distance keys (3 ops/cell); the traceback's recompute runs after it on the same SIMDs and is not in
-        # this model (kernel_ms is the DP)
-        ck_ops = "dot" if batch.dot_keys else "nolen"
-        ops_cell = CELL_OPS[(ck_ops if batch.traceback_mode == 2 else "script") if want_script
-                            else ("nolen_x2" if npk == P else "nolen")]
+        # this model (kernel_ms is the DP).  Per-cell codes on ladder dot keys (CHAIN, config 3): v_dot4, v_min3,
+        # v_and_or, v_alignbit on the d = -1 rows, plus 2 adds on the ladder's jump rows (2 of 8 at R = 8).
+        if want_script and batch.traceback_mode == 2:
+            ops_cell = CELL_OPS["dot" if batch.dot_keys else "nolen"]
+        elif want_script:
+            ops_cell = lad_ops(R) if batch.ladder_dot_keys else CELL_OPS["script"]
+        else:
+            ops_cell = CELL_OPS["nolen_x2" if npk == P else "nolen"]
     valu_peak = SIMDS * CLOCK * 64 / (VALU_CYCLES_PER_OP * ops_cell) if ops_cell else None
     rate = cells / (dp_avg * 1e-3)
     if batch.mode != "i32":
@@ -457,41 +634,60 @@ def main():
         wave_k = "sed_wf_i32_chain_kernel" if batch.chains else "sed_wf_i32_kernel"
         parts = ((["sed_wf_i32x2_kernel"] if wave_x2 else []) + ([wave_k] if nl + wave_x2 < P else []) +
                  ([("sed_lane_i32x2_kernel" if lane_x2 else "sed_lane_i32_kernel")] if nl else []))
+    tb_kernels = []
+    if want_script and nl < P:
+        tb_kernels = {2: ["sed_traceback_ck_kernel"], 3: ["sed_tb_stripemap_kernel", "sed_tb_stripeemit_kernel"],
+                      1: ["sed_traceback_kernel", "sed_traceback_window_kernel"]}.get(batch.traceback_mode, [])
     kname = "+".join(parts)
-    traffic, traffic_src = None, None
+    traffic, traffic_src, issue, issue_src = None, None, None, None
     if args.traffic == "measure" and world == 1:
         traffic, detail = measure_traffic(set(parts))
         traffic_src = {"measured": "rocprofv3 --pmc, this workload, one step per counter", **detail} \
             if traffic is not None else {"measure_failed": detail}
+        issue, why = measure_issue(set(parts) | set(tb_kernels))
+        issue_src = "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE, this workload, one step" \
+            if issue is not None else {"measure_failed": why}
     if traffic is None and args.traffic != "none" and args.pmc_json and os.path.exists(args.pmc_json):
         with open(args.pmc_json) as f:
             pm = json.load(f)
         if pm.get("workload") == desc and batch.mode == "i32" and want_script and P == WORKLOADS[args.workload][0]:
             traffic = pm.get("hbm_bytes_per_launch")
             traffic_src = dict(traffic_src or {}, file=os.path.relpath(args.pmc_json, REPO))
+    env = {k: v for k, v in sorted(os.environ.items()) if k.startswith("SED_")}
     line = {
         "metric": METRIC, "value": value, "unit": "cells/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u32" if batch.mode == "i32" else "f64", "data": "synthetic",
         "config": {"workload": desc, "pairs_per_gpu": P, "n": n, "m": m, "costs": costs_file,
                    "script": want_script, "pipeline": pipeline and batch.traceback_mode != 2, "mode": batch.mode,
-                   "rows_per_lane": batch.rows_per_lane, "lane_pairs": nl, "packed_pairs": npk,
-                   "chains": batch.chains, "dot_keys": batch.dot_keys,
+                   "rows_per_lane": R, "lane_pairs": nl, "packed_pairs": npk,
+                   "chains": batch.chains, "dot_keys": batch.dot_keys, "ladder_dot_keys": batch.ladder_dot_keys,
                    "traceback": {0: None, 1: "per-cell codes", 2: "checkpoints + recompute",
                                  3: "per-cell codes, stripe-parallel walk"}[batch.traceback_mode],
-                   "parallelism": "dp%d" % world},
+                   "parallelism": "dp%d" % world, "env": env},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": kname,
-                     "kernel_ms": dp_avg, "algo_bytes_per_launch": algo_bytes},
+                     "kernel": kname, "kernel_ms": dp_avg,
+                     "algo_bytes_per_launch": algo_bytes,
+                     "algo_bytes_def": "SURVEY.md 8(d): per pair (n+m)/4 in + 8 out" +
+                                       (" + 0.25 B/cell traceback + (n+m) reads + (n+m)/4 ops out" if want_script
+                                        else ""),
+                     "frac_step": algo_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "design_bytes_per_launch": design_bytes,
+                     "design_frac": design_bytes / (dp_avg * 1e-3) / 1e9 / HBM_PEAK_GBS},
         "valu": None if valu_peak is None else {
             "model": "%.4g VALU ops/cell x %.1f cycles/op per wave64 (tools/ubench/valu_row.hip), 1024 SIMDs, %.1f GHz"
                      % (ops_cell, VALU_CYCLES_PER_OP, CLOCK / 1e9),
             "achieved": rate, "peak": valu_peak, "unit": "cells/s", "frac": rate / valu_peak},
+        "issue": issue, "issue_source": issue_src,
         "traceback_ms": float(np.mean(tb_ms)) if want_script else None,
         "gather_ms": gather_ms,
         "cpu_baseline": cpu_obj if cpu is not None else None,
     }
+    if issue and line["valu"] is not None:
+        dom = [k for k in parts if k in issue]
+        if dom:
+            line["valu"]["issue_util"] = issue[dom[0]]["valu_issue"]
     line.update(check)
     print(json.dumps(line), flush=True)
     if dist is not None:

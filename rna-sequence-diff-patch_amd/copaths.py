@@ -100,9 +100,33 @@ class LengthWindows:
         return self.lo[c], self.hi[c]
 
 
+# Windows cost 8 * words bytes per cell and every widening recomputes them in O(cells * words).  A window must cover
+# [lmin(c), lmin(c) + delta] at every cell c for paths delta ops longer than the shortest (a prefix may be shortest
+# while its suffix is long), so it cannot slide; the widening stops at MAX_WORDS (the C limit) or at
+# SED_COPATHS_MAX_GB of windows (default 8), with a SedError that says so.
+MAX_WORDS = 1024
+
+
+def _wider(words, n, m, ell, lmin):
+    import os
+    budget = float(os.environ.get("SED_COPATHS_MAX_GB", "8")) * 1e9
+    new = words * 2
+    need = 8.0 * new * (n + 1) * (m + 1)
+    if new > MAX_WORDS or need > budget:
+        from sedgpu import SedError
+        raise SedError("create_paths: paths of %d ops are %d longer than the shortest (%d); enumerating them needs "
+                       "length windows of %d x 64 bits per cell (%.1f GB for %d x %d cells), past the limit of %d "
+                       "words / SED_COPATHS_MAX_GB=%.3g" % (ell, ell - lmin, lmin, new, need / 1e9, n + 1, m + 1,
+                                                           MAX_WORDS, budget / 1e9))
+    return new
+
+
 def iter_paths(M, L=None):
     """Yield every co-optimal path as uint8 op codes (0 insert, 1 delete, 2 update,
-    origin -> sink) in the reference's create_paths order."""
+    origin -> sink) in the reference's create_paths order.
+
+    Memory: the length windows take 8 * words bytes per cell (words = 1 covers paths up to 63 ops longer than the
+    shortest; each further doubling is recomputed on demand, see _wider)."""
     M = np.asarray(M)
     n, m = M.shape[0] - 1, M.shape[1] - 1
     mk = memoryview(np.ascontiguousarray(M & 7, dtype=np.uint8).tobytes())
@@ -114,7 +138,7 @@ def iter_paths(M, L=None):
     for ell in range(lo, hi + 1):
         lim = win.exact_up_to()
         while lim is not None and ell > lim:  # beyond the window: twice as wide
-            win = LengthWindows(M, win.words * 2)
+            win = LengthWindows(M, _wider(win.words, n, m, ell, lo))
             lim = win.exact_up_to()
         if not win.has(n, m, ell):
             continue

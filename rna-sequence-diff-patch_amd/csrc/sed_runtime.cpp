@@ -112,6 +112,7 @@ struct sed_batch {
     // per buffer: the event-log entry of the last run that used it (handles copied from `log`)
     std::array<hipEvent_t, 4> evk[3] = {};
     long runs = 0;
+    long chain_launches = 0;   // dynamic-CHAIN launches since the fill (the device counter's base)
     bool ran = false;
     // per-run event log (sed_batch_times): {dp start, dp end, tb start, tb end}
     std::vector<std::array<hipEvent_t, 4>> log;
@@ -398,6 +399,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     b->flags = flags;
     b->ran = false;
     b->runs = 0;
+    b->chain_launches = 0;
     b->nbuf = (flags & SED_PIPELINE) ? 3 : 1;
     b->n.assign(len_a, len_a + npairs);
     b->m.assign(len_b, len_b + npairs);
@@ -869,13 +871,15 @@ int run_batch(sed_batch *b) {
             L.nchains = b->nchains;
             L.chain_list = (int)b->chain_npairs;
             L.chain_counter = nullptr;
-            if (b->chain_dyn) {  // zeroed on a batch's first run only: a run takes list + waves values
+            if (b->chain_dyn) {  // zeroed on a batch's first launch only: a launch takes list + waves values
+                // (counted per launch, not per run: a run that fails after its CHAIN launch has still advanced it)
                 L.chain_counter = (uint32_t *)b->d_chain.p + b->chain_npairs + 1;
-                L.chain_base = (uint32_t)((uint64_t)b->runs * (uint64_t)(b->chain_npairs + b->nchains));
-                if (b->runs == 0 && (e = hipMemsetAsync(L.chain_counter, 0, 4, c->stream)) != hipSuccess)
+                L.chain_base = (uint32_t)((uint64_t)b->chain_launches * (uint64_t)(b->chain_npairs + b->nchains));
+                if (b->chain_launches == 0 && (e = hipMemsetAsync(L.chain_counter, 0, 4, c->stream)) != hipSuccess)
                     return c->hipfail(e, "reset chain counter");
             }
             e = sed_launch_i32_chain(L, ip, len);
+            if (e == hipSuccess && b->chain_dyn) ++b->chain_launches;
         } else if (b->mode == SED_MODE_I32)
             e = sed_launch_i32(L, ip, len);
         else
@@ -914,10 +918,7 @@ int run_batch(sed_batch *b) {
             }
         }
     }
-    // SED_DEBUG_NOTB=1 (debugging only): skip the traceback kernels, so a script batch reports the forward kernel's
-    // distances and lengths (its scripts are left as they were)
-    static const bool no_tb = [] { const char *e = getenv("SED_DEBUG_NOTB"); return e && atoi(e) > 0; }();
-    if (want_tb && !no_tb) {
+    if (want_tb) {
         if (ts != c->stream && (e = hipStreamWaitEvent(ts, lg[1], 0)) != hipSuccess) return c->hipfail(e, "stream wait");
         if (b->nwave == 0 && (e = hipEventRecord(lg[2], ts)) != hipSuccess) return c->hipfail(e, "event record");
         if (b->nwave > 0) {
@@ -1161,12 +1162,13 @@ int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave)
     int32_t f = 0, mx = 0;
     if (b->nchains > 0 && b->npairs > 0) {
         hipError_t e;
-        if (b->chain_dyn && b->runs > 0) {  // every persistent wave ends with one failed grab: a run takes list + waves
+        if (b->chain_dyn && b->chain_launches > 0) {  // every persistent wave ends with one failed grab: a run takes list + waves
             uint32_t cnt = 0;
             if ((e = hipMemcpy(&cnt, (uint32_t *)b->d_chain.p + b->chain_npairs + 1, 4, hipMemcpyDeviceToHost)) !=
                 hipSuccess)
                 return c->hipfail(e, "download chain counter");
-            const uint32_t base = (uint32_t)((uint64_t)(b->runs - 1) * (uint64_t)(b->chain_npairs + b->nchains));
+            const uint32_t base =
+                (uint32_t)((uint64_t)(b->chain_launches - 1) * (uint64_t)(b->chain_npairs + b->nchains));
             f = (int32_t)(cnt - base) - b->nchains;
         }
         std::vector<sed_result> h(b->npairs);

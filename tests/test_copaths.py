@@ -4,6 +4,7 @@ import itertools
 import math
 
 import numpy as np
+import pytest
 
 from conftest import load_golden
 import copaths
@@ -126,3 +127,16 @@ def test_window_bounds_and_large_counts():
     assert w.lengths_at_sink() == (40, 80) and w.exact_up_to() == 103
     total = copaths.count_paths(M)
     assert total == copaths._count_paths_py(M) and total.bit_length() > 64  # Delannoy D(40, 40)
+
+
+def test_window_widening_is_capped(monkeypatch):
+    """Widening the length windows past MAX_WORDS words or SED_COPATHS_MAX_GB raises a SedError that names the
+    limit instead of allocating without bound."""
+    import sedgpu
+    assert copaths._wider(1, 40, 40, 140, 40) == 2
+    monkeypatch.setenv("SED_COPATHS_MAX_GB", "0.00001")  # 10 kB
+    with pytest.raises(sedgpu.SedError, match="SED_COPATHS_MAX_GB"):
+        copaths._wider(1, 40, 40, 140, 40)
+    monkeypatch.delenv("SED_COPATHS_MAX_GB")
+    with pytest.raises(sedgpu.SedError, match="1024 words"):
+        copaths._wider(1024, 4, 4, 70000, 8)

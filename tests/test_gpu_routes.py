@@ -334,3 +334,62 @@ def test_split_handoff_repeated_runs(gpu, tables, R, pipeline):
     finally:
         gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
         gpu.set_option(sedgpu.SED_OPT_SPLIT, 0)
+
+
+def _factorable_tables(seed, want_ck, want_lad, maxmin, maxsum):
+    """Seeded random integer ACGU tables (insert / delete 1..3, substitutions 1..2, as a GUI edit could write them)
+    that sed_dot_factor accepts: want_ck for dot keys at min(n, m) <= maxmin, want_lad for ladder dot keys at
+    n + m <= maxsum."""
+    rng = np.random.default_rng(seed)
+    ck, lad = [], []
+    K = "ACGU"
+    while len(ck) < want_ck or len(lad) < want_lad:
+        ins, de = int(rng.integers(1, 4)), int(rng.integers(1, 4))
+        sub = rng.integers(1, min(2, ins + de) + 1, size=(4, 4)).astype(float)
+        np.fill_diagonal(sub, 0)
+        table = {"insert": float(ins), "delete": float(de),
+                 "update": {a: {b: float(sub[i, j]) for j, b in enumerate(K) if b != a} for i, a in enumerate(K)}}
+        if len(ck) < want_ck and sedgpu.dot_factor(sub, ins, de, maxmin, 0) is not None:
+            ck.append(table)
+        if len(lad) < want_lad and sedgpu.dot_factor(sub, ins, de, 0, maxsum) is not None:
+            lad.append(table)
+    return ck, lad
+
+
+def test_dot_keys_on_random_factorable_tables(gpu):
+    """Dot keys and ladder dot keys are picked automatically for any integer table that factors over signed bytes,
+    not only the two shipped ones (a GUI-edited user_costs.json can hold others).  Seeded random tables the
+    factorisation accepts: the checkpoint route (R = 16) must take dot keys, the dynamic-CHAIN route with per-cell
+    codes (R = 8) ladder dot keys; every pair vs the oracle and identical to SED_OPT_DOT = 2."""
+    ck_tables, lad_tables = _factorable_tables(3600, 3, 2, 1500, 1024)
+    A, B = _ragged(3601, 300, 1, 1500, 1, 1500)
+    a2, b2 = _ragged(3602, 2200, 1, 512, 1, 512)
+    cases = [(t, A, B, {sedgpu.SED_OPT_TB: 2, sedgpu.SED_OPT_CHAIN: 2, sedgpu.SED_OPT_ROWS_PER_LANE: 16}, "dot")
+             for t in ck_tables]
+    cases += [(t, a2, b2, {sedgpu.SED_OPT_TB: 1, sedgpu.SED_OPT_CHAIN: 1, sedgpu.SED_OPT_ROWS_PER_LANE: 8,
+                           sedgpu.SED_OPT_LANE: 2}, "lad") for t in lad_tables]
+    for table, AA, BB, opts, kind in cases:
+        plan = _plan(table)
+        gpu.set_costs(plan)
+        packed = sedgpu.PackedPairs(AA, BB)
+        for k, v in opts.items():
+            gpu.set_option(k, v)
+        try:
+            b, (d, ii, ln, ops) = _batch_run(gpu, packed, True)
+            try:
+                assert (b.dot_keys if kind == "dot" else b.ladder_dot_keys), (kind, table)
+                if kind == "lad":
+                    assert b.chains > 0
+            finally:
+                b.close()
+            _check_all(plan, packed, d, ii, ln, ops)
+            gpu.set_option(sedgpu.SED_OPT_DOT, 2)
+            b, (d2, ii2, ln2, ops2) = _batch_run(gpu, packed, True)
+            try:
+                assert not b.dot_keys and not b.ladder_dot_keys
+            finally:
+                b.close()
+            assert np.array_equal(d2, d) and np.array_equal(ln2, ln) and np.array_equal(ops2, ops)
+        finally:
+            for k in list(opts) + [sedgpu.SED_OPT_DOT]:
+                gpu.set_option(k, 0)
