@@ -197,7 +197,14 @@ def cpu_baseline_python(table, alphabet, A, B, qa, qb, want_script, cores, secon
         res = pool.map(_pyref_task, jobs, chunksize=max(1, len(jobs) // (4 * cores)))
         dt = time.perf_counter() - t0
     cells = float(sum(c for c, _ in res))
-    return {"value": cells / dt, "unit": "cells/s", "cores": cores, "kind": "port",
+    cal = None
+    cal_path = os.path.join(REPO, "profiles", "r03", "pyref_calibration.json")
+    if os.path.exists(cal_path):  # tools/calibrate_pyref.py: the reference itself, timed against pyref on one core
+        with open(cal_path) as f:
+            c = json.load(f)
+        cal = {"reference_over_pyref": c["ratio_mean"], "source": os.path.relpath(cal_path, REPO),
+               "reference_estimate": cells / dt * c["ratio_mean"]}
+    return {"value": cells / dt, "unit": "cells/s", "cores": cores, "kind": "port", "calibration": cal,
             "sample": "%s, pure-Python node graph (oracle/pyref.py: the reference's Node/Edge regime, %s), "
                       "%.1f s" % (what, "distance + canonical edit script" if want_script else "distance", dt)}
 
