@@ -40,7 +40,7 @@ for ti, table in enumerate(lad_tables):
     print("table", ti, table["insert"], table["delete"], plan.sub.tolist(), flush=True)
     for name, extra in (("lad", {}), ("nodot", {sedgpu.SED_OPT_DOT: 2}),
                         ("nochain", {sedgpu.SED_OPT_CHAIN: 2}), ("static3", {sedgpu.SED_OPT_CHAIN: 3})):
-        print(" ", name, run(plan, a2, b2, dict(base, **extra)), flush=True)
+        print(" ", name, run(plan, a2, b2, {**base, **extra}), flush=True)
     # bisect the lad failure to a small subset
     idx = list(range(len(a2)))
     while len(idx) > 1:
@@ -61,4 +61,4 @@ for ti, table in enumerate(lad_tables):
             print("   pair", i, "a", "".join("ACGU"[c] for c in a2[i]), "b", "".join("ACGU"[c] for c in b2[i]),
                   flush=True)
             print("   alone:", run(plan, [a2[i]], [b2[i]], base), flush=True)
-            print("   alone nodot:", run(plan, [a2[i]], [b2[i]], dict(base, **{sedgpu.SED_OPT_DOT: 2})), flush=True)
+            print("   alone nodot:", run(plan, [a2[i]], [b2[i]], {**base, sedgpu.SED_OPT_DOT: 2}), flush=True)
