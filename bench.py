@@ -63,6 +63,9 @@ WORKLOADS = {
            "config 2: 1 pair 4096x4096 synthetic ACGU, user_costs.json, distance + edit script"),
     "iupac": (8192, 1024, 1024, "costs.json",
               "fp64 path: 8192 pairs of 1024x1024 synthetic 15-symbol IUPAC, costs.json, distance + edit script"),
+    "timing": (51200, 0, 0, "costs.json",
+               "timing.py methodology, batched: pair p is two random 15-symbol IUPAC sequences of length 10 + 10 (p mod "
+               "50) (timing.py:12-15,45-57: lengths 10..500 step 10), costs.json (fp64 path), distance + edit script"),
     "c5": (500, 0, 0, "costs.json",
            "config 5 (synthetic): all-vs-all wf_score over 500 ACGU sequences of length U[24,32], costs.json, "
            "250000 ordered pairs, distance only"),
@@ -348,9 +351,29 @@ def refuse_reason(gpus, environ):
     return None
 
 
+def gen_timing(pair_ids):
+    """timing.py's sweep (timing.py:45-57: random 15-symbol pairs of equal length 10, 20, .., 500), batched: pair id p
+    has length 10 + 10 (p mod 50) on both sides."""
+    ids = np.asarray(pair_ids, dtype=np.uint64)
+    ln = 10 + 10 * (ids % np.uint64(50)).astype(np.int64)
+    qa = [None] * len(ids)
+    qb = [None] * len(ids)
+    for L in np.unique(ln):
+        sel = np.flatnonzero(ln == L)
+        a = synth.iupac_codes(ids[sel], int(L), 0)
+        b = synth.iupac_codes(ids[sel], int(L), 1)
+        for k, x in enumerate(sel):
+            qa[x] = a[k]
+            qb[x] = b[k]
+    return qa, qb
+
+
 def shard_inputs(workload, P, n, m, world, r):
     """Rank r's inputs, regenerated from the seeds: (A, B, None, None) for fixed-shape workloads (pair ids
-    [r*P, (r+1)*P)), (None, None, qa, qb) for the all-vs-all rows of config 5."""
+    [r*P, (r+1)*P)), (None, None, qa, qb) for the all-vs-all rows of config 5 and the ragged timing sweep."""
+    if workload == "timing":
+        qa, qb = gen_timing(np.arange(r * P, (r + 1) * P, dtype=np.uint64))
+        return None, None, qa, qb
     if workload in ("c5", "c5n"):
         import sedshard
         lo, hi = sedshard.shard_range(P, world, r)  # query rows of this rank
@@ -370,6 +393,21 @@ def valid_scripts(plan, A, B, dist, ln, ops, ops_off, exact_int):
         ok, cost = script_costs(plan, A[sl], B[sl], ln[sl], ops, ops_off[sl])
         same = (cost == dist[sl]) if exact_int else np.isclose(cost, dist[sl], rtol=1e-12)
         good += int((ok & same).sum())
+    return good
+
+
+def valid_scripts_ragged(plan, qa, qb, dist, ln, ops, ops_off, exact_int):
+    """valid_scripts over ragged pairs, grouped by shape."""
+    la = np.array([len(x) for x in qa])
+    lb = np.array([len(x) for x in qb])
+    good = 0
+    for (n, m) in set(zip(la.tolist(), lb.tolist())):
+        sel = np.flatnonzero((la == n) & (lb == m))
+        if n == 0 or m == 0:
+            continue
+        A = np.stack([qa[x] for x in sel])
+        B = np.stack([qb[x] for x in sel])
+        good += valid_scripts(plan, A, B, dist[sel], ln[sel], ops, ops_off[sel], exact_int)
     return good
 
 
@@ -394,7 +432,7 @@ def verify_gathered(args, plan, P, n, m, world, gdist, glen, gops, want_script, 
     within `seconds` of CPU time in total.  Returns the bench line's check fields."""
     exact_int = mode == "i32"
     valid = total = agree = sampled = 0
-    base = 0
+    base = wbase = 0
     per_rank = []
     for r in range(world):
         A, B, qa, qb = shard_inputs(args.workload, P, n, m, world, r)
@@ -402,12 +440,14 @@ def verify_gathered(args, plan, P, n, m, world, gdist, glen, gops, want_script, 
         Pr = packed.npairs
         d = gdist[base:base + Pr]
         ln = glen[base:base + Pr]
+        words = int(packed.ops_off[Pr])  # this rank's script words (its segment of the gathered buffer)
         if want_script:
-            w0 = (n + m + 15) // 16  # script words per pair (fixed shapes)
-            ops = gops[base * w0:(base + Pr) * w0]
-            valid += valid_scripts(plan, A, B, d, ln, ops, packed.ops_off, exact_int)
+            ops = gops[wbase:wbase + words]
+            valid += (valid_scripts(plan, A, B, d, ln, ops, packed.ops_off, exact_int) if A is not None else
+                      valid_scripts_ragged(plan, qa, qb, d, ln, ops, packed.ops_off, exact_int))
         else:
             ops = None
+        wbase += words
         total += Pr
         # oracle sample: the rank's leading pairs, about seconds / world of single-thread-equivalent work
         la, lb = packed.len_a[:Pr].astype(np.float64), packed.len_b[:Pr].astype(np.float64)
@@ -436,6 +476,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     ap.add_argument("--pairs", type=int, default=0, help="override pairs per GPU")
+    ap.add_argument("--shape", default="", help="override the pair shape NxM (experiments; fixed-shape workloads)")
     ap.add_argument("--no-script", action="store_true", help="distance only (no traceback)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run DP and traceback back to back on one stream (no overlap across steps)")
@@ -492,8 +533,11 @@ def main():
     P, n, m, costs_file, desc = WORKLOADS[args.workload]
     if args.pairs:
         P = args.pairs
+    if args.shape:
+        n, m = (int(x) for x in args.shape.lower().split("x"))
+        desc += " [shape overridden: %dx%d]" % (n, m)
     want_script = not args.no_script and args.workload not in ("c5", "c5n")
-    iupac = args.workload == "iupac"
+    iupac = args.workload in ("iupac", "timing")
     with open(os.path.join(REPO, "tests", "golden", costs_file)) as f:
         table = json.load(f)
     alpha = synth.IUPAC if iupac else (synth.ALPHABET + "N" if args.workload == "c5n" else synth.ALPHABET)
@@ -588,6 +632,9 @@ def main():
         if want_script and A is not None:
             check["script_valid_rate"] = valid_scripts(plan, A, B, d_gpu, ln_gpu, ops, packed.ops_off,
                                                        batch.mode == "i32") / P
+        elif want_script:
+            check["script_valid_rate"] = valid_scripts_ragged(plan, qa, qb, d_gpu, ln_gpu, ops, packed.ops_off,
+                                                              batch.mode == "i32") / P
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(plan, packed, args.cpu_seconds, threads, want_script)
             c = cpu["count"]

@@ -141,10 +141,19 @@ __host__ __device__ inline uint64_t sed_ck_col_word(int R, int stripe, int nchun
 __host__ __device__ inline uint64_t sed_ck_col_words(int R, int nstripes, int nchunks) {
     return (uint64_t)nstripes * (uint64_t)nchunks * (uint64_t)(R + 1) * 64u;
 }
-// row checkpoint of forward lane t (t = G-1 mod G) at step s of stripe k (G = 64/R)
+// Row checkpoints: every step, the bottom row of the forward lanes t = GH-1 (mod GH), GH = SED_CK_TILE / R, i.e.
+// of every SED_CK_TILE-th matrix row (the traceback's tile height, 64).  Per stripe and G-step group (G = 64/R):
+// SED_CK_RW = 64 * 64 / SED_CK_TILE words, [group][t / GH][step % G].  SED_CK_TILE = 32 (twice the row checkpoints)
+// served a two-pairs-per-wave traceback of 32-row tiles, measured and dropped in round 3: the forward kernel took
+// 9.87 instead of 9.18-9.32 ms and that traceback 2.43 instead of 2.20 ms (profiles/r03/ab_tb_tiles.jsonl).
+#ifndef SED_CK_TILE
+#define SED_CK_TILE 64
+#endif
+#define SED_CK_RW (64 * 64 / SED_CK_TILE)
+// row checkpoint of forward lane t (t = GH-1 mod GH) at step s of stripe k
 __host__ __device__ inline uint64_t sed_ck_row_word(int R, int k, int ngroups, int s, int t) {
-    const int G = 64 / R;
-    return ((uint64_t)k * (uint64_t)ngroups + (uint64_t)(s / G)) * 64u + (uint64_t)(t / G) * (uint64_t)G +
+    const int G = 64 / R, GH = SED_CK_TILE / R;
+    return ((uint64_t)k * (uint64_t)ngroups + (uint64_t)(s / G)) * (uint64_t)SED_CK_RW + (uint64_t)(t / GH) * (uint64_t)G +
            (uint64_t)(s % G);
 }
 // CK batches (L.ck): the traceback that recomputes tiles from the forward kernel's checkpoints

@@ -568,7 +568,7 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         // CK: column checkpoints of stripe k at ccb[(chunk * (R+1) + v) * 64 + lane], row checkpoints at
         // rcb[group * 64 + (lane / G) * G + step % G] (sed_ck_*_word, the layout sed_traceback_ck_kernel reads)
         uint32_t *ccb = tb + d.tb_off + sed_ck_col_word(R, k, nchunks, 0, 0, 0);
-        uint32_t *rcb = tb + d.tb_off + sed_ck_col_words(R, nstripes, nchunks) + (uint64_t)k * (uint64_t)(SG / G) * 64u;
+        uint32_t *rcb = tb + d.tb_off + sed_ck_col_words(R, nstripes, nchunks) + (uint64_t)k * (uint64_t)(SG / G) * SED_CK_RW;
         uint32_t rcv[G];
         const bool last = (k == nstripes - 1);
         const int cap_step = last ? m - 1 + cap_lane : -1;
@@ -593,7 +593,9 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                     store_tb(gp + lane * 4, W);
                 }
                 if constexpr (CK) {
-                    if ((lane & (G - 1)) == G - 1) store_words<G>(rcb + (uint64_t)(s0 / G) * 64u + (uint32_t)(lane / G) * G, rcv);
+                    constexpr int GH = SED_CK_TILE / R;  // forward lanes per traceback tile
+                    if ((lane & (GH - 1)) == GH - 1)
+                        store_words<G>(rcb + (uint64_t)(s0 / G) * SED_CK_RW + (uint32_t)(lane / GH) * G, rcv);
                     if (lane == 63 && !last) store_words<G>(bnd + d.bnd_off + (uint32_t)s0, rcv);  // next stripe's top row
                 }
             };
@@ -1042,14 +1044,15 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
                 }
             }
             if constexpr (CK) {  // row checkpoints of lanes t = G-1 (mod G), to the pair(s) the group's steps belong to
-                if ((lane & (G - 1)) == G - 1) {
-                    const uint32_t lo = (uint32_t)(lane / G) * G;
+                constexpr int GH = SED_CK_TILE / R;
+                if ((lane & (GH - 1)) == GH - 1) {
+                    const uint32_t lo = (uint32_t)(lane / GH) * G;
                     if (have_cur && s >= cur.T)
                         store_words<G>(tb + cur.tb_off + sed_ck_col_words(R, 1, cur.nchunks) +
-                                           (uint64_t)((s - cur.T) / G) * 64u + lo, rcv);
+                                           (uint64_t)((s - cur.T) / G) * SED_CK_RW + lo, rcv);
                     if (have_prv && s < (have_cur ? cur.T + 64 : prv.end) && (s - prv.T) / G < prv.sg)
                         store_words<G>(tb + prv.tb_off + sed_ck_col_words(R, 1, prv.nchunks) +
-                                           (uint64_t)((s - prv.T) / G) * 64u + lo, rcv);
+                                           (uint64_t)((s - prv.T) / G) * SED_CK_RW + lo, rcv);
                 }
             }
             if (capg) {
@@ -1949,34 +1952,52 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
             const int re = i - rowbase - 1;             // the entry cell's tile row
             const int sig_end = (j - J0 + G - 1) + re;  // the entry cell's sweep step (<= 126)
             // ---- boundaries (distance keys -> traceback keys) ----
+            // Every load of the tile is issued before the first use (one memory round trip per tile visit): addresses
+            // are clamped to valid words and the border cases are selects afterwards.
             const int ir = min(rowbase + lane, n - 1);  // 0-based str1 index of this lane's row (clamped)
-            const uint32_t a = (pa[ir >> 4] >> ((ir & 15) * 2)) & 3u;
-            const uint32_t cv = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
+            const uint32_t wa = pa[ir >> 4];
+            uint32_t ck0 = 0, ck1 = 0;
+            if (c >= 1) {  // (uniform)
+                const uint32_t *cp = ccp + sed_ck_col_word(R, k, nchunks, c - 1, lane & (R - 1), G * Q + band);
+                ck0 = cp[0];
+                ck1 = cp[(R - (lane & (R - 1))) * 64];
+            }
+            // the row above the tile at column J0 - G + x (x = lane, lane + 64, lane + 128 < 132): row checkpoints of
+            // forward lane G*Q - 1 (or lane 63 of the stripe above); steps clamped: past SG the columns are beyond m and
+            // never read by the walk; columns < 1 are the column-0 border (a CHAIN wave's lanes still hold the
+            // previous pair there)
+            const bool above = Q >= 1 || k >= 1;  // (uniform) else row 0: the border
+            const int kr = Q >= 1 ? k : k - 1, tr = Q >= 1 ? G * Q - 1 : 63, s0r = Q >= 1 ? 64 * c - G - 1 : 64 * c + 63 - G;
+            uint32_t rk[3] = {0, 0, 0}, wb[3];
+#pragma unroll
+            for (int h = 0; h < 3; ++h) {
+                const int x = lane + 64 * h;
+                if (h < 2 || x < 132) {
+                    if (above) rk[h] = rcp[sed_ck_row_word(R, kr, ngroups, min(max(s0r + x, 0), SG - 1), tr)];
+                    const int ci = min(max(J0 - (G - 1) + x - 1, 0), m - 1);
+                    wb[h] = pb[ci >> 4];
+                }
+            }
+            const uint32_t a = (wa >> ((ir & 15) * 2)) & 3u;
+            const uint32_t clo = (a & 1u) ? prm.costrow[1] : prm.costrow[0];
+            const uint32_t chi = (a & 1u) ? prm.costrow[3] : prm.costrow[2];
+            const uint32_t cv = (a & 2u) ? chi : clo;
             uint32_t V = SED_KB, tp = SED_KB;  // c = 0: the column-0 borders
             if (c >= 1) {
-                const uint32_t *cp = ccp + sed_ck_col_word(R, k, nchunks, c - 1, lane & (R - 1), G * Q + band);
-                V = ck_to_tb(cp[0], prm);
-                tp = ck_to_tb(cp[(R - (lane & (R - 1))) * 64], prm);
+                V = ck_to_tb(ck0, prm);
+                tp = ck_to_tb(ck1, prm);
             }
             tp += 1u;  // diagonals carry the +1 of the delete candidate they were taken from
-            {
-            }
-            for (int x = lane; x < 132; x += 64) {
-                // the row above the tile at column J0 - G + x: row checkpoints of forward lane G*Q - 1 (or lane 63
-                // of the stripe above); steps clamped: past SG the columns are beyond m and never read by the
-                // walk; before step 0 the border
-                // (columns < 1 are the column-0 border: a CHAIN wave's lanes still hold the previous pair there)
-                uint32_t v = SED_KB;
-                if (J0 - G + x >= 1) {
-                    if (Q >= 1)
-                        v = ck_to_tb(rcp[sed_ck_row_word(R, k, ngroups, min(64 * c - G - 1 + x, SG - 1), G * Q - 1)], prm);
-                    else if (k >= 1)
-                        v = ck_to_tb(rcp[sed_ck_row_word(R, k - 1, ngroups, min(64 * c + 63 - G + x, SG - 1), 63)], prm);
+#pragma unroll
+            for (int h = 0; h < 3; ++h) {
+                const int x = lane + 64 * h;
+                if (h < 2 || x < 132) {
+                    const uint32_t v = (above && J0 - G + x >= 1) ? ck_to_tb(rk[h], prm) : SED_KB;
+                    topb[x] = v + 1u;
+                    const int col = J0 - (G - 1) + x;  // column of lane 0 at step x
+                    const int ci = min(max(col - 1, 0), m - 1);
+                    selb[64 + x] = col < 1 ? SED_SEL_SENT : i32_sel((wb[h] >> ((ci & 15) * 2)) & 3u);
                 }
-                topb[x] = v + 1u;
-                const int col = J0 - (G - 1) + x;  // column of lane 0 at step x
-                const int ci = min(max(col - 1, 0), m - 1);
-                selb[64 + x] = col < 1 ? SED_SEL_SENT : i32_sel((pb[ci >> 4] >> ((ci & 15) * 2)) & 3u);
             }
             ck_sync<WAVE>();
             // ---- sweep: lane r at step sigma computes (row rowbase + r + 1, column J0 - (G-1) + sigma - r) ----
@@ -1992,10 +2013,10 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
             uint32_t ent = 0;
             const uint32_t *selp = selb + 64 - lane;  // lane r's selector at step sigma: selp[sigma]
             const int w_end = sig_end >> 4;
-            auto step = [&](const int sig, uint32_t &wv) {
+            auto step = [&](const int sig, uint32_t &wv, const uint32_t topin, const uint32_t selv) {
                 if (sig < G - 1) return;  // every lane holds
-                const uint32_t topv = dpp_shr1_add(topb[sig + 1], V, one);
-                const uint32_t selv = selp[sig];  // steps before the lane's first column read don't-care
+                const uint32_t topv = dpp_shr1_add(topin, V, one);
+                // (selv: steps before the lane's first column read don't-care)
                 uint32_t diag = tprev;
                 const int bs = ck_band_start<R>(sig);  // folds to a constant in the unrolled sweep
                 if (bs > 0) diag = lane == R * bs ? tp : diag;
@@ -2010,15 +2031,22 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
             for (int w = 0; w < 8; ++w) {
                 if (w > w_end) break;  // the path never needs later steps
                 if (w == w_end) {  // up to the entry step exactly: the lanes then hold the entry keys
+                    // the word's LDS inputs first, so the per-step exits do not serialise an LDS round trip per step
+                    uint32_t tw[16], sw[16];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) {
+                        tw[u] = topb[16 * w + u + 1];
+                        sw[u] = selp[16 * w + u];
+                    }
 #pragma unroll
                     for (int u = 0; u < 16; ++u) {
                         if (16 * w + u > sig_end) break;
-                        step(16 * w + u, W[w]);
+                        step(16 * w + u, W[w], tw[u], sw[u]);
                     }
                     W[w] >>= 2u * (15u - ((uint32_t)sig_end & 15u));  // step u's code to bits 2u, 2u+1
                 } else {
 #pragma unroll
-                    for (int u = 0; u < 16; ++u) step(16 * w + u, W[w]);
+                    for (int u = 0; u < 16; ++u) step(16 * w + u, W[w], topb[16 * w + u + 1], selp[16 * w + u]);
                 }
                 if (w < 4) W[w] |= hm[w];
             }

@@ -247,7 +247,10 @@ DotKeys dot_keys(const int64_t kap[4][4], int64_t maxmin, int64_t lad_amin = 0, 
     for (int64_t a = a_hi; a >= 1; --a) {
         const int64_t A = den * a;
         if (lad ? A < lad_amin : A * kmin <= maxmin * (kmax - kmin)) break;  // fails for every smaller a too
-        if (lad && A >= 65536) continue;
+        // ladder keys keep the rung c(i) and the op in the low 3 bits of W = A*(D - i*delete - j*insert) + 8*(L - i - j)
+        // + B + c(i): A must be a multiple of 8, or the D part leaks into them (a random GUI table found this:
+        // insert 2 / delete 1 factored with A = 8835, and its scripts came out wrong)
+        if (lad && (A >= 65536 || (A & 7))) continue;
         const int64_t J = num * a + beta;
         int64_t x = 0, y = 0;
         for (int64_t t = 1; t <= 127 && !x; ++t)
@@ -523,7 +526,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
             const uint64_t SG = (mm + 63 + G - 1) / G * G;
             const uint64_t nchunks = (SG + 63) / 64;
             if (want_tb) {  // CK: per stripe nchunks x (R+1) x 64 column checkpoints + (SG/G) x 64 row checkpoints
-                const uint64_t w = b->ck ? nstripes * (nchunks * (R + 1) * 64 + (SG / G) * 64) : nstripes * (SG / G) * 64 * 4;
+                const uint64_t w = b->ck ? nstripes * (nchunks * (R + 1) * 64 + (SG / G) * SED_CK_RW) : nstripes * (SG / G) * 64 * 4;
                 tbw += w;
                 ck_bytes += 4.0 * (double)w;
             }

@@ -52,3 +52,24 @@ def test_dot_keys_bound_and_ladder_eligibility():
     fractional = sub.copy()
     fractional[0, 1] = 0.5
     assert sedgpu.dot_factor(fractional, ins, dele, maxmin=100) is None
+
+
+def test_ladder_unit_is_a_multiple_of_8_on_random_tables():
+    """Ladder dot keys keep the rung and the op in the low 3 bits of A*(D - i*delete - j*insert) + 8*(L - i - j) + B
+    + c(i): every ladder factorisation must have A % 8 == 0 (a random insert 2 / delete 1 table once factored with
+    A = 8835 and produced wrong scripts on the GPU), A within 16 bits and above 8 (n + m) + 7, and exact bytes."""
+    rng = np.random.default_rng(91)
+    seen = 0
+    for _ in range(3000):
+        ins, de = int(rng.integers(1, 4)), int(rng.integers(1, 4))
+        sub = rng.integers(1, min(2, ins + de) + 1, size=(4, 4)).astype(float)
+        np.fill_diagonal(sub, 0)
+        got = sedgpu.dot_factor(sub, ins, de, 0, 1024)
+        if got is None:
+            continue
+        seen += 1
+        A, rows, cols, _ = got
+        assert A % 8 == 0 and 8 * 1024 + 7 < A < 65536
+        kap = ins + de - sub
+        assert np.array_equal(rows @ cols.T, -(A * kap + 7))
+    assert seen >= 3
