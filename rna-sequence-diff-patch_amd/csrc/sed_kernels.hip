@@ -408,6 +408,9 @@ __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)
 // the hot loop does not spill (R=16: 96 VGPRs / 5 waves; the 80-VGPR budget of 6 waves spills the
 // cost rows and ran 2.5x slower; R=4/8: 72 / 7; R=32: 128 / 4, which still spills: never chosen).
 template <int R> struct I32Waves { static constexpr int value = R >= 32 ? 4 : (R == 16 ? 5 : 7); };
+#ifndef SED_SPLIT_BWORDS
+#define SED_SPLIT_BWORDS 1024  // SPLIT: str2 words staged in LDS (m <= 16384)
+#endif
 #ifndef SED_CK_WAVES
 #define SED_CK_WAVES 5
 #endif
@@ -495,6 +498,15 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
     __shared__ uint32_t lds_sel[SPLIT ? 1 : 4][256];
     uint32_t *lch = lds_top[SPLIT ? 0 : (threadIdx.x >> 6)];
     uint32_t *ring = lds_sel[SPLIT ? 0 : (threadIdx.x >> 6)];
+    // SPLIT: str2's packed words in LDS (m <= 16 * SED_SPLIT_BWORDS), so the chunk loop issues no global load of its
+    // own: a wait for one with the group's stores in flight is a vmcnt(0), i.e. a store round trip per chunk
+    constexpr int BW = SPLIT ? SED_SPLIT_BWORDS : 1;
+    __shared__ uint32_t lds_b[BW];
+    const int bwords = (m + 15) >> 4;
+    const bool bl = SPLIT && bwords <= BW;  // (uniform)
+    if (bl) {
+        for (int x = lane; x < bwords; x += 64) lds_b[x] = pb[x];
+    }
 
     for (int k = kfirst; k <= klast; ++k) {
         // in-place single buffer per pair when one wave does all stripes; one buffer per stripe otherwise
@@ -550,7 +562,8 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         };
         auto load_sel = [&](int c) -> uint32_t {
             const int ci = 64 * c + lane;
-            const uint32_t b = (pb[ci >> 4] >> ((ci & 15) * 2)) & 3u;
+            const uint32_t wb = bl ? lds_b[min(ci >> 4, bwords - 1)] : pb[ci >> 4];  // (past m: never read)
+            const uint32_t b = (wb >> ((ci & 15) * 2)) & 3u;
             if constexpr (DOT) return b == 0 ? prm.dotcol[0] : b == 1 ? prm.dotcol[1] : b == 2 ? prm.dotcol[2] : prm.dotcol[3];
             return i32_sel(b);
         };
@@ -619,13 +632,19 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                     else
                         i32_group<R, TB, LEN, false, CK, DOT>(V, cv, top_prev, bottom, selv, lch, lsel, outc, W, s, lane,
                                                          cap_step, cap_lane, cap_row, cap, rcv);
+                    // SPLIT: the next group's words are waited for before this group's stores issue.  A load wait
+                    // with stores in flight is an s_waitcnt vmcnt(0) (the compiler counts mixed reads and writes as
+                    // out of order), so waiting after the stores made every consumer group wait for its own stores
+                    // to complete: 84 instead of 51 ns per step below stripe 0 (profiles/r03/c2_shapes.jsonl).
+                    if constexpr (SPLIT) {
+                        if (fetch) fetch_finish(s + G);
+                    }
                     stores(s);
                     if constexpr (SPLIT) {
                         // lanes 64-G+u hold lane 63's bottom cell of step s+u, column s+u-62 (word col + 64)
                         if (!last && lane >= 64 - G)
                             store_tagged(bout64 + (uint32_t)(s + lane - (64 - G) - 62 + 64),
                                          prm.epoch | (ok ? 0u : SED_PROG_POISON), outc);
-                        if (fetch) fetch_finish(s + G);
                     }
                 }
             }
