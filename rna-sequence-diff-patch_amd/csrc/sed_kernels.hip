@@ -127,6 +127,16 @@ __device__ __forceinline__ uint64_t load_sc1_u64(const uint64_t *p) {
 // = 16 bytes per lane, one dwordx4 store; the wave writes 1 KiB contiguous.
 template <int R> struct Grp { static constexpr int G = 64 / R; };
 
+// t[b] for a per-lane 2-bit symbol b as two levels of selects on SGPR copies: indexing the kernel-argument array
+// (or a ?: chain over it, which the compiler turns back into an index) makes a private copy in scratch and a
+// scratch load per use, each one an s_waitcnt vmcnt(0) behind the wave's stores in flight
+__device__ __forceinline__ uint32_t sel4(const uint32_t b, const uint32_t (&t)[4]) {
+    const uint32_t c0 = __builtin_amdgcn_readfirstlane(t[0]), c1 = __builtin_amdgcn_readfirstlane(t[1]);
+    const uint32_t c2 = __builtin_amdgcn_readfirstlane(t[2]), c3 = __builtin_amdgcn_readfirstlane(t[3]);
+    const uint32_t lo = (b & 1u) ? c1 : c0, hi = (b & 1u) ? c3 : c2;
+    return (b & 2u) ? hi : lo;
+}
+
 __device__ __forceinline__ void store_tb(uint32_t *p, const uint32_t (&w)[4]) {
     *reinterpret_cast<uint4 *>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
@@ -422,8 +432,8 @@ template <int R> struct I32Waves { static constexpr int value = R >= 32 ? 4 : (R
 // Inter-workgroup hand-off of stripe bottom rows (SPLIT mode), per 16-step group and self-validating: every
 // bottom-row cell travels as one 64-bit word {tag, value}, stored with a relaxed agent-scope 64-bit atomic
 // (single-copy atomic, so a reader sees the tag and the value of one store together), tag = the run's epoch
-// (1..32767, prm.epoch) | poison << 31.  The consumer loads its next group's words one group ahead (sc1, past
-// its L1) and re-polls any whose tag is not this run's.  No counter, fence or s_waitcnt on the producer side:
+// (1..32767, prm.epoch) | poison << 31.  The consumer's feeder wave (split_feed) polls the words and re-polls any
+// whose tag is not this run's.  No counter, fence or s_waitcnt on the producer side:
 // with the per-chunk counter hand-off (stores, s_waitcnt, release fence, counter; the consumer prefetching a
 // chunk ahead) each stripe ran 3 chunks (192 steps) behind the one above.
 // The previous run's words carry another epoch; the host zeroes the buffer on a batch's first run and when the
@@ -434,10 +444,60 @@ __device__ __forceinline__ void store_tagged(uint64_t *p, uint32_t tag, uint32_t
     __hip_atomic_store(p, ((uint64_t)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// SPLIT: the ring of lane 0's top values (one per step) and the hand-off feeder.  Each stripe below the first runs
+// as two waves: the compute wave, which never waits on a global load (any such wait with its own stores in flight is
+// an s_waitcnt vmcnt(0): the compiler counts mixed reads and writes as out of order, and the store round trip then
+// sat in every group), and this feeder.  The feeder polls the stripe above's tagged words 64 columns at a time (sc1,
+// past its L1), moves the longest valid prefix into the LDS ring and publishes how many steps are ready (flag[0]);
+// the compute wave publishes how many it has consumed (flag[1]), which bounds how far the feeder may run ahead.
+// A poisoned word upstream, or no progress for ~2^22 polls, poisons flag[0] (bit 31) with every step ready, so the
+// compute wave never waits again and the last stripe reports err.
+#define SED_SPLIT_RING 256
+// the flags are relaxed workgroup-scope atomics: a volatile LDS access is followed by s_waitcnt vmcnt(0) lgkmcnt(0)
+__device__ __forceinline__ uint32_t lds_flag_get(uint32_t *f) {
+    return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_flag_set(uint32_t *f, uint32_t v) {
+    __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <int G>
+__device__ __forceinline__ void split_feed(const uint64_t *__restrict__ bin64, const int m, const int SG,
+                                           const uint32_t epoch, uint32_t *ring, uint32_t *flag,
+                                           const int lane) {
+    uint32_t poison = 0, idle = 0;
+    int have = 0;  // steps whose top values are in the ring
+    while (have < SG) {
+        if (have + 64 > (int)lds_flag_get(flag + 1) + SED_SPLIT_RING) {  // ring full: the compute wave is behind
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        const int t = have + lane, col = t + 1;
+        const bool need = t < SG && col <= m;  // columns past m are never stored nor waited for
+        const uint64_t w = need ? load_sc1_u64(bin64 + (uint32_t)(col + 64)) : 0ull;
+        const bool good = !need || (((uint32_t)(w >> 32) & ~SED_PROG_POISON) == epoch);
+        const uint64_t bad = __ballot(!good);
+        const int nv = min(bad ? (int)__builtin_ctzll(bad) : 64, SG - have);  // the valid prefix
+        if (__any(lane < nv && need && (w >> 63))) poison = SED_PROG_POISON;  // poisoned upstream
+        if (nv > 0) {
+            if (lane < nv) ring[t & (SED_SPLIT_RING - 1)] = (uint32_t)w;
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the values before the count
+            have += nv;
+            idle = 0;
+        } else if (++idle > (1u << 22)) {  // the stripe above stopped: give up, let the compute wave drain
+            poison = SED_PROG_POISON;
+            have = SG;
+        } else {
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (lane == 0 && (nv > 0 || poison)) lds_flag_set(flag, (uint32_t)have | poison);
+    }
+}
+
 // SPLIT = false: one wave per pair walks all of its stripes (batches).
-// SPLIT = true : one wave (one 64-thread workgroup) per stripe, all stripes of
-//                a pair run concurrently, each a few groups behind the stripe
-//                above it (single long pairs: config 2, the GUI; hand-off above).
+// SPLIT = true : one 128-thread workgroup per stripe (the compute wave and its
+//                feeder, split_feed), all stripes of a pair run concurrently,
+//                each a few groups behind the stripe above it (single long
+//                pairs: config 2, the GUI; hand-off above).
 // CK (not SPLIT): instead of per-cell codes, tb receives checkpoints for the recompute traceback
 // (sed_traceback_ck_kernel; layout in sed_internal.h): per stripe, at every chunk end each lane's R row values
 // and its top_prev ("column checkpoints", [chunk][R+1][64 lanes]), and every step the bottom row of the lanes
@@ -447,7 +507,7 @@ __device__ __forceinline__ void store_tagged(uint64_t *p, uint32_t tag, uint32_t
 // The CK kernel (distance keys, no codes) would fit 80 VGPRs (6 waves per SIMD, spills per chunk only) but
 // ran slower: 12.45 against 12.11 ms at 5 waves (profiles/r02/ab_ck_waves.txt).
 template <int R, bool TB, bool SPLIT, bool LEN = true, bool CK = false, bool DOT = false>
-__global__ __launch_bounds__(SPLIT ? 64 : 256) __attribute__((amdgpu_waves_per_eu(CK ? SED_CK_WAVES : SED_I32_WAVES(R))))
+__global__ __launch_bounds__(SPLIT ? 128 : 256) __attribute__((amdgpu_waves_per_eu(CK ? SED_CK_WAVES : SED_I32_WAVES(R))))
 void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *__restrict__ tasks,
                   const uint32_t *__restrict__ seqa, const uint32_t *__restrict__ seqb,
                   uint32_t *__restrict__ tb, uint32_t *__restrict__ bnd, sed_result *__restrict__ res,
@@ -494,18 +554,24 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
     // per wave: lane 0's top values of the current 64-step chunk, and a ring of str2 selectors by column
     // (column ci at slots ci & 127 and (ci & 127) + 128; the 64 columns before 0 hold the virtual-column
     // sentinel), from which lane t reads column s - t at step s
-    __shared__ uint32_t lds_top[SPLIT ? 1 : 4][64];
+    __shared__ uint32_t lds_top[SPLIT ? SED_SPLIT_RING / 64 : 4][64];
     __shared__ uint32_t lds_sel[SPLIT ? 1 : 4][256];
-    uint32_t *lch = lds_top[SPLIT ? 0 : (threadIdx.x >> 6)];
+    __shared__ uint32_t split_flag[2];
+    uint32_t *lch = lds_top[SPLIT ? 0 : (threadIdx.x >> 6)];  // SPLIT: the whole array is the feeder's ring
     uint32_t *ring = lds_sel[SPLIT ? 0 : (threadIdx.x >> 6)];
     // SPLIT: str2's packed words in LDS (m <= 16 * SED_SPLIT_BWORDS), so the chunk loop issues no global load of its
-    // own: a wait for one with the group's stores in flight is a vmcnt(0), i.e. a store round trip per chunk
+    // own: a wait for one with the group's stores in flight is a vmcnt(0), i.e. a store round trip per chunk.  (The
+    // same per wave in the one-wave-per-pair kernels made the checkpoint kernel spill.)
     constexpr int BW = SPLIT ? SED_SPLIT_BWORDS : 1;
     __shared__ uint32_t lds_b[BW];
     const int bwords = (m + 15) >> 4;
     const bool bl = SPLIT && bwords <= BW;  // (uniform)
-    if (bl) {
+    if (bl && threadIdx.x < 64) {
         for (int x = lane; x < bwords; x += 64) lds_b[x] = pb[x];
+    }
+    if constexpr (SPLIT) {
+        if (threadIdx.x < 2) split_flag[threadIdx.x] = 0u;
+        __syncthreads();
     }
 
     for (int k = kfirst; k <= klast; ++k) {
@@ -514,14 +580,19 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         uint32_t *bnd_out = bnd + d.bnd_off;
         const uint64_t *bin64 = reinterpret_cast<const uint64_t *>(bnd + d.bnd_off) + (uint32_t)(k - 1) * bstride;
         uint64_t *bout64 = reinterpret_cast<uint64_t *>(bnd + d.bnd_off) + (uint32_t)k * bstride;
+        if constexpr (SPLIT) {
+            if (threadIdx.x >= 64) {  // the feeder wave
+                if (k > 0) split_feed<G>(bin64, m, SG, prm.epoch, lch, split_flag, lane);
+                return;
+            }
+        }
         const int row0 = k * ROWS + lane * R;  // 0-based str1 index of this lane's first row
         uint32_t cv[R], V[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int ri = row0 + r;
             const uint32_t a = (pa[ri >> 4] >> ((ri & 15) * 2)) & 3u;
-            if constexpr (DOT) cv[r] = a == 0 ? prm.dotrow[0] : a == 1 ? prm.dotrow[1] : a == 2 ? prm.dotrow[2] : prm.dotrow[3];
-            else cv[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
+            cv[r] = sel4(a, DOT ? prm.dotrow : prm.costrow);
         }
         uint32_t top_prev;
         i32_reset<R, LEN, DOT>(V, top_prev);
@@ -538,42 +609,23 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
             if constexpr (CK) return load_sc1(bnd + d.bnd_off + (uint32_t)(j + 62));
             return load_sc1(bnd_in + j + 64);
         };
-        // SPLIT: lane u < G loads the tagged word of column s0 + u + 1 for the group starting at step s0 (issued a
-        // group ahead), then every word is checked and re-polled until it carries this run's epoch; the values go
-        // to the LDS ring of lane 0's tops (slot = step & 63).  Columns past m are never stored nor waited for.
-        uint64_t pre = 0;
-        auto fetch_issue = [&](int s0n) {
-            if (lane < G) pre = load_sc1_u64(bin64 + (uint32_t)(s0n + lane + 1 + 64));
-        };
-        auto fetch_finish = [&](int s0n) {
-            const int col = s0n + lane + 1;
-            auto good = [&]() { return lane >= G || col > m || ((uint32_t)(pre >> 32) & ~SED_PROG_POISON) == prm.epoch; };
-            uint32_t spins = 0;
-            while (!__all(good())) {  // after one timeout stop waiting: the kernel must still drain quickly
-                if (!ok || ++spins > (1u << 24)) {
-                    ok = false;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-                if (!good()) pre = load_sc1_u64(bin64 + (uint32_t)(col + 64));
-            }
-            if (__any(lane < G && col <= m && (pre >> 63))) ok = false;  // poisoned upstream
-            if (lane < G) lch[(s0n + lane) & 63] = (uint32_t)pre;
-        };
         auto load_sel = [&](int c) -> uint32_t {
             const int ci = 64 * c + lane;
-            const uint32_t wb = bl ? lds_b[min(ci >> 4, bwords - 1)] : pb[ci >> 4];  // (past m: never read)
+            uint32_t wb;  // (past m: never read; a branch, so the LDS read stays a ds_read)
+            if (bl) wb = ((const __attribute__((address_space(3))) uint32_t *)lds_b)[min(ci >> 4, bwords - 1)];
+            else wb = pb[ci >> 4];
             const uint32_t b = (wb >> ((ci & 15) * 2)) & 3u;
-            if constexpr (DOT) return b == 0 ? prm.dotcol[0] : b == 1 ? prm.dotcol[1] : b == 2 ? prm.dotcol[2] : prm.dotcol[3];
+            if constexpr (DOT) return sel4(b, prm.dotcol);
             return i32_sel(b);
         };
         uint32_t tch = (SPLIT && k > 0) ? 0u : load_top(0), sch = load_sel(0);
-        lch[lane] = tch;  // SPLIT: stripe 0's constant row; the others fetch group by group
-        if constexpr (SPLIT) {
-            if (k > 0) {
-                fetch_issue(0);
-                fetch_finish(0);
+        if constexpr (SPLIT) {  // stripe 0's constant row in the whole ring; the feeder fills the others'
+            if (k == 0) {
+#pragma unroll
+                for (int x = 0; x < SED_SPLIT_RING; x += 64) lch[x + lane] = tch;
             }
+        } else {
+            lch[lane] = tch;
         }
         ring[lane] = ring[lane + 128] = sch;
         ring[lane + 64] = ring[lane + 192] = i32_sent<LEN, DOT>();
@@ -623,28 +675,37 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                 s = 64 * (c + 1);  // lane 63's bottom cells of the whole chunk are in outc (!CK)
             } else {
                 for (int g = 0; g < 64 / G && s < SG; ++g, s += G, lsel += G) {
-                    const bool fetch = SPLIT && k > 0 && s + G < SG;
-                    if (fetch) fetch_issue(s + G);
+                    const uint32_t *ltop = lch;
+                    if constexpr (SPLIT) {
+                        ltop = lch + (s & (SED_SPLIT_RING - 64));
+                        if (k > 0) {  // the feeder has this group's top values in the ring (LDS only: no vmcnt)
+                            uint32_t f = lds_flag_get(split_flag), spins = 0;
+                            while (ok && (int)(f & ~SED_PROG_POISON) < s + G) {
+                                if (++spins > (1u << 24)) ok = false;
+                                __builtin_amdgcn_s_sleep(1);
+                                f = lds_flag_get(split_flag);
+                            }
+                            if (f & SED_PROG_POISON) ok = false;
+                            asm volatile("" ::: "memory");
+                        }
+                    }
                     const bool capg = cap_step >= s && cap_step < s + G;
                     if (capg)
-                        i32_group<R, TB, LEN, true, CK, DOT>(V, cv, top_prev, bottom, selv, lch, lsel, outc, W, s, lane,
+                        i32_group<R, TB, LEN, true, CK, DOT>(V, cv, top_prev, bottom, selv, ltop, lsel, outc, W, s, lane,
                                                         cap_step, cap_lane, cap_row, cap, rcv);
                     else
-                        i32_group<R, TB, LEN, false, CK, DOT>(V, cv, top_prev, bottom, selv, lch, lsel, outc, W, s, lane,
+                        i32_group<R, TB, LEN, false, CK, DOT>(V, cv, top_prev, bottom, selv, ltop, lsel, outc, W, s, lane,
                                                          cap_step, cap_lane, cap_row, cap, rcv);
-                    // SPLIT: the next group's words are waited for before this group's stores issue.  A load wait
-                    // with stores in flight is an s_waitcnt vmcnt(0) (the compiler counts mixed reads and writes as
-                    // out of order), so waiting after the stores made every consumer group wait for its own stores
-                    // to complete: 84 instead of 51 ns per step below stripe 0 (profiles/r03/c2_shapes.jsonl).
-                    if constexpr (SPLIT) {
-                        if (fetch) fetch_finish(s + G);
-                    }
                     stores(s);
                     if constexpr (SPLIT) {
                         // lanes 64-G+u hold lane 63's bottom cell of step s+u, column s+u-62 (word col + 64)
                         if (!last && lane >= 64 - G)
                             store_tagged(bout64 + (uint32_t)(s + lane - (64 - G) - 62 + 64),
                                          prm.epoch | (ok ? 0u : SED_PROG_POISON), outc);
+                        if (k > 0) {  // this group's ring slots are free again
+                            asm volatile("" ::: "memory");
+                            if (lane == 0) lds_flag_set(split_flag + 1, (uint32_t)(s + G));
+                        }
                     }
                 }
             }
@@ -773,8 +834,8 @@ sed_wf_i32x2_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restr
         for (int r = 0; r < R; ++r) {
             const int ri = row0 + r;
             const uint32_t aP = (paP[ri >> 4] >> ((ri & 15) * 2)) & 3u, aQ = (paQ[ri >> 4] >> ((ri & 15) * 2)) & 3u;
-            cP[r] = aP == 0 ? prm.costrow16[0] : aP == 1 ? prm.costrow16[1] : aP == 2 ? prm.costrow16[2] : prm.costrow16[3];
-            cQ[r] = aQ == 0 ? prm.costrow16[0] : aQ == 1 ? prm.costrow16[1] : aQ == 2 ? prm.costrow16[2] : prm.costrow16[3];
+            cP[r] = sel4(aP, prm.costrow16);
+            cQ[r] = sel4(aQ, prm.costrow16);
         }
         uint32_t top_prev = 0xFFFFFFFFu;  // column 0 and row 0 are the offset key 0xFFFF in both halves
 #pragma unroll
@@ -981,15 +1042,14 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
         for (int r = 0; r < R; ++r) {
             const int ri = row0 + r;
             const uint32_t a = (pa[ri >> 4] >> ((ri & 15) * 2)) & 3u;
-            if constexpr (LDOT) out[r] = a == 0 ? prm.ladrow[0] : a == 1 ? prm.ladrow[1] : a == 2 ? prm.ladrow[2] : prm.ladrow[3];
-            else out[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
+            out[r] = sel4(a, LDOT ? prm.ladrow : prm.costrow);
         }
     };
     auto chunk_of = [&](const chain_pair_state &c, int cl) -> uint2 {  // lane 0's inputs, local chunk cl
         const int j = 64 * cl + lane;
         const uint32_t b = (c.pb[j >> 4] >> ((j & 15) * 2)) & 3u;
         if constexpr (LDOT)
-            return make_uint2(i32_row0<LEN>(), b == 0 ? prm.ladcol[0] : b == 1 ? prm.ladcol[1] : b == 2 ? prm.ladcol[2] : prm.ladcol[3]);
+            return make_uint2(i32_row0<LEN>(), sel4(b, prm.ladcol));
         return make_uint2(i32_row0<LEN>(), i32_sel(b));  // row 0, str2 selector
     };
     // ladder dot keys: the host's column vector {s, 0, 0, 0} adds s*x in [8, 490] (above any jump, and the border
@@ -2160,8 +2220,8 @@ __global__ void sed_selftest_kernel(uint32_t *out) {
 // ---------------------------------------------------------------------------
 template <int R, bool TB, bool LEN = true, bool CK = false, bool DOT = false>
 static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
-    if (L.ntasks > 0) {  // SPLIT: one 64-thread workgroup per (pair, stripe)
-        SED_LAUNCH((sed_wf_i32_kernel<R, TB, true, LEN>), dim3(L.ntasks), dim3(64), 0, L, L.pd, L.npairs,
+    if (L.ntasks > 0) {  // SPLIT: one workgroup per (pair, stripe): the compute wave and its feeder
+        SED_LAUNCH((sed_wf_i32_kernel<R, TB, true, LEN>), dim3(L.ntasks), dim3(128), 0, L, L.pd, L.npairs,
                            L.tasks, (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res,
                            prm);
     } else {
