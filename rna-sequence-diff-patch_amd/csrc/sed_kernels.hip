@@ -127,16 +127,6 @@ __device__ __forceinline__ uint64_t load_sc1_u64(const uint64_t *p) {
 // = 16 bytes per lane, one dwordx4 store; the wave writes 1 KiB contiguous.
 template <int R> struct Grp { static constexpr int G = 64 / R; };
 
-// t[b] for a per-lane 2-bit symbol b as two levels of selects on SGPR copies: indexing the kernel-argument array
-// (or a ?: chain over it, which the compiler turns back into an index) makes a private copy in scratch and a
-// scratch load per use, each one an s_waitcnt vmcnt(0) behind the wave's stores in flight
-__device__ __forceinline__ uint32_t sel4(const uint32_t b, const uint32_t (&t)[4]) {
-    const uint32_t c0 = __builtin_amdgcn_readfirstlane(t[0]), c1 = __builtin_amdgcn_readfirstlane(t[1]);
-    const uint32_t c2 = __builtin_amdgcn_readfirstlane(t[2]), c3 = __builtin_amdgcn_readfirstlane(t[3]);
-    const uint32_t lo = (b & 1u) ? c1 : c0, hi = (b & 1u) ? c3 : c2;
-    return (b & 2u) ? hi : lo;
-}
-
 __device__ __forceinline__ void store_tb(uint32_t *p, const uint32_t (&w)[4]) {
     *reinterpret_cast<uint4 *>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
@@ -592,7 +582,8 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         for (int r = 0; r < R; ++r) {
             const int ri = row0 + r;
             const uint32_t a = (pa[ri >> 4] >> ((ri & 15) * 2)) & 3u;
-            cv[r] = sel4(a, DOT ? prm.dotrow : prm.costrow);
+            if constexpr (DOT) cv[r] = a == 0 ? prm.dotrow[0] : a == 1 ? prm.dotrow[1] : a == 2 ? prm.dotrow[2] : prm.dotrow[3];
+            else cv[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
         }
         uint32_t top_prev;
         i32_reset<R, LEN, DOT>(V, top_prev);
@@ -611,11 +602,9 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         };
         auto load_sel = [&](int c) -> uint32_t {
             const int ci = 64 * c + lane;
-            uint32_t wb;  // (past m: never read; a branch, so the LDS read stays a ds_read)
-            if (bl) wb = ((const __attribute__((address_space(3))) uint32_t *)lds_b)[min(ci >> 4, bwords - 1)];
-            else wb = pb[ci >> 4];
+            const uint32_t wb = bl ? lds_b[min(ci >> 4, bwords - 1)] : pb[ci >> 4];  // (past m: never read)
             const uint32_t b = (wb >> ((ci & 15) * 2)) & 3u;
-            if constexpr (DOT) return sel4(b, prm.dotcol);
+            if constexpr (DOT) return b == 0 ? prm.dotcol[0] : b == 1 ? prm.dotcol[1] : b == 2 ? prm.dotcol[2] : prm.dotcol[3];
             return i32_sel(b);
         };
         uint32_t tch = (SPLIT && k > 0) ? 0u : load_top(0), sch = load_sel(0);
@@ -834,8 +823,8 @@ sed_wf_i32x2_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restr
         for (int r = 0; r < R; ++r) {
             const int ri = row0 + r;
             const uint32_t aP = (paP[ri >> 4] >> ((ri & 15) * 2)) & 3u, aQ = (paQ[ri >> 4] >> ((ri & 15) * 2)) & 3u;
-            cP[r] = sel4(aP, prm.costrow16);
-            cQ[r] = sel4(aQ, prm.costrow16);
+            cP[r] = aP == 0 ? prm.costrow16[0] : aP == 1 ? prm.costrow16[1] : aP == 2 ? prm.costrow16[2] : prm.costrow16[3];
+            cQ[r] = aQ == 0 ? prm.costrow16[0] : aQ == 1 ? prm.costrow16[1] : aQ == 2 ? prm.costrow16[2] : prm.costrow16[3];
         }
         uint32_t top_prev = 0xFFFFFFFFu;  // column 0 and row 0 are the offset key 0xFFFF in both halves
 #pragma unroll
@@ -1042,14 +1031,15 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
         for (int r = 0; r < R; ++r) {
             const int ri = row0 + r;
             const uint32_t a = (pa[ri >> 4] >> ((ri & 15) * 2)) & 3u;
-            out[r] = sel4(a, LDOT ? prm.ladrow : prm.costrow);
+            if constexpr (LDOT) out[r] = a == 0 ? prm.ladrow[0] : a == 1 ? prm.ladrow[1] : a == 2 ? prm.ladrow[2] : prm.ladrow[3];
+            else out[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
         }
     };
     auto chunk_of = [&](const chain_pair_state &c, int cl) -> uint2 {  // lane 0's inputs, local chunk cl
         const int j = 64 * cl + lane;
         const uint32_t b = (c.pb[j >> 4] >> ((j & 15) * 2)) & 3u;
         if constexpr (LDOT)
-            return make_uint2(i32_row0<LEN>(), sel4(b, prm.ladcol));
+            return make_uint2(i32_row0<LEN>(), b == 0 ? prm.ladcol[0] : b == 1 ? prm.ladcol[1] : b == 2 ? prm.ladcol[2] : prm.ladcol[3]);
         return make_uint2(i32_row0<LEN>(), i32_sel(b));  // row 0, str2 selector
     };
     // ladder dot keys: the host's column vector {s, 0, 0, 0} adds s*x in [8, 490] (above any jump, and the border
