@@ -1080,6 +1080,33 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
             }
         }
         const uint32_t *lsel0 = ring + ((s0 - lane) & 127);  // this lane's global column at the chunk's first step
+        // A chunk with every lane on cur, no switch window and no sink capture runs its own loop of plain groups:
+        // with the three group variants in one loop, the register allocator copied the row state (18 v_mov) after
+        // every plain group at the merge point (5.6 % of its VALU).  Pairs start on chunk boundaries (T is a
+        // multiple of 64), so a window is always a whole chunk.
+        const bool plain = have_cur && s0 >= cur.T && !(have_prv && s0 < cur.T + 64) &&
+                           !(have_prv && prv.cap_step >= s0 && prv.cap_step < s0 + 64) &&
+                           !(cur.cap_step >= s0 && cur.cap_step < s0 + 64);
+        if (plain) {
+            for (int g = 0; g < 64 / G; ++g) {
+                const int s = s0 + g * G;
+                i32_chain_group<R, TB, LEN, false, false, CK, LDOT>(
+                    V, cv, cvn, Vb, tpb, top_prev, bottom, selv, lsel0 + g * G, outc, W, s, lane, -(1 << 30), prv.cap_step,
+                    prv.cap_lane, prv.cap_row, capA, cur.cap_step, cur.cap_lane, cur.cap_row, capB, rcv);
+                if constexpr (TB) {
+                    uint32_t lo = (uint32_t)lane * 16u;
+                    asm volatile("" : "+v"(lo));
+                    char *gp = reinterpret_cast<char *>(tb + cur.tb_off + (uint64_t)((s - cur.T) / G) * 256u);
+                    *reinterpret_cast<uint4 *>(gp + lo) = make_uint4(W[0], W[1], W[2], W[3]);
+                }
+                if constexpr (CK) {
+                    constexpr int GH = SED_CK_TILE / R;
+                    if ((lane & (GH - 1)) == GH - 1)
+                        store_words<G>(tb + cur.tb_off + sed_ck_col_words(R, 1, cur.nchunks) +
+                                           (uint64_t)((s - cur.T) / G) * SED_CK_RW + (uint32_t)(lane / GH) * G, rcv);
+                }
+            }
+        } else
         for (int g = 0; g < 64 / G; ++g) {
             const int s = s0 + g * G;
             const uint32_t *lsel = lsel0 + g * G;
