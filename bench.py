@@ -663,7 +663,11 @@ def main():
             dist.destroy_process_group()
         return
     dp_avg = float(np.mean(dp_ms))
-    achieved = algo_bytes / (dp_avg * 1e-3) / 1e9
+    # a checkpoint batch of >= 2048 pairs runs as two halves on two streams (SED_CK_HALVES): the run times are the
+    # first half's kernels, one launch each, so bytes and cells are per launch too; frac_step covers the whole step
+    launches = batch.dp_launches
+    algo_launch, design_launch, cells_launch = algo_bytes / launches, design_bytes / launches, cells / launches
+    achieved = algo_launch / (dp_avg * 1e-3) / 1e9
     nl, npk = batch.lane_pairs, batch.packed_pairs
     lane_x2 = batch.mode == "i32" and not want_script and nl > 0 and not args.no_pack
     wave_x2 = npk - (nl if lane_x2 else 0)  # wave pairs computed two per wave
@@ -681,7 +685,7 @@ def main():
         else:
             ops_cell = CELL_OPS["nolen_x2" if npk == P else "nolen"]
     valu_peak = SIMDS * CLOCK * 64 / (VALU_CYCLES_PER_OP * ops_cell) if ops_cell else None
-    rate = cells / (dp_avg * 1e-3)
+    rate = cells_launch / (dp_avg * 1e-3)
     if batch.mode != "i32":
         parts = (["sed_wf_f64_kernel"] if nl < P else []) + (["sed_lane_f64_kernel"] if nl else [])
     else:
@@ -721,14 +725,14 @@ def main():
                    "parallelism": "dp%d" % world, "env": env},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": kname, "kernel_ms": dp_avg,
-                     "algo_bytes_per_launch": algo_bytes,
+                     "kernel": kname, "kernel_ms": dp_avg, "launches_per_step": launches,
+                     "algo_bytes_per_launch": algo_launch,
                      "algo_bytes_def": "SURVEY.md 8(d): per pair (n+m)/4 in + 8 out" +
                                        (" + 0.25 B/cell traceback + (n+m) reads + (n+m)/4 ops out" if want_script
                                         else ""),
                      "frac_step": algo_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "design_bytes_per_launch": design_bytes,
-                     "design_frac": design_bytes / (dp_avg * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                     "design_bytes_per_launch": design_launch,
+                     "design_frac": design_launch / (dp_avg * 1e-3) / 1e9 / HBM_PEAK_GBS},
         "valu": None if valu_peak is None else {
             "model": "%.4g VALU ops/cell x %.1f cycles/op per wave64 (tools/ubench/valu_row.hip), 1024 SIMDs, %.1f GHz"
                      % (ops_cell, VALU_CYCLES_PER_OP, CLOCK / 1e9),

@@ -140,7 +140,10 @@ int sed_batch_traceback_mode(const sed_batch *b);     /* 0 no script, 1 per-cell
  * the most pairs one wave computed back to back (0 when CHAIN mode is off). */
 int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave);
 int sed_batch_run(sed_batch *b);                      /* enqueue on the context stream, returns at once */
-int sed_batch_sync(sed_batch *b);                     /* wait for the last run */
+int sed_batch_sync(sed_batch *b);                     /* wait for the last run (every stream the batch uses) */
+/* Forward launches per run: 2 when a checkpoint batch of >= 2048 wave pairs runs as two halves on two streams
+ * (SED_CK_HALVES, default on), else 1.  Then the run times below are the first half's kernels, one launch each. */
+int sed_batch_dp_launches(const sed_batch *b);
 /* device time of the last run, from HIP events on the launching stream (ms) */
 int sed_batch_last_times(const sed_batch *b, float *dp_ms, float *traceback_ms);
 /* Device times of every run since the last sed_batch_reset_times (waits for them):
@@ -149,7 +152,8 @@ int sed_batch_times(sed_batch *b, float *dp_ms, float *traceback_ms, int max_run
 int sed_batch_reset_times(sed_batch *b);
 int sed_batch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32_t *out_len,
                       uint32_t *out_ops, const int64_t *ops_off);
-/* Device pointers of the result arrays (for an RCCL gather); any may be NULL. */
+/* Device pointers of the result arrays (for an RCCL gather); any may be NULL.  Call sed_batch_sync first: the
+ * pointers are not ordered after the batch's streams. */
 int sed_batch_device_results(const sed_batch *b, uint64_t *d_dist, uint64_t *d_is_int,
                              uint64_t *d_len, uint64_t *d_ops, uint64_t *ops_words);
 /* Copy dist (f64[npairs]), len (i32[npairs]) and the packed scripts (u32[ops_words]) of the last

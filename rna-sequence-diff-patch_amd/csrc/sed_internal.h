@@ -146,6 +146,9 @@ __host__ __device__ inline uint64_t sed_ck_col_words(int R, int nstripes, int nc
 // SED_CK_RW = 64 * 64 / SED_CK_TILE words, [group][t / GH][step % G].  SED_CK_TILE = 32 (twice the row checkpoints)
 // served a two-pairs-per-wave traceback of 32-row tiles, measured and dropped in round 3: the forward kernel took
 // 9.87 instead of 9.18-9.32 ms and that traceback 2.43 instead of 2.20 ms (profiles/r03/ab_tb_tiles.jsonl).
+#ifndef SED_CK_HALVES_DEFAULT
+#define SED_CK_HALVES_DEFAULT 1  // checkpoint batches of >= 2048 wave pairs in two halves on two streams (sed_runtime.cpp)
+#endif
 #ifndef SED_CK_TILE
 #define SED_CK_TILE 64
 #endif

@@ -75,6 +75,7 @@ SIGNATURES = [
     ("sed_batch_times", C.c_int, [C.c_void_p, _f32p, _f32p, C.c_int]),
     ("sed_batch_reset_times", C.c_int, [C.c_void_p]),
     ("sed_batch_results", C.c_int, [C.c_void_p, _f64p, _u8p, _i32p, C.c_void_p, C.c_void_p]),
+    ("sed_batch_dp_launches", C.c_int, [C.c_void_p]),
     ("sed_batch_device_results", C.c_int, [C.c_void_p] + [C.POINTER(C.c_uint64)] * 5),
     ("sed_batch_export", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64]),
     ("sed_batch_work", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
@@ -338,6 +339,12 @@ class Batch:
         a, b = C.c_double(), C.c_double()
         self._lib.sed_batch_work(self.ptr, C.byref(a), C.byref(b))
         return a.value, b.value
+
+    @property
+    def dp_launches(self):
+        """Forward launches per run (2: a checkpoint batch in two halves on two streams; the run times are then
+        the first half's kernels)."""
+        return self._lib.sed_batch_dp_launches(self.ptr)
 
     def device_results(self):
         vals = [C.c_uint64() for _ in range(5)]

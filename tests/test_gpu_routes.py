@@ -243,6 +243,45 @@ def test_checkpoint_traceback_reports_a_corrupt_checkpoint(gpu, tables):
     _check_all(plan, packed, d, ii, ln, ops)
 
 
+def test_checkpoint_halves_on_two_streams(gpu, tables):
+    """A checkpoint batch of >= 2048 wave pairs runs as two halves on two streams (SED_CK_HALVES, default on: one
+    half's traceback beside the other half's forward, no join between runs).  2200 ragged wave pairs plus 101
+    lane-kernel pairs, shuffled (an odd count): three runs back to back, every pair vs the oracle; then a corrupted
+    checkpoint of a second-half pair fails the run naming that pair, and the batch size's first run after it is
+    right again."""
+    A1, B1 = _ragged(3600, 2200, 200, 700, 200, 700)
+    A2, B2 = _ragged(3601, 101, 1, 300, 1, 32)
+    A, B = A1 + A2, B1 + B2
+    order = np.random.default_rng(3602).permutation(len(A))
+    A, B = [A[i] for i in order], [B[i] for i in order]
+    plan = _plan(tables[True])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs(A, B)
+    gpu.set_option(sedgpu.SED_OPT_TB, 2)
+    gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 4)
+    try:
+        b, (d, ii, ln, ops) = _batch_run(gpu, packed, True, runs=3)
+        try:
+            assert b.traceback_mode == 2 and b.dp_launches == 2 and b.lane_pairs == 101
+        finally:
+            b.close()
+        _check_all(plan, packed, d, ii, ln, ops)
+        victim = max(p for p in range(len(A)) if len(B[p]) > 32)  # a wave pair of the second half
+        gpu.set_option(sedgpu.SED_OPT_DEBUG_CORRUPT, victim + 1)
+        try:
+            with pytest.raises(sedgpu.SedError, match="pair %d: traceback failed" % victim):
+                gpu.run(packed, True)
+        finally:
+            gpu.set_option(sedgpu.SED_OPT_DEBUG_CORRUPT, 0)
+        d2, ii2, ln2, ops2 = gpu.run(packed, True)
+        assert np.array_equal(d2, d) and np.array_equal(ln2, ln)
+        assert all(np.array_equal(sedgpu.unpack_ops(ops2, packed.ops_off, p, int(ln[p])),
+                                  sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln[p]))) for p in range(len(A)))
+    finally:
+        gpu.set_option(sedgpu.SED_OPT_TB, 0)
+        gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
+
+
 def test_repeated_runs_reuse_the_context(gpu, tables):
     """sed_run_batch refills one scratch batch per call (event log reused, not grown): many small calls in
     a row stay correct."""

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Interleaved A/B of environment settings on one build: tools/ab_env.sh TAG ROUNDS "ENV1" "ENV2" ...  (bench args in
+# $AB_ARGS, default the c4 bench; "-" = no extra variable) -> gpurun_out/TAG/ab.jsonl
+set -e
+TAG=$1; N=$2; shift 2
+O=gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+for r in $(seq 1 $N); do
+  for V in "$@"; do
+    if [ "$V" = "-" ]; then EV=""; else EV="$V"; fi
+    env $EV timeout -k 10 200 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --traffic none ${AB_ARGS} > $O/ab.json 2>> $O/ab.log
+    python3 -c "import json; d=json.load(open('$O/ab.json')); print(json.dumps({'env':'$V','round':$r,'value':d['value'],'dp_ms':d['roofline']['kernel_ms'],'valid':d.get('script_valid_rate'),'exact':d.get('script_exact_rate'),'tb_ms':d.get('traceback_ms'),'step_ms':d['ms_per_step']}))" >> $O/ab.jsonl
+  done
+done
