@@ -141,8 +141,9 @@ int sed_batch_traceback_mode(const sed_batch *b);     /* 0 no script, 1 per-cell
 int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave);
 int sed_batch_run(sed_batch *b);                      /* enqueue on the context stream, returns at once */
 int sed_batch_sync(sed_batch *b);                     /* wait for the last run (every stream the batch uses) */
-/* Forward launches per run: 2 when a checkpoint batch of >= 2048 wave pairs runs as two halves on two streams
- * (SED_CK_HALVES, default on), else 1.  Then the run times below are the first half's kernels, one launch each. */
+/* Forward launches per run: a checkpoint batch of >= 2048 wave pairs runs in parts on as many streams
+ * (SED_CK_HALVES = parts, default 2, >= 1024 wave pairs each), else 1.  With parts, the run times below are part 0's
+ * kernels, one launch each. */
 int sed_batch_dp_launches(const sed_batch *b);
 /* device time of the last run, from HIP events on the launching stream (ms) */
 int sed_batch_last_times(const sed_batch *b, float *dp_ms, float *traceback_ms);

@@ -109,10 +109,10 @@ struct sed_batch {
     int nbuf = 1;
     DevBuf d_tb[3], d_res[3];
     hipStream_t tb_stream = nullptr;
-    // Checkpoint batches in two halves (SED_CK_HALVES): pairs [0, h) run forward then traceback on the context's
-    // stream, pairs [h, n) on half_stream, so one half's traceback overlaps the other half's forward.
-    bool halves = false;
-    hipStream_t half_stream = nullptr;
+    // Checkpoint batches in parts (SED_CK_HALVES = number of parts): part 0 runs forward then traceback on the
+    // context's stream, part i on part_stream[i - 1], so one part's traceback overlaps another part's forward.
+    int nparts = 1;
+    hipStream_t part_stream[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_start = nullptr;
     // per buffer: the event-log entry of the last run that used it (handles copied from `log`)
     std::array<hipEvent_t, 4> evk[3] = {};
@@ -135,7 +135,8 @@ struct sed_batch {
             d_res[i].release();
         }
         if (tb_stream) (void)hipStreamDestroy(tb_stream);
-        if (half_stream) (void)hipStreamDestroy(half_stream);
+        for (hipStream_t &ps : part_stream)
+            if (ps) (void)hipStreamDestroy(ps);
         if (ev_start) (void)hipEventDestroy(ev_start);
         for (auto &a : log)
             for (hipEvent_t e : a)
@@ -403,7 +404,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
                uint32_t flags) {
     sed_ctx *c = b->ctx;
     if (!c->have_costs) return c->fail(SED_E_STATE, "sed_set_costs() was not called");
-    if (b->half_stream) (void)hipStreamSynchronize(b->half_stream);  // (a refill must not overwrite a running half)
+    for (hipStream_t ps : b->part_stream)  // (a refill must not overwrite a running part)
+        if (ps) (void)hipStreamSynchronize(ps);
     if (npairs < 0 || (npairs > 0 && (!codes_a || !off_a || !len_a || !codes_b || !off_b || !len_b)))
         return c->fail(SED_E_ARG, "bad batch arguments");
     b->npairs = npairs;
@@ -811,76 +813,79 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     if (b->nbuf > 1 && !b->tb_stream &&
         (e = hipStreamCreateWithFlags(&b->tb_stream, hipStreamNonBlocking)) != hipSuccess)
         return c->hipfail(e, "traceback stream");
-    // SED_CK_HALVES: 0 off, 1 on (A/B; default SED_CK_HALVES_DEFAULT)
-    static const int halves_env = [] { const char *e = getenv("SED_CK_HALVES"); return e ? atoi(e) : -1; }();
-    const int hv = halves_env < 0 ? SED_CK_HALVES_DEFAULT : halves_env;
-    b->halves = hv > 0 && b->ck && b->nchains == 0 && b->nbuf == 1 && b->nwave >= 2048 && b->nwave_x2 == 0;
-    if (b->halves) {
-        if (!b->half_stream && (e = hipStreamCreateWithFlags(&b->half_stream, hipStreamNonBlocking)) != hipSuccess)
-            return c->hipfail(e, "second stream");
-        if (!b->ev_start && (e = hipEventCreateWithFlags(&b->ev_start, hipEventDisableTiming)) != hipSuccess)
-            return c->hipfail(e, "event create");
-    }
+    // SED_CK_HALVES: parts per checkpoint batch of >= 1024 wave pairs per part (1 = off; default
+    // SED_CK_HALVES_DEFAULT; at most 4, the hardware queues a process gets)
+    static const int parts_env = [] { const char *e = getenv("SED_CK_HALVES"); return e ? atoi(e) : -1; }();
+    const int want = std::min(4, std::max(1, parts_env < 0 ? SED_CK_HALVES_DEFAULT : parts_env));
+    b->nparts = 1;
+    if (b->ck && b->nchains == 0 && b->nbuf == 1 && b->nwave_x2 == 0)
+        b->nparts = std::max(1, std::min(want, b->nwave / 1024));
+    for (int i = 0; i + 1 < b->nparts; ++i)
+        if (!b->part_stream[i] && (e = hipStreamCreateWithFlags(&b->part_stream[i], hipStreamNonBlocking)) != hipSuccess)
+            return c->hipfail(e, "part stream");
+    if (b->nparts > 1 && !b->ev_start && (e = hipEventCreateWithFlags(&b->ev_start, hipEventDisableTiming)) != hipSuccess)
+        return c->hipfail(e, "event create");
     return SED_OK;
 }
 
-// A checkpoint batch as two halves on two streams (b->halves).  Stream 1 runs forward(H1) then traceback(H1),
-// stream 2 forward(H2) then traceback(H2).  Stream 2 starts each run after stream 1's previous work, and
-// nothing joins the streams at a run's end, so the halves settle into a stagger: one half's traceback runs
-// beside the other half's forward (config 4: 11.2-11.35 -> 10.6 ms per step; joined at every run's end, the
-// halves ran in lockstep and gained nothing, profiles/r03/halves/).  The halves share no buffer region (every
-// pair has its own checkpoints, bottom rows, script words and result), and sync_batch waits for both streams.
-// The run's event log times the first half's kernels, one launch each (sed_batch_dp_launches() = 2).
-int run_batch_halves(sed_batch *b, const std::array<hipEvent_t, 4> &lg, sed_launch L, const sed_i32_params &ip,
-                     bool len) {
+// A checkpoint batch in parts on as many streams (b->nparts).  Stream i runs forward(part i) then
+// traceback(part i).  The other streams start each run after stream 0's previous work, and nothing joins the
+// streams at a run's end, so the parts settle into a stagger: one part's traceback runs beside another part's
+// forward (config 4, two parts: 11.2-11.35 -> 10.6 ms per step; joined at every run's end the halves ran in
+// lockstep and gained nothing, profiles/r03/halves/).  The parts share no buffer region (every pair has its own
+// checkpoints, bottom rows, script words and result), and sync_batch waits for every stream.  The run's event
+// log times part 0's kernels, one launch each (sed_batch_dp_launches() = nparts).
+int run_batch_parts(sed_batch *b, const std::array<hipEvent_t, 4> &lg, sed_launch L, const sed_i32_params &ip,
+                    bool len) {
     sed_ctx *c = b->ctx;
     hipError_t e;
-    const int h = b->npairs / 2;
-    hipStream_t s1 = c->stream, s2 = b->half_stream;
-    // the second stream starts after everything queued before this run (uploads, the previous run's first half)
-    if ((e = hipEventRecord(b->ev_start, s1)) != hipSuccess || (e = hipStreamWaitEvent(s2, b->ev_start, 0)) != hipSuccess)
-        return c->hipfail(e, "stream fork");
-    sed_launch L1 = L, L2 = L;
-    L1.npairs = h;
-    L1.stream = s1;
-    L1.ev0 = lg[0];
-    L1.ev1 = lg[1];
-    L2.pd = L.pd + h;
-    L2.res = L.res + h;
-    L2.npairs = b->npairs - h;
-    L2.stream = s2;
-    L2.ev0 = L2.ev1 = nullptr;
-    if ((e = sed_launch_i32(L1, ip, len)) != hipSuccess || (e = sed_launch_i32(L2, ip, len)) != hipSuccess)
-        return c->hipfail(e, "DP kernel launch");
-    if (b->nlane > 0) {  // lane pairs (the whole batch's, by index) after the first half's forward
-        L1.pd = L.pd;
-        L1.res = L.res;
-        L1.npairs = b->npairs;
-        L1.ev0 = L1.ev1 = nullptr;
-        if ((e = sed_launch_lane_i32(L1, (const int32_t *)b->d_lane.p, b->nlane, ip, len)) != hipSuccess)
+    const int P = b->nparts;
+    auto stream = [&](int i) { return i == 0 ? c->stream : b->part_stream[i - 1]; };
+    auto first = [&](int i) { return (int)((int64_t)b->npairs * i / P); };
+    // the other streams start after everything queued before this run (uploads, the previous run's part 0)
+    if ((e = hipEventRecord(b->ev_start, c->stream)) != hipSuccess) return c->hipfail(e, "stream fork");
+    for (int i = 1; i < P; ++i)
+        if ((e = hipStreamWaitEvent(stream(i), b->ev_start, 0)) != hipSuccess) return c->hipfail(e, "stream fork");
+    // SED_CK_PART_EVENTS=1 (A/B): each phase's end event on the last part's kernel instead of part 0's
+    static const bool ev_last = [] { const char *v = getenv("SED_CK_PART_EVENTS"); return v && atoi(v) == 1; }();
+    auto part = [&](int i, hipEvent_t e0, hipEvent_t e1) {
+        sed_launch Li = L;
+        Li.pd = L.pd + first(i);
+        Li.res = L.res + first(i);
+        Li.npairs = first(i + 1) - first(i);
+        Li.stream = stream(i);
+        Li.ev0 = i == 0 ? e0 : nullptr;
+        Li.ev1 = i == (ev_last ? P - 1 : 0) ? e1 : nullptr;
+        return Li;
+    };
+    for (int i = 0; i < P; ++i)
+        if ((e = sed_launch_i32(part(i, lg[0], lg[1]), ip, len)) != hipSuccess) return c->hipfail(e, "DP kernel launch");
+    if (b->nlane > 0) {  // lane pairs (the whole batch's, by index) after part 0's forward
+        sed_launch Ll = L;
+        Ll.ev0 = Ll.ev1 = nullptr;
+        if ((e = sed_launch_lane_i32(Ll, (const int32_t *)b->d_lane.p, b->nlane, ip, len)) != hipSuccess)
             return c->hipfail(e, "lane kernel launch");
-        L1.npairs = h;
     }
     if (c->opt_debug_corrupt > 0 && c->opt_debug_corrupt <= b->npairs) {
         const int p = c->opt_debug_corrupt - 1;
         const sed_pair_desc &d = b->pd[p];
         const int R = b->R, ROWS = R * 64, G = 64 / R;
+        int ip_ = 0;
+        while (ip_ + 1 < P && p >= first(ip_ + 1)) ++ip_;
         if (!d.lane && d.n > 0 && d.m > 0) {
             const int nstripes = (d.n + ROWS - 1) / ROWS, SG = (d.m + 63 + G - 1) / G * G, nchunks = (SG + 63) >> 6;
             const int t = ((d.n - 1) % ROWS) / R, r = (d.n - 1) % R, cs = (d.m - 1 + t) >> 6;
             if (cs >= 1) {
                 uint32_t *w = (uint32_t *)L.tb + d.tb_off + sed_ck_col_word(R, nstripes - 1, nchunks, cs - 1, r, t);
-                if ((e = hipMemsetD32Async((hipDeviceptr_t)w, b->dot ? 0x3FFFFFFFu : 0x0000FFFCu, 1, p < h ? s1 : s2)) !=
+                if ((e = hipMemsetD32Async((hipDeviceptr_t)w, b->dot ? 0x3FFFFFFFu : 0x0000FFFCu, 1, stream(ip_))) !=
                     hipSuccess)
                     return c->hipfail(e, "debug corrupt");
             }
         }
     }
-    L1.ev0 = lg[2];
-    L1.ev1 = lg[3];
-    if ((e = sed_launch_traceback_ck(L1, (uint32_t *)b->d_ops.p, ip)) != hipSuccess ||
-        (e = sed_launch_traceback_ck(L2, (uint32_t *)b->d_ops.p, ip)) != hipSuccess)
-        return c->hipfail(e, "traceback kernel launch");
+    for (int i = 0; i < P; ++i)
+        if ((e = sed_launch_traceback_ck(part(i, lg[2], lg[3]), (uint32_t *)b->d_ops.p, ip)) != hipSuccess)
+            return c->hipfail(e, "traceback kernel launch");
     b->evk[0] = lg;
     ++b->runs;
     b->ran = true;
@@ -942,7 +947,7 @@ int run_batch(sed_batch *b) {
         (e = hipMemsetAsync(b->d_bnd.p, 0, 4 * b->bnd_words, c->stream)) != hipSuccess)
         return c->hipfail(e, "memset hand-off words");
     const bool len = want_tb || !(b->flags & SED_NO_LEN);
-    if (b->halves && want_tb) return run_batch_halves(b, lg, L, ip, len);
+    if (b->nparts > 1 && want_tb) return run_batch_parts(b, lg, L, ip, len);
     if (b->nwave_x2 > 0) {
         dp_events();
         if ((e = sed_launch_i32x2(L, (const int32_t *)b->d_x2.p, b->nwave_x2, ip)) != hipSuccess)
@@ -1031,7 +1036,8 @@ int sync_batch(sed_batch *b) {
     sed_ctx *c = b->ctx;
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess && b->tb_stream) e = hipStreamSynchronize(b->tb_stream);
-    if (e == hipSuccess && b->half_stream) e = hipStreamSynchronize(b->half_stream);
+    for (hipStream_t ps : b->part_stream)
+        if (e == hipSuccess && ps) e = hipStreamSynchronize(ps);
     return e == hipSuccess ? SED_OK : c->hipfail(e, "kernel execution");
 }
 
@@ -1326,7 +1332,7 @@ int sed_batch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32
     return fetch_results(b, out_dist, out_is_int, out_len, out_ops, ops_off);
 }
 
-int sed_batch_dp_launches(const sed_batch *b) { return b ? (b->halves ? 2 : 1) : SED_E_ARG; }
+int sed_batch_dp_launches(const sed_batch *b) { return b ? b->nparts : SED_E_ARG; }
 
 int sed_batch_device_results(const sed_batch *b, uint64_t *d_dist, uint64_t *d_is_int, uint64_t *d_len,
                              uint64_t *d_ops, uint64_t *ops_words) {
