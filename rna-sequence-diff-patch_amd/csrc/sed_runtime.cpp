@@ -831,8 +831,9 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
 // A checkpoint batch in parts on as many streams (b->nparts).  Stream i runs forward(part i) then
 // traceback(part i).  The other streams start each run after stream 0's previous work, and nothing joins the
 // streams at a run's end, so the parts settle into a stagger: one part's traceback runs beside another part's
-// forward (config 4, two parts: 11.2-11.35 -> 10.6 ms per step; joined at every run's end the halves ran in
-// lockstep and gained nothing, profiles/r03/halves/).  The parts share no buffer region (every pair has its own
+// forward (config 4: 11.42-11.47 ms in one part, 10.85-11.0 in two, 10.77-10.83 in three, 11.6-11.8 in four;
+// joined at every run's end two halves ran in lockstep and gained nothing; profiles/r03/halves/, parts/).  The
+// parts share no buffer region (every pair has its own
 // checkpoints, bottom rows, script words and result), and sync_batch waits for every stream.  The run's event
 // log times part 0's kernels, one launch each (sed_batch_dp_launches() = nparts).
 int run_batch_parts(sed_batch *b, const std::array<hipEvent_t, 4> &lg, sed_launch L, const sed_i32_params &ip,
@@ -846,8 +847,6 @@ int run_batch_parts(sed_batch *b, const std::array<hipEvent_t, 4> &lg, sed_launc
     if ((e = hipEventRecord(b->ev_start, c->stream)) != hipSuccess) return c->hipfail(e, "stream fork");
     for (int i = 1; i < P; ++i)
         if ((e = hipStreamWaitEvent(stream(i), b->ev_start, 0)) != hipSuccess) return c->hipfail(e, "stream fork");
-    // SED_CK_PART_EVENTS=1 (A/B): each phase's end event on the last part's kernel instead of part 0's
-    static const bool ev_last = [] { const char *v = getenv("SED_CK_PART_EVENTS"); return v && atoi(v) == 1; }();
     auto part = [&](int i, hipEvent_t e0, hipEvent_t e1) {
         sed_launch Li = L;
         Li.pd = L.pd + first(i);
@@ -855,7 +854,7 @@ int run_batch_parts(sed_batch *b, const std::array<hipEvent_t, 4> &lg, sed_launc
         Li.npairs = first(i + 1) - first(i);
         Li.stream = stream(i);
         Li.ev0 = i == 0 ? e0 : nullptr;
-        Li.ev1 = i == (ev_last ? P - 1 : 0) ? e1 : nullptr;
+        Li.ev1 = i == 0 ? e1 : nullptr;
         return Li;
     };
     for (int i = 0; i < P; ++i)

@@ -243,13 +243,13 @@ def test_checkpoint_traceback_reports_a_corrupt_checkpoint(gpu, tables):
     _check_all(plan, packed, d, ii, ln, ops)
 
 
-def test_checkpoint_halves_on_two_streams(gpu, tables):
-    """A checkpoint batch of >= 2048 wave pairs runs as two halves on two streams (SED_CK_HALVES, default on: one
-    half's traceback beside the other half's forward, no join between runs).  2200 ragged wave pairs plus 101
-    lane-kernel pairs, shuffled (an odd count): three runs back to back, every pair vs the oracle; then a corrupted
-    checkpoint of a second-half pair fails the run naming that pair, and the batch size's first run after it is
-    right again."""
-    A1, B1 = _ragged(3600, 2200, 200, 700, 200, 700)
+def test_checkpoint_parts_on_streams(gpu, tables):
+    """A checkpoint batch of >= 2048 wave pairs runs in parts on as many streams (SED_CK_HALVES, default 3 parts of
+    >= 1024 wave pairs: one part's traceback beside another part's forward, no join between runs).  3100 ragged wave
+    pairs plus 101 lane-kernel pairs, shuffled (an odd count): three runs back to back, every pair vs the oracle;
+    then a corrupted checkpoint of a last-part pair fails the run naming that pair, and the next run is right
+    again."""
+    A1, B1 = _ragged(3600, 3100, 200, 700, 200, 700)
     A2, B2 = _ragged(3601, 101, 1, 300, 1, 32)
     A, B = A1 + A2, B1 + B2
     order = np.random.default_rng(3602).permutation(len(A))
@@ -262,11 +262,11 @@ def test_checkpoint_halves_on_two_streams(gpu, tables):
     try:
         b, (d, ii, ln, ops) = _batch_run(gpu, packed, True, runs=3)
         try:
-            assert b.traceback_mode == 2 and b.dp_launches == 2 and b.lane_pairs == 101
+            assert b.traceback_mode == 2 and b.dp_launches == 3 and b.lane_pairs == 101
         finally:
             b.close()
         _check_all(plan, packed, d, ii, ln, ops)
-        victim = max(p for p in range(len(A)) if len(B[p]) > 32)  # a wave pair of the second half
+        victim = max(p for p in range(len(A)) if len(B[p]) > 32)  # a wave pair of the last part
         gpu.set_option(sedgpu.SED_OPT_DEBUG_CORRUPT, victim + 1)
         try:
             with pytest.raises(sedgpu.SedError, match="pair %d: traceback failed" % victim):
