@@ -663,8 +663,9 @@ def main():
             dist.destroy_process_group()
         return
     dp_avg = float(np.mean(dp_ms))
-    # a checkpoint batch of >= 2048 pairs runs as two halves on two streams (SED_CK_HALVES): the run times are the
-    # first half's kernels, one launch each, so bytes and cells are per launch too; frac_step covers the whole step
+    # a checkpoint batch of >= 2048 pairs runs in parts on as many streams (SED_CK_HALVES): the run times are the
+    # mean launch over the parts, so bytes and cells are per launch too; the launches overlap each other's kernels,
+    # so frac_step (the whole step's bytes over the step time) is the aggregate
     launches = batch.dp_launches
     algo_launch, design_launch, cells_launch = algo_bytes / launches, design_bytes / launches, cells / launches
     achieved = algo_launch / (dp_avg * 1e-3) / 1e9

@@ -142,8 +142,8 @@ int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave)
 int sed_batch_run(sed_batch *b);                      /* enqueue on the context stream, returns at once */
 int sed_batch_sync(sed_batch *b);                     /* wait for the last run (every stream the batch uses) */
 /* Forward launches per run: a checkpoint batch of >= 2048 wave pairs runs in parts on as many streams
- * (SED_CK_HALVES = parts, default 3, >= 1024 wave pairs each), else 1.  With parts, the run times below are part 0's
- * kernels, one launch each. */
+ * (SED_CK_HALVES = parts, default 3, >= 1024 wave pairs each), else 1.  With parts, the run times below are the mean
+ * launch over the parts (the launches overlap each other's kernels). */
 int sed_batch_dp_launches(const sed_batch *b);
 /* device time of the last run, from HIP events on the launching stream (ms) */
 int sed_batch_last_times(const sed_batch *b, float *dp_ms, float *traceback_ms);

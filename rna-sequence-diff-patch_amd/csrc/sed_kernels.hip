@@ -1955,6 +1955,14 @@ __device__ __forceinline__ uint32_t ck_walk(const uint32_t (&W)[8], uint32_t S, 
     return S & 0xFFFFu;
 }
 
+// SED_CK_VHOLD (experimental, default off): lanes left of their window hold without a select at R = 16 (per-band
+// selector copies, a compensated delete addend on each band's first row); it fails the entry check on costs.json
+// pairs, so it is kept as a switch for the debug dumps below
+#ifndef SED_CK_VHOLD
+#define SED_CK_VHOLD 0
+#endif
+#define SED_CK_SELB (64 + 132)
+template <int R> struct CkVHold { static constexpr bool value = SED_CK_VHOLD && R == 16; };
 // lanes 0 .. n-1 have reached their window at sweep step sig (sig0(r) = r - r/R + G - 1 is nondecreasing)
 template <int R> constexpr int ck_active_lanes(int sig) {
     constexpr int G = 64 / R;
@@ -2004,8 +2012,12 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
                                                   uint32_t *__restrict__ selb) {
     constexpr int ROWS = 64 * R, G = Grp<R>::G;  // a tile: G forward lanes (bands) of R rows
     constexpr int LR = R == 4 ? 2 : R == 8 ? 3 : 4;
+    constexpr bool VHOLD = CkVHold<R>::value;
     static_assert((1 << LR) == R, "R in {4, 8, 16}");
     const int n = d.n, m = d.m;
+#ifdef SED_TB_DEBUG
+    int visit = 0;  // debug dumps: 136 words per tile visit (entry keys, initial keys, coordinates)
+#endif
     uint32_t *out = ops + d.ops_off;
     uint32_t q = q0, err = 0;
     uint64_t acc = 0;  // the last 32 ops, the latest (position q) in bits 1:0
@@ -2082,6 +2094,7 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
             if (c >= 1) {
                 V = ck_to_tb(ck0, prm);
                 tp = ck_to_tb(ck1, prm);
+                if (VHOLD && J0 - band - 1 > m) V = 0u;  // (forward garbage past m: key 0 holds under the recurrence)
             }
             tp += 1u;  // diagonals carry the +1 of the delete candidate they were taken from
 #pragma unroll
@@ -2092,7 +2105,13 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
                     topb[x] = v + 1u;
                     const int col = J0 - (G - 1) + x;  // column of lane 0 at step x
                     const int ci = min(max(col - 1, 0), m - 1);
-                    selb[64 + x] = col < 1 ? SED_SEL_SENT : i32_sel((wb[h] >> ((ci & 15) * 2)) & 3u);
+                    const uint32_t sv = col < 1 ? SED_SEL_SENT : i32_sel((wb[h] >> ((ci & 15) * 2)) & 3u);
+                    if constexpr (VHOLD) {  // band b's copy: the sentinel left of its window (x < G - 1 - b)
+#pragma unroll
+                        for (int b = 0; b < G; ++b) selb[b * SED_CK_SELB + 64 + x] = x < G - 1 - b ? SED_SEL_SENT : sv;
+                    } else {
+                        selb[64 + x] = sv;
+                    }
                 }
             }
             ck_sync<WAVE>();
@@ -2105,21 +2124,33 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
             // scalar mask; their codes become 3 through hm.  Steps 0 .. G-2 hold every lane and are skipped.
             uint32_t W[8];
             W[0] = 0u;  // steps 0 .. G-2 are skipped: their bits are OR-ed to 3 from a defined word
+            if constexpr (VHOLD) {  // a band's first row: V - V_above + 1 until the band starts
+                const uint32_t vabove = dpp_shr1(0u, V);
+                one = ((lane & (R - 1)) == 0 && lane > 0) ? V - vabove + 1u : 1u;
+            }
+#ifdef SED_TB_DEBUG
+            const uint32_t vinit = V;
+#endif
             uint32_t tprev = dpp_shr1_add(topb[G - 1], V, one);  // diagonal of step G-1 (+1)
             uint32_t ent = 0;
-            const uint32_t *selp = selb + 64 - lane;  // lane r's selector at step sigma: selp[sigma]
+            const uint32_t *selp = selb + (VHOLD ? band * SED_CK_SELB : 0) + 64 - lane;  // lane r's selector at step sigma
             const int w_end = sig_end >> 4;
             auto step = [&](const int sig, uint32_t &wv, const uint32_t topin, const uint32_t selv) {
                 if (sig < G - 1) return;  // every lane holds
+                const int bs = ck_band_start<R>(sig);  // folds to a constant in the unrolled sweep
+                if (VHOLD && bs > 0) one = lane == R * bs ? 1u : one;  // the band starts: its first row's real delete
                 const uint32_t topv = dpp_shr1_add(topin, V, one);
                 // (selv: steps before the lane's first column read don't-care)
                 uint32_t diag = tprev;
-                const int bs = ck_band_start<R>(sig);  // folds to a constant in the unrolled sweep
                 if (bs > 0) diag = lane == R * bs ? tp : diag;
                 const uint32_t mm = umin3(V, topv, diag + __builtin_amdgcn_perm(cv, 0xFFFFFFFDu, selv));
                 const uint32_t vn = mm & ~3u;
-                const int act = ck_active_lanes<R>(sig);  // lanes 0 .. act-1 are inside their window
-                V = act >= 64 ? vn : ck_hold(vn, V, act);
+                if constexpr (VHOLD) {
+                    V = vn;
+                } else {
+                    const int act = ck_active_lanes<R>(sig);  // lanes 0 .. act-1 are inside their window
+                    V = act >= 64 ? vn : ck_hold(vn, V, act);
+                }
                 wv = __builtin_amdgcn_alignbit(mm, wv, 2);
                 tprev = topv;
             };
@@ -2148,16 +2179,16 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
             }
             ent = V;
 #ifdef SED_TB_DEBUG
-            {  // debug builds only: pair 0's first tile -> ops[0 .. 648), then stop
-                for (int w = 0; w < 8; ++w) out[w * 64 + lane] = w <= w_end ? W[w] : 0u;
-                out[512 + lane] = ent;
-                out[576 + lane] = V;
+            if (visit < 32) {  // debug builds only (pair 0; its script words, 64 spare, then 136 words per visit v)
+                uint32_t *dv = out + ((n + m + 15) >> 4) + 64 + 136 * visit;
+                dv[lane] = ent;
+                dv[64 + lane] = vinit;
                 if (lane == 0) {
-                    out[640] = (uint32_t)i; out[641] = (uint32_t)j; out[642] = (uint32_t)c; out[643] = (uint32_t)Q;
-                    out[644] = (uint32_t)k; out[645] = (uint32_t)sig_end; out[646] = (uint32_t)re; out[647] = q;
+                    dv[128] = (uint32_t)i; dv[129] = (uint32_t)j; dv[130] = (uint32_t)c; dv[131] = (uint32_t)Q;
+                    dv[132] = (uint32_t)k; dv[133] = (uint32_t)sig_end; dv[134] = (uint32_t)re; dv[135] = q;
                 }
-                return;
             }
+            ++visit;
 #endif
             // ---- the entry cell's key must carry the ops still to emit (L of a canonical-path cell) ----
             {
@@ -2189,7 +2220,11 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
         while (i > 0) { emit(1u); --i; }
         if (q != 0) err = SED_ERR_TB_LENGTH;
     }
+#ifdef SED_TB_DEBUG
+    if (lane == 0) out[((n + m + 15) >> 4) + 63] = err | ((uint32_t)visit << 8);  // (debug: no error, the dumps stay)
+#else
     if (err && lane == 0) res[pair].err = (uint8_t)err;
+#endif
 }
 
 template <int R>
@@ -2207,7 +2242,12 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
 #ifdef SED_TB_DEBUG
     if (pair != 0) return;
 #endif
-    __shared__ uint32_t topb[132], selb[64 + 132];
+    constexpr int NSEL = CkVHold<R>::value ? Grp<R>::G : 1;
+    __shared__ uint32_t topb[132], selb[NSEL * SED_CK_SELB];
+    if constexpr (NSEL > 1) {
+        for (int x = lane; x < NSEL * SED_CK_SELB; x += 64) selb[x] = SED_SEL_SENT;  // (entries below 64: before column 1)
+        __syncthreads();
+    }
     const uint32_t q0 = (uint32_t)__builtin_amdgcn_readfirstlane(res[pair].len);
     ck_traceback_pair<R, false>(d, pair, q0, lane, seqa, seqb, ck, res, ops, prm, topb, selb);
 }

@@ -114,6 +114,8 @@ struct sed_batch {
     int nparts = 1;
     hipStream_t part_stream[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_start = nullptr;
+    // per event-log entry: the {dp start, dp end, tb start, tb end} events of parts 1..3 (created on first use)
+    std::vector<std::array<hipEvent_t, 12>> plog;
     // per buffer: the event-log entry of the last run that used it (handles copied from `log`)
     std::array<hipEvent_t, 4> evk[3] = {};
     long runs = 0;
@@ -138,6 +140,9 @@ struct sed_batch {
         for (hipStream_t &ps : part_stream)
             if (ps) (void)hipStreamDestroy(ps);
         if (ev_start) (void)hipEventDestroy(ev_start);
+        for (auto &a : plog)
+            for (hipEvent_t e : a)
+                if (e) (void)hipEventDestroy(e);
         for (auto &a : log)
             for (hipEvent_t e : a)
                 if (e) (void)hipEventDestroy(e);
@@ -835,7 +840,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
 // joined at every run's end two halves ran in lockstep and gained nothing; profiles/r03/halves/, parts/).  The
 // parts share no buffer region (every pair has its own
 // checkpoints, bottom rows, script words and result), and sync_batch waits for every stream.  The run's event
-// log times part 0's kernels, one launch each (sed_batch_dp_launches() = nparts).
+// log keeps every part's kernels, one launch each: sed_batch_times reports the mean launch (sed_batch_dp_launches() =
+// nparts).
 int run_batch_parts(sed_batch *b, const std::array<hipEvent_t, 4> &lg, sed_launch L, const sed_i32_params &ip,
                     bool len) {
     sed_ctx *c = b->ctx;
@@ -847,18 +853,27 @@ int run_batch_parts(sed_batch *b, const std::array<hipEvent_t, 4> &lg, sed_launc
     if ((e = hipEventRecord(b->ev_start, c->stream)) != hipSuccess) return c->hipfail(e, "stream fork");
     for (int i = 1; i < P; ++i)
         if ((e = hipStreamWaitEvent(stream(i), b->ev_start, 0)) != hipSuccess) return c->hipfail(e, "stream fork");
-    auto part = [&](int i, hipEvent_t e0, hipEvent_t e1) {
+    // every part's kernels carry their own events (sed_batch_times averages the parts' launches)
+    const size_t li = b->nlog - 1;
+    while (b->plog.size() <= li) {
+        std::array<hipEvent_t, 12> a{};
+        for (auto &x : a)
+            if ((e = hipEventCreate(&x)) != hipSuccess) return c->hipfail(e, "event create");
+        b->plog.push_back(a);
+    }
+    const std::array<hipEvent_t, 12> &pl = b->plog[li];
+    auto part = [&](int i, int ph) {  // ph 0: forward, 1: traceback
         sed_launch Li = L;
         Li.pd = L.pd + first(i);
         Li.res = L.res + first(i);
         Li.npairs = first(i + 1) - first(i);
         Li.stream = stream(i);
-        Li.ev0 = i == 0 ? e0 : nullptr;
-        Li.ev1 = i == 0 ? e1 : nullptr;
+        Li.ev0 = i == 0 ? lg[2 * ph] : pl[4 * (i - 1) + 2 * ph];
+        Li.ev1 = i == 0 ? lg[2 * ph + 1] : pl[4 * (i - 1) + 2 * ph + 1];
         return Li;
     };
     for (int i = 0; i < P; ++i)
-        if ((e = sed_launch_i32(part(i, lg[0], lg[1]), ip, len)) != hipSuccess) return c->hipfail(e, "DP kernel launch");
+        if ((e = sed_launch_i32(part(i, 0), ip, len)) != hipSuccess) return c->hipfail(e, "DP kernel launch");
     if (b->nlane > 0) {  // lane pairs (the whole batch's, by index) after part 0's forward
         sed_launch Ll = L;
         Ll.ev0 = Ll.ev1 = nullptr;
@@ -883,7 +898,7 @@ int run_batch_parts(sed_batch *b, const std::array<hipEvent_t, 4> &lg, sed_launc
         }
     }
     for (int i = 0; i < P; ++i)
-        if ((e = sed_launch_traceback_ck(part(i, lg[2], lg[3]), (uint32_t *)b->d_ops.p, ip)) != hipSuccess)
+        if ((e = sed_launch_traceback_ck(part(i, 1), (uint32_t *)b->d_ops.p, ip)) != hipSuccess)
             return c->hipfail(e, "traceback kernel launch");
     b->evk[0] = lg;
     ++b->runs;
@@ -1307,11 +1322,25 @@ int sed_batch_times(sed_batch *b, float *dp_ms, float *tb_ms, int max_runs) {
     int rc = sync_batch(b);
     if (rc != SED_OK) return rc;
     const int cnt = (int)std::min<size_t>(b->nlog, (size_t)std::max(0, max_runs));
+    const bool script = (b->flags & SED_WANT_SCRIPT) != 0;
     for (int i = 0; i < cnt; ++i) {
         float a = 0, t = 0;
         if (hipEventElapsedTime(&a, b->log[i][0], b->log[i][1]) != hipSuccess ||
-            ((b->flags & SED_WANT_SCRIPT) && hipEventElapsedTime(&t, b->log[i][2], b->log[i][3]) != hipSuccess))
+            (script && hipEventElapsedTime(&t, b->log[i][2], b->log[i][3]) != hipSuccess))
             return b->ctx->fail(SED_E_DEVICE, "event timing");
+        if (b->nparts > 1 && (size_t)i < b->plog.size()) {  // parts: the mean launch of the run's parts
+            for (int p = 1; p < b->nparts; ++p) {
+                float ap = 0, tp = 0;
+                const std::array<hipEvent_t, 12> &pl = b->plog[i];
+                if (hipEventElapsedTime(&ap, pl[4 * (p - 1)], pl[4 * (p - 1) + 1]) != hipSuccess ||
+                    (script && hipEventElapsedTime(&tp, pl[4 * (p - 1) + 2], pl[4 * (p - 1) + 3]) != hipSuccess))
+                    return b->ctx->fail(SED_E_DEVICE, "event timing");
+                a += ap;
+                t += tp;
+            }
+            a /= b->nparts;
+            t /= b->nparts;
+        }
         if (dp_ms) dp_ms[i] = a;
         if (tb_ms) tb_ms[i] = t;
     }
