@@ -2125,7 +2125,11 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
             uint32_t W[8];
             W[0] = 0u;  // steps 0 .. G-2 are skipped: their bits are OR-ed to 3 from a defined word
             if constexpr (VHOLD) {  // a band's first row: V - V_above + 1 until the band starts
-                const uint32_t vabove = dpp_shr1(0u, V);
+                // (through the asm DPP add: with the builtin, the compiler folded V - dpp(V) into one
+                // v_subrev_u32_dpp ... bound_ctrl:1, which returned V_above - V on the device)
+                uint32_t zero = 0u;
+                asm volatile("" : "+v"(zero));
+                const uint32_t vabove = dpp_shr1_add(0u, V, zero);
                 one = ((lane & (R - 1)) == 0 && lane > 0) ? V - vabove + 1u : 1u;
             }
 #ifdef SED_TB_DEBUG
@@ -2153,6 +2157,14 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
                 }
                 wv = __builtin_amdgcn_alignbit(mm, wv, 2);
                 tprev = topv;
+#ifdef SED_TB_DEBUG_VISIT
+                if (visit == SED_TB_DEBUG_VISIT) {  // every step's keys of one visit, after the visit dumps
+                    uint32_t *ds = out + ((n + m + 15) >> 4) + 64 + 136 * 32 + 3 * 64 * sig;
+                    ds[lane] = V;
+                    ds[64 + lane] = topv;
+                    ds[128 + lane] = mm;
+                }
+#endif
             };
 #pragma unroll
             for (int w = 0; w < 8; ++w) {

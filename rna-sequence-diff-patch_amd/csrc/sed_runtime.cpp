@@ -390,6 +390,21 @@ int choose_R(int mode, int max_n, int forced) {
     return std::min(8, std::max(4, want));
 }
 
+// fp64 wave kernel: R = 4 or 8 by a cost model over the batch, not by its longest pair.  A pair costs
+// stripes(R) * (m + 63) steps of R rows plus a per-step overhead worth ~0.6 rows (fitted to the iupac workload,
+// 1024^2: R = 8 5.01 ms, R = 4 5.34 ms).  The timing workload (lengths 10..500) then takes R = 4: 4.59 against
+// 4.82 ms at R = 8 (profiles/r03/fp64_R.jsonl).
+int choose_R_f64(const int32_t *len_a, const int32_t *len_b, int npairs) {
+    double cost[2] = {0, 0};
+    for (int p = 0; p < npairs; ++p) {
+        for (int k = 0; k < 2; ++k) {
+            const int R = 4 << k;
+            cost[k] += (double)((len_a[p] + 64 * R - 1) / (64 * R)) * (len_b[p] + 63) * (R + 0.6);
+        }
+    }
+    return cost[1] < cost[0] ? 8 : 4;
+}
+
 // Event-log entries {DP start, DP end, traceback start, traceback end}, created ahead of the runs
 // that use them (outside any timed loop for up to `more` runs).
 hipError_t grow_log(sed_batch *b, size_t more) {
@@ -444,7 +459,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     case 3: mode = SED_MODE_F64_TYPED; break;
     default: mode = elig ? SED_MODE_I32 : (simple_typing(c) ? SED_MODE_F64 : SED_MODE_F64_TYPED);
     }
-    int R = choose_R(mode, max_n, c->opt_R);
+    int R = (mode == SED_MODE_I32 || c->opt_R) ? choose_R(mode, max_n, c->opt_R) : choose_R_f64(len_a, len_b, npairs);
     if (mode == SED_MODE_I32) {
         const int ROWS = 64 * R;
         bool fits = true;
@@ -459,7 +474,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         if (!fits) {
             if (c->opt_mode == 1) return c->fail(SED_E_RANGE, "integer key would overflow (D < 2^16, L < 2^14)");
             mode = simple_typing(c) ? SED_MODE_F64 : SED_MODE_F64_TYPED;
-            R = choose_R(mode, max_n, c->opt_R);
+            R = c->opt_R ? c->opt_R : choose_R_f64(len_a, len_b, npairs);
         }
     } else if (c->K > SED_MAX_K) {
         return c->fail(SED_E_ALPHABET, "alphabet of %d symbols exceeds %d", c->K, SED_MAX_K);

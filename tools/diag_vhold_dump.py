@@ -14,9 +14,9 @@ pairs = _random_pairs(900, 24, "ACGU", 1, 2600, related=True) + _random_pairs(91
 a0, b0 = pairs[31]
 assert (len(a0), len(b0)) == (208, 106), (len(a0), len(b0))
 rng = np.random.default_rng(5)
-dummy = ["".join(rng.choice(list("ACGU"), size=1000)) for _ in range(80)]
-A = [a0] + dummy[:40]
-B = [b0] + dummy[40:]
+dummy = ["".join(rng.choice(list("ACGU"), size=2000)) for _ in range(400)]
+A = [a0] + dummy[:200]
+B = [b0] + dummy[200:]
 plan = sedcost.build_plan(table, A, B)
 ctx = sedgpu.Context(0)
 ctx.set_costs(plan)
@@ -31,4 +31,6 @@ tiles = []
 for v in range(min(32, info >> 8)):
     d = w[base + 136 * v: base + 136 * (v + 1)]
     tiles.append({"ent": [int(x) for x in d[:64]], "vinit": [int(x) for x in d[64:128]], "coord": [int(x) for x in d[128:136]]})
-print(json.dumps({"lib": os.path.basename(sedgpu.LIB_PATH), "err": info & 255, "visits": info >> 8, "tiles": tiles}), flush=True)
+steps = w[base + 136 * 32: base + 136 * 32 + 3 * 64 * 127].reshape(127, 3, 64)
+print(json.dumps({"lib": os.path.basename(sedgpu.LIB_PATH), "err": info & 255, "visits": info >> 8, "tiles": tiles,
+                  "steps": [[[int(x) for x in r] for r in st] for st in steps]}), flush=True)
