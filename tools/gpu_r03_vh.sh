@@ -4,6 +4,7 @@ set -e
 O=gpurun_out/r03vh
 mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 200 python3 -u -m pytest tests/test_dist_gpu.py -m gpu -x -v --timeout 150 --timeout-method thread > $O/tests_rccl.log 2>&1; tail -2 $O/tests_rccl.log
 SED_LIBRARY=$PWD/tools/ab_libs/libsed_vhold.so timeout -k 10 500 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_routes.py -m gpu -x -v --timeout 200 --timeout-method thread > $O/tests_vhold.log 2>&1
 tail -2 $O/tests_vhold.log
 tools/ab2.sh r03vh_ab 3 tools/ab_libs/libsed_cur.so tools/ab_libs/libsed_vhold.so
