@@ -44,6 +44,8 @@ SIMDS, CLOCK = 1024, 2.4e9
 # keys (D << 16 - U carries the path length; the traceback recomputes the op tie-break): "nolen".
 VALU_CYCLES_PER_OP = 4.0
 CELL_OPS = {"script": 5 + 3 / 16, "len": 4 + 3 / 16, "nolen": 3, "nolen_x2": 2, "dot": 2}
+# the bit-parallel unit-cost lane kernel: ~15 VALU per str1 symbol for a whole row of str2 (m <= 32), from its ISA
+BITPAR_OPS_PER_ROW = 15
 
 
 def lad_ops(R):
@@ -484,6 +486,8 @@ def main():
     ap.add_argument("--no-lane", action="store_true", help="route short pairs to the wave kernels too (A/B)")
     ap.add_argument("--no-pack", action="store_true",
                     help="distance-only pairs one per lane / wave (no packed 16-bit cells; A/B)")
+    ap.add_argument("--no-bitpar", action="store_true",
+                    help="unit-cost distance-only lane pairs on the DP lane kernels instead of bit-parallel (A/B)")
     ap.add_argument("--split", type=int, default=0, help="SED_OPT_SPLIT: 0 auto, 1 force, 2 off (A/B)")
     ap.add_argument("--tb", type=int, default=0,
                     help="SED_OPT_TB: 0 auto, 1 per-cell traceback codes, 2 checkpoints + recompute (A/B)")
@@ -556,6 +560,8 @@ def main():
         ctx.set_option(sedgpu.SED_OPT_LANE, 2)
     if args.no_pack:
         ctx.set_option(sedgpu.SED_OPT_PACK, 2)
+    if args.no_bitpar:
+        ctx.set_option(sedgpu.SED_OPT_BITPAR, 2)
     if args.chain:
         ctx.set_option(sedgpu.SED_OPT_CHAIN, args.chain)
     if args.split:
@@ -669,8 +675,8 @@ def main():
     launches = batch.dp_launches
     algo_launch, design_launch, cells_launch = algo_bytes / launches, design_bytes / launches, cells / launches
     achieved = algo_launch / (dp_avg * 1e-3) / 1e9
-    nl, npk = batch.lane_pairs, batch.packed_pairs
-    lane_x2 = batch.mode == "i32" and not want_script and nl > 0 and not args.no_pack
+    nl, npk, nbp = batch.lane_pairs, batch.packed_pairs, batch.bitpar_pairs
+    lane_x2 = batch.mode == "i32" and not want_script and nl > 0 and not args.no_pack and nbp == 0
     wave_x2 = npk - (nl if lane_x2 else 0)  # wave pairs computed two per wave
     ops_cell = None
     R = batch.rows_per_lane
@@ -683,6 +689,8 @@ def main():
             ops_cell = CELL_OPS["dot" if batch.dot_keys else "nolen"]
         elif want_script:
             ops_cell = lad_ops(R) if batch.ladder_dot_keys else CELL_OPS["script"]
+        elif nbp == P:
+            ops_cell = BITPAR_OPS_PER_ROW * float(np.sum(packed.len_a[:P])) / max(cells, 1.0)
         else:
             ops_cell = CELL_OPS["nolen_x2" if npk == P else "nolen"]
     valu_peak = SIMDS * CLOCK * 64 / (VALU_CYCLES_PER_OP * ops_cell) if ops_cell else None
@@ -692,7 +700,8 @@ def main():
     else:
         wave_k = "sed_wf_i32_chain_kernel" if batch.chains else "sed_wf_i32_kernel"
         parts = ((["sed_wf_i32x2_kernel"] if wave_x2 else []) + ([wave_k] if nl + wave_x2 < P else []) +
-                 ([("sed_lane_i32x2_kernel" if lane_x2 else "sed_lane_i32_kernel")] if nl else []))
+                 ([("sed_lane_bitpar_kernel" if nbp else "sed_lane_i32x2_kernel" if lane_x2 else
+                    "sed_lane_i32_kernel")] if nl else []))
     tb_kernels = []
     if want_script and nl < P:
         tb_kernels = {2: ["sed_traceback_ck_kernel"], 3: ["sed_tb_stripemap_kernel", "sed_tb_stripeemit_kernel"],
@@ -719,7 +728,7 @@ def main():
         "vs_baseline": None, "dtype": "u32" if batch.mode == "i32" else "f64", "data": "synthetic",
         "config": {"workload": desc, "pairs_per_gpu": P, "n": n, "m": m, "costs": costs_file,
                    "script": want_script, "pipeline": pipeline and batch.traceback_mode != 2, "mode": batch.mode,
-                   "rows_per_lane": R, "lane_pairs": nl, "packed_pairs": npk,
+                   "rows_per_lane": R, "lane_pairs": nl, "packed_pairs": npk, "bitpar_pairs": nbp,
                    "chains": batch.chains, "dot_keys": batch.dot_keys, "ladder_dot_keys": batch.ladder_dot_keys,
                    "traceback": {0: None, 1: "per-cell codes", 2: "checkpoints + recompute",
                                  3: "per-cell codes, stripe-parallel walk"}[batch.traceback_mode],

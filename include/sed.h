@@ -76,6 +76,10 @@ enum {
 #define SED_OPT_DOT 10          /* checkpoint batches of the stripe kernel and CHAIN batches: 0 auto (dot keys when
                                    the cost table's update addends factor over signed bytes and the pairs fit the
                                    bound), 2 never */
+#define SED_OPT_BITPAR 11       /* distance-only batches under unit costs (insert = delete = 1, every mismatch 1): lane
+                                   pairs (m <= 32) run one per lane bit-parallel; in fp64 batches (e.g. costs.json with N)
+                                   the lane pairs whose symbols all have unit costs among themselves: 0 auto (on),
+                                   2 never */
 #define SED_OPT_DEBUG_CORRUPT 9 /* testing only: p + 1 overwrites one checkpoint word of pair p before its traceback,
                                    which must then fail with SED_E_DEVICE naming the pair; 0 off */
 
@@ -126,6 +130,7 @@ int sed_batch_rows_per_lane(const sed_batch *b);
 int sed_batch_lane_pairs(const sed_batch *b);         /* pairs on the lane-per-pair kernel (short str2) */
 int sed_batch_chains(const sed_batch *b);             /* CHAIN mode: number of chains (0 = not used) */
 int sed_batch_packed_pairs(const sed_batch *b);       /* pairs computed two per lane / wave (SED_OPT_PACK) */
+int sed_batch_bitpar_pairs(const sed_batch *b);       /* lane pairs computed bit-parallel (SED_OPT_BITPAR) */
 /* The byte factorisation behind SED_OPT_DOT, without a device (tests): for the 4 x 4 table sub (a -> b, row-major)
  * and insert/delete costs, the dot keys for pairs with min(n, m) <= maxmin (ladder_maxsum = 0) or the ladder dot
  * keys for n + m <= ladder_maxsum.  out[0..3] = row vectors, out[4..7] = column vectors (4 signed bytes each),

@@ -123,9 +123,12 @@ hipError_t sed_launch_lane_i32(const sed_launch &L, const int32_t *idx, int nidx
 hipError_t sed_launch_i32x2(const sed_launch &L, const int32_t *list, int nwaves, const sed_i32_params &prm);
 // distance only, two pairs of equal n per lane (packed 16-bit cells); idx holds 2 * nlanes pair indices
 hipError_t sed_launch_lane_i32x2(const sed_launch &L, const int32_t *idx, int nlanes, const sed_i32_params &prm);
-// fp64 distance-only lane kernel (SED_MODE_F64 with SED_NO_LEN): gtab = the {value, flag} table.
+// distance only under unit costs, one pair per lane, bit-parallel (str2 as the bit dimension, m <= 32)
+hipError_t sed_launch_lane_bitpar(const sed_launch &L, const int32_t *idx, int nidx);
+// fp64 distance-only lane kernel (SED_MODE_F64 with SED_NO_LEN): gtab = the {value, flag} table.  Pairs with
+// pd.pad[0] = 1 (every symbol in the unit-cost code set umask, at most 4 codes) run bit-parallel.
 hipError_t sed_launch_lane_f64(const sed_launch &L, const int32_t *idx, int nidx, const double *gtab, double ins,
-                               double del, int K);
+                               double del, int K, uint32_t umask);
 hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops);
 // stripe-parallel traceback of few long pairs (per-cell codes): map[pd.map_off ...] per pair, ops zeroed first
 hipError_t sed_launch_traceback_stripes(const sed_launch &L, uint32_t *ops, uint32_t *map, int items, int kmax);

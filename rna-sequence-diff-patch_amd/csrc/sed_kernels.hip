@@ -1405,6 +1405,20 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
                 if (TYPED) tnx = load_t(c + 1);
                 snx = load_sel(c + 1);
             }
+            // A chunk whose steps all have every lane inside columns 1..m runs its own loop of unmasked steps: with
+            // the masked and unmasked step in one loop, the register allocator copied the row state at the merge
+            // point after every group (~6 v_mov per cell in the ISA), as in the integer kernels.
+            if (s >= 63 && s + 63 < m) {
+                for (int g = 0; g < 64 / G; ++g, s += G) {
+#pragma unroll
+                    for (int u = 0; u < G; ++u)
+                        f64_step<R, TB, TYPED, false, FULL>(D, LK, T, rowbase, tab, dtop_prev, ltop_prev, ttop_prev,
+                                                            dbot, lbot, tbot, bsel, dch, lch, tch, sch, doutc, loutc,
+                                                            toutc, W, u, prm.ins, prm.del, tins, tdel, true, fo,
+                                                            row0 + 1, s + u - lane + 1);
+                    if constexpr (TB) store_tb(tbk + ((uint64_t)(s / G) * 64u + lane) * 4u, W);
+                }
+            } else
             for (int g = 0; g < 64 / G && s < SG; ++g, s += G) {
                 const bool full = (s >= 63) && (s + G - 1 < m);
 #pragma unroll
@@ -1955,11 +1969,12 @@ __device__ __forceinline__ uint32_t ck_walk(const uint32_t (&W)[8], uint32_t S, 
     return S & 0xFFFFu;
 }
 
-// SED_CK_VHOLD (experimental, default off): lanes left of their window hold without a select at R = 16 (per-band
-// selector copies, a compensated delete addend on each band's first row); it fails the entry check on costs.json
-// pairs, so it is kept as a switch for the debug dumps below
+// SED_CK_VHOLD (default on; -DSED_CK_VHOLD=0 restores the select): at R = 16 lanes left of their window hold
+// their key without a select (per-band selector copies carry the sentinel, and each band's first row takes a
+// compensated delete addend until its band starts).  6 VALU per swept cell instead of 7; profiles/r03/vhold:
+// traceback 3.78 against 3.91 ms beside the forward parts, step within noise
 #ifndef SED_CK_VHOLD
-#define SED_CK_VHOLD 0
+#define SED_CK_VHOLD 1
 #endif
 #define SED_CK_SELB (64 + 132)
 template <int R> struct CkVHold { static constexpr bool value = SED_CK_VHOLD && R == 16; };

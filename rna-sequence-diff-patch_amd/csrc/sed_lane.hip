@@ -224,12 +224,83 @@ __global__ __launch_bounds__(256) void sed_lane_i32x2_kernel(const sed_pair_desc
     res[Q] = r;
 }
 
+// Distance only under unit costs (insert = delete = 1, every mismatch 1: costs.json's ACGU block, config 5 and
+// the IRMethods wf_score searches), one pair per lane, bit-parallel (Myers 1999, in Hyyrö's formulation for the
+// global distance).  str2 (m <= 32) is the bit dimension: bit j-1 holds the vertical delta D[j] - D[j-1] of the
+// current row as the pair (Pv, Mv) = (+1, -1) masks; every row of str1 updates all of them with ~18 word ops,
+// and the top border's +1 per row enters as the carry-in of the shifted Ph.  Row 0 is D[j] = j (Pv all ones), so
+// the sink is D[n][m] = n + popcount(Pv) - popcount(Mv) over bits 0..m-1 (StringEditDistance.py:146-182 borders,
+// :92-128 recurrence; the values are integers, a Python int exactly when 0).  Bits at and above m hold don't-care
+// values: additions carry and shifts move only upward, so they never reach bits below m.  The match masks come
+// from two bit planes of str2's 2-bit codes: Eq = ~t with t = (E0 ^ c0) | (E1 ^ c1), c0/c1 = the row symbol's
+// bits sign-extended; Eq itself is never formed (bfi folds the complement into its uses).
+__device__ __forceinline__ uint32_t even_bits(uint32_t x) {  // bits 0, 2, .., 30 of x -> bits 0..15
+    x &= 0x55555555u;
+    x = (x | (x >> 1)) & 0x33333333u;
+    x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+    x = (x | (x >> 4)) & 0x00FF00FFu;
+    return (x | (x >> 8)) & 0x0000FFFFu;
+}
+__global__ __launch_bounds__(256) void sed_lane_bitpar_kernel(const sed_pair_desc *__restrict__ pd,
+                                                              const int32_t *__restrict__ idx, int nidx,
+                                                              const uint32_t *__restrict__ seqa,
+                                                              const uint32_t *__restrict__ seqb,
+                                                              sed_result *__restrict__ res) {
+    static_assert(SED_LANE_MAXM == 32, "str2 fits one 32-bit word of bit-parallel state");
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nidx) return;
+    const int pair = idx[t];
+    const sed_pair_desc d = pd[pair];
+    const int n = d.n, m = d.m;  // host guarantees 1 <= n <= SED_LANE_MAXN, 1 <= m <= 32
+    const uint32_t *pb = seqb + d.b_off, *pa = seqa + d.a_off;
+    const uint32_t wb0 = pb[0], wb1 = pb[1];  // (the upload pads every sequence buffer)
+    const uint32_t E0 = even_bits(wb0) | (even_bits(wb1) << 16);            // bit j: symbol j's low bit
+    const uint32_t E1 = even_bits(wb0 >> 1) | (even_bits(wb1 >> 1) << 16);  // and its high bit
+    uint32_t Pv = ~0u, Mv = 0u;
+    uint32_t wa = pa[0];
+    for (int i0 = 0; i0 < n; i0 += 16) {
+        const uint32_t w = wa;
+        if (i0 + 16 < n) wa = pa[(i0 >> 4) + 1];  // next word in flight during these 16 rows
+        const int cnt = min(16, n - i0);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            if (u >= cnt) break;
+            const uint32_t c0 = (uint32_t)__builtin_amdgcn_sbfe((int)w, 2 * u, 1);  // 0 or ~0
+            const uint32_t c1 = (uint32_t)__builtin_amdgcn_sbfe((int)w, 2 * u + 1, 1);
+            const uint32_t tq = (E0 ^ c0) | (E1 ^ c1);  // ~Eq
+            const uint32_t Xv = Mv | ~tq;
+            const uint32_t Xh = (((Pv & ~tq) + Pv) ^ Pv) | ~tq;
+            const uint32_t Ph = (Mv | ~(Xh | Pv)) << 1 | 1u;  // (the top border's +1)
+            const uint32_t Mh = (Pv & Xh) << 1;
+            Pv = Mh | ~(Xv | Ph);
+            Mv = Ph & Xv;
+        }
+    }
+    const uint32_t keep = m >= 32 ? ~0u : (1u << m) - 1u;
+    const uint32_t D = (uint32_t)n + (uint32_t)__builtin_popcount(Pv & keep) - (uint32_t)__builtin_popcount(Mv & keep);
+    sed_result r;
+    r.dist = (double)D;
+    r.len = -1;
+    r.is_int = (D == 0);
+    r.err = 0;
+    r.seq = 0;
+    res[pair] = r;
+}
+
 // fp64 distance-only variant (SED_MODE_F64 = "simple typing", SED_NO_LEN): short pairs whose
 // alphabet or costs rule out the integer keys (IUPAC codes, N in piRNA data; config 5 with N).
 // Cells follow the reference exactly: borders j*insert and i*delete are products
 // (StringEditDistance.py:146-182), each candidate is one fp64 add, the value is the minimum
 // (ties have equal values; in this mode a value is a Python int exactly when it is 0).
 // The K x K cost table sits in LDS; a lane keeps per-column byte offsets into it.
+// Pairs flagged by the host (d.pad[0]: every symbol in the unit-cost set `umask`, see sed_runtime.cpp:
+// unit_subset) take the bit-parallel recurrence of sed_lane_bitpar_kernel instead: their distance does not depend
+// on the other symbols' costs, and it is an integer, a Python int exactly when 0 (config 5 with N: the pairs
+// without N).  The host puts them first in idx, so waves are uniform but for one.
+__device__ __forceinline__ uint32_t unit_code(uint32_t c, uint32_t umask) {  // 2-bit index of code c in umask
+    return (uint32_t)__builtin_popcount(umask & ((1u << c) - 1u));
+}
+
 template <int MM>
 __global__ __launch_bounds__(256) void sed_lane_f64_kernel(const sed_pair_desc *__restrict__ pd,
                                                            const int32_t *__restrict__ idx, int nidx,
@@ -237,7 +308,7 @@ __global__ __launch_bounds__(256) void sed_lane_f64_kernel(const sed_pair_desc *
                                                            const uint8_t *__restrict__ seqb,
                                                            sed_result *__restrict__ res,
                                                            const double *__restrict__ gtab, double ins, double del,
-                                                           int K) {
+                                                           int K, uint32_t umask) {
     __shared__ double tab[SED_MAX_K * SED_MAX_K];
     for (int e = threadIdx.x; e < K * K; e += blockDim.x) tab[e] = gtab[2 * e];
     __syncthreads();
@@ -247,6 +318,35 @@ __global__ __launch_bounds__(256) void sed_lane_f64_kernel(const sed_pair_desc *
     const sed_pair_desc d = pd[pair];
     const int n = d.n, m = d.m;  // host guarantees 1 <= n <= SED_LANE_MAXN, 1 <= m <= MM
     const uint8_t *pa = seqa + d.a_off, *pb = seqb + d.b_off;
+    if (d.pad[0]) {  // unit costs over this pair's symbols: bit-parallel (sed_lane_bitpar_kernel)
+        uint32_t E0 = 0, E1 = 0;
+        for (int j = 0; j < m; ++j) {
+            const uint32_t b = unit_code(pb[j], umask);
+            E0 |= (b & 1u) << j;
+            E1 |= (b >> 1) << j;
+        }
+        uint32_t Pv = ~0u, Mv = 0u;
+        for (int i = 0; i < n; ++i) {
+            const uint32_t a = unit_code(pa[i], umask);
+            const uint32_t tq = (E0 ^ (0u - (a & 1u))) | (E1 ^ (0u - (a >> 1)));  // ~Eq
+            const uint32_t Xv = Mv | ~tq;
+            const uint32_t Xh = (((Pv & ~tq) + Pv) ^ Pv) | ~tq;
+            const uint32_t Ph = (Mv | ~(Xh | Pv)) << 1 | 1u;
+            const uint32_t Mh = (Pv & Xh) << 1;
+            Pv = Mh | ~(Xv | Ph);
+            Mv = Ph & Xv;
+        }
+        const uint32_t keep = m >= 32 ? ~0u : (1u << m) - 1u;
+        const uint32_t Dv = (uint32_t)n + (uint32_t)__builtin_popcount(Pv & keep) - (uint32_t)__builtin_popcount(Mv & keep);
+        sed_result r;
+        r.dist = (double)Dv;
+        r.len = -1;
+        r.is_int = (Dv == 0);
+        r.err = 0;
+        r.seq = 0;
+        res[pair] = r;
+        return;
+    }
     uint32_t col[MM];  // byte offset of cost(., b_j) within a table row
     double V[MM + 1];
 #pragma unroll
@@ -287,10 +387,17 @@ __global__ __launch_bounds__(256) void sed_lane_f64_kernel(const sed_pair_desc *
 }  // namespace
 
 hipError_t sed_launch_lane_f64(const sed_launch &L, const int32_t *idx, int nidx, const double *gtab, double ins,
-                               double del, int K) {
+                               double del, int K, uint32_t umask) {
     if (nidx <= 0) return hipSuccess;
     SED_LAUNCH((sed_lane_f64_kernel<SED_LANE_MAXM>), dim3((nidx + 255) / 256), dim3(256), 0, L, L.pd,
-                       idx, nidx, (const uint8_t *)L.seqa, (const uint8_t *)L.seqb, L.res, gtab, ins, del, K);
+                       idx, nidx, (const uint8_t *)L.seqa, (const uint8_t *)L.seqb, L.res, gtab, ins, del, K, umask);
+    return hipGetLastError();
+}
+
+hipError_t sed_launch_lane_bitpar(const sed_launch &L, const int32_t *idx, int nidx) {
+    if (nidx <= 0) return hipSuccess;
+    SED_LAUNCH(sed_lane_bitpar_kernel, dim3((nidx + 255) / 256), dim3(256), 0, L, L.pd, idx, nidx,
+               (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.res);
     return hipGetLastError();
 }
 

@@ -60,6 +60,7 @@ struct sed_ctx {
     // options
     int opt_mode = 0, opt_R = 0, opt_split = 0, opt_lane = 0, opt_chain = 0, opt_pack = 0, opt_tb = 0;
     int opt_chain_waves = 0;
+    int opt_bitpar = 0;         // SED_OPT_BITPAR: 0 auto (unit-cost distance-only lane pairs), 2 never
     int opt_dot = 0;            // SED_OPT_DOT: 0 auto, 2 never (checkpoint batches keep the perm-based distance keys)    // SED_OPT_CHAIN_WAVES: cap on the persistent waves of dynamic CHAIN mode
     int opt_debug_corrupt = 0;  // SED_OPT_DEBUG_CORRUPT: pair + 1 whose sink-tile checkpoint is overwritten
     DevBuf selftest;
@@ -97,6 +98,9 @@ struct sed_batch {
     bool lad = false;          // CHAIN kernel with the L field on ladder dot keys (dot_keys ladder mode)
     int nlane = 0, nwave = 0;  // pairs on the lane-per-pair kernel / on the wave kernels
     int nlane_x2 = 0;          // > 0: lane pairs run two per lane (distance only), in this many lanes
+    bool lane_bitpar = false;  // lane pairs run the bit-parallel unit-cost kernel (distance only)
+    uint32_t umask = 0;        // fp64 lane kernel: codes of the unit-cost subset; its pairs run bit-parallel
+    int nbitpar_f64 = 0;       // fp64 lane pairs flagged for it (pd.pad[0])
     int nwave_x2 = 0;          // distance-only wave pairs of equal shape run two per wave, in this many waves
     int nchains = 0;           // CHAIN mode: wave pairs run as nchains back-to-back chains (0 = off)
     size_t chain_npairs = 0;   // d_chain = [chain_pairs (chain_npairs) | chain_off (nchains + 1) | counter]
@@ -374,6 +378,40 @@ bool x2_costs_ok(const sed_ctx *c) {
     return true;
 }
 
+// Unit costs (insert = delete = 1, every mismatch 1, every match the int 0): the bit-parallel lane kernel
+// (sed_lane.hip: sed_lane_bitpar_kernel) computes exactly the reference's distance.
+bool unit_costs(const sed_ctx *c) {
+    if (c->K > 4 || c->ins_int || c->del_int || c->ins != 1.0 || c->del != 1.0) return false;
+    for (int a = 0; a < c->K; ++a)
+        for (int bb = 0; bb < c->K; ++bb) {
+            const int e = a * c->K + bb;
+            if (a == bb ? !(c->sub_int[e] && c->sub[e] == 0) : (c->sub_int[e] || c->sub[e] != 1.0)) return false;
+        }
+    return true;
+}
+
+// A set of at most 4 codes with unit costs among themselves (insert = delete = 1.0, every mismatch 1.0, every match
+// the int 0), as a bit mask, greedily in code order; 0 when insert / delete are not 1.0.  A pair whose symbols all
+// lie in it has the unit-cost distance whatever the other symbols cost (config 5 with N: the pairs without N).
+uint32_t unit_subset(const sed_ctx *c) {
+    if (c->K > SED_MAX_K || c->ins_int || c->del_int || c->ins != 1.0 || c->del != 1.0) return 0;
+    uint32_t S = 0;
+    int cnt = 0;
+    for (int a = 0; a < c->K && cnt < 4; ++a) {
+        bool ok = c->sub_int[a * c->K + a] && c->sub[a * c->K + a] == 0;
+        for (int bb = 0; bb < c->K && ok; ++bb)
+            if ((S >> bb) & 1u) {
+                const int e1 = a * c->K + bb, e2 = bb * c->K + a;
+                ok = !c->sub_int[e1] && c->sub[e1] == 1.0 && !c->sub_int[e2] && c->sub[e2] == 1.0;
+            }
+        if (ok) {
+            S |= 1u << a;
+            ++cnt;
+        }
+    }
+    return cnt >= 2 ? S : 0;
+}
+
 // "simple typing": a cell's value is an int exactly when it equals 0.
 bool simple_typing(const sed_ctx *c) {
     if (c->ins_int || c->del_int || !(c->ins > 0) || !(c->del > 0)) return false;
@@ -591,12 +629,34 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // distance-only integer lane pairs: two pairs of equal n per lane (sed_lane.hip: i32x2). Stable
     // sort by n, pair neighbours of equal n; a pair without a partner shares its lane with itself.
     b->nlane_x2 = 0;
+    // unit costs: one pair per lane, bit-parallel (~18 word ops per str1 symbol instead of 2 per cell)
+    b->lane_bitpar = mode == SED_MODE_I32 && !want_tb && (flags & SED_NO_LEN) && c->opt_bitpar != 2 &&
+                     !lane_idx.empty() && unit_costs(c);
+    // fp64 lane pairs whose symbols all lie in a unit-cost subset: bit-parallel inside the fp64 lane kernel, first
+    // in the lane list so that waves stay uniform
+    b->umask = 0;
+    b->nbitpar_f64 = 0;
+    if (mode == SED_MODE_F64 && use_lane && !want_tb && (flags & SED_NO_LEN) && c->opt_bitpar != 2 &&
+        !lane_idx.empty() && (b->umask = unit_subset(c)) != 0) {
+        auto inside = [&](const uint8_t *s, int len) {
+            for (int i = 0; i < len; ++i)
+                if (!((b->umask >> s[i]) & 1u)) return false;
+            return true;
+        };
+        for (int32_t x : lane_idx)
+            if (inside(codes_a + off_a[x], len_a[x]) && inside(codes_b + off_b[x], len_b[x])) {
+                b->pd[x].pad[0] = 1;
+                ++b->nbitpar_f64;
+            }
+        std::stable_partition(lane_idx.begin(), lane_idx.end(), [&](int32_t x) { return b->pd[x].pad[0] != 0; });
+    }
     const bool x2_ok = mode == SED_MODE_I32 && x2_costs_ok(c);
     // 16-bit offset keys: n*delete + 32*insert (the lane kernel's whole block) within 0xFFFF
     bool lane_fit16 = true;
     for (int32_t x : lane_idx)
         if ((double)len_a[x] * c->del + SED_LANE_MAXM * c->ins > 65535.0) lane_fit16 = false;
-    if (x2_ok && lane_fit16 && !want_tb && (flags & SED_NO_LEN) && c->opt_pack != 2 && !lane_idx.empty()) {
+    if (x2_ok && lane_fit16 && !b->lane_bitpar && !want_tb && (flags & SED_NO_LEN) && c->opt_pack != 2 &&
+        !lane_idx.empty()) {
         std::stable_sort(lane_idx.begin(), lane_idx.end(), [&](int32_t x, int32_t y) { return len_a[x] < len_a[y]; });
         std::vector<int32_t> two;
         two.reserve(lane_idx.size() + 1);
@@ -1007,13 +1067,15 @@ int run_batch(sed_batch *b) {
     }
     if (b->nlane > 0) {
         dp_events();
-        if (b->nlane_x2 > 0)
+        if (b->lane_bitpar)
+            e = sed_launch_lane_bitpar(L, (const int32_t *)b->d_lane.p, b->nlane);
+        else if (b->nlane_x2 > 0)
             e = sed_launch_lane_i32x2(L, (const int32_t *)b->d_lane.p, b->nlane_x2, ip);
         else if (b->mode == SED_MODE_I32)
             e = sed_launch_lane_i32(L, (const int32_t *)b->d_lane.p, b->nlane, ip, len);
         else
             e = sed_launch_lane_f64(L, (const int32_t *)b->d_lane.p, b->nlane, (const double *)c->gtab.p, c->ins,
-                                    c->del, c->K);
+                                    c->del, c->K, b->umask);
         if (e != hipSuccess) return c->hipfail(e, "lane kernel launch");
     }
     if (ndp == 0 && (e = hipEventRecord(lg[1], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
@@ -1169,6 +1231,10 @@ int sed_set_option(sed_ctx *c, int key, int value) {
         c->opt_pack = value;
         return SED_OK;
     }
+    if (key == SED_OPT_BITPAR && (value == 0 || value == 2)) {
+        c->opt_bitpar = value;
+        return SED_OK;
+    }
     if (key == SED_OPT_DOT && (value == 0 || value == 2)) {
         c->opt_dot = value;
         return SED_OK;
@@ -1302,6 +1368,10 @@ int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave)
     if (fetched) *fetched = f;
     if (max_per_wave) *max_per_wave = mx;
     return SED_OK;
+}
+
+int sed_batch_bitpar_pairs(const sed_batch *b) {
+    return b ? (b->lane_bitpar ? b->nlane : b->nbitpar_f64) : SED_E_ARG;
 }
 
 int sed_batch_packed_pairs(const sed_batch *b) {

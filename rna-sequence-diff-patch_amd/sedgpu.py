@@ -39,6 +39,7 @@ SED_OPT_TB = 7
 SED_OPT_CHAIN_WAVES = 8
 SED_OPT_DEBUG_CORRUPT = 9
 SED_OPT_DOT = 10
+SED_OPT_BITPAR = 11
 MODE_NAMES = {1: "i32", 2: "f64", 3: "f64-typed"}
 
 _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
@@ -67,6 +68,7 @@ SIGNATURES = [
     ("sed_batch_dot_keys", C.c_int, [C.c_void_p]),
     ("sed_dot_factor", C.c_int, [_f64p, C.c_double, C.c_double, C.c_int, C.c_int, _u32p]),
     ("sed_batch_packed_pairs", C.c_int, [C.c_void_p]),
+    ("sed_batch_bitpar_pairs", C.c_int, [C.c_void_p]),
     ("sed_batch_traceback_mode", C.c_int, [C.c_void_p]),
     ("sed_batch_chain_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("sed_batch_run", C.c_int, [C.c_void_p]),
@@ -311,6 +313,11 @@ class Batch:
     def packed_pairs(self):
         """Pairs computed two per lane / per wave in packed 16-bit cells (distance-only batches)."""
         return self._lib.sed_batch_packed_pairs(self.ptr)
+
+    @property
+    def bitpar_pairs(self):
+        """Lane pairs computed bit-parallel (unit costs, distance only; SED_OPT_BITPAR)."""
+        return self._lib.sed_batch_bitpar_pairs(self.ptr)
 
     def run(self):
         self.ctx._check(self._lib.sed_batch_run(self.ptr), "sed_batch_run")

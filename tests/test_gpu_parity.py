@@ -20,7 +20,8 @@ OPCH = "idu"
 IUPAC = "AGCUYRWSKMDVHBN"
 
 
-def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len=False, chain=0, pack=0, tb=0):
+def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len=False, chain=0, pack=0, tb=0,
+            bitpar=0):
     """Run (s1, s2) pairs through the engine; returns [(dist, is_int, len, opstr)]."""
     plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
     ctx.set_mode(mode)
@@ -30,6 +31,7 @@ def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len
     ctx.set_option(sedgpu.SED_OPT_CHAIN, chain)
     ctx.set_option(sedgpu.SED_OPT_PACK, pack)
     ctx.set_option(sedgpu.SED_OPT_TB, tb)
+    ctx.set_option(sedgpu.SED_OPT_BITPAR, bitpar)
     ctx.set_costs(plan)
     packed = sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs], [plan.encode(b) for _, b in pairs])
     dist, is_int, ln, ops = ctx.run(packed, script, no_len=no_len)
@@ -46,6 +48,7 @@ def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len
     ctx.set_option(sedgpu.SED_OPT_CHAIN, 0)
     ctx.set_option(sedgpu.SED_OPT_PACK, 0)
     ctx.set_option(sedgpu.SED_OPT_TB, 0)
+    ctx.set_option(sedgpu.SED_OPT_BITPAR, 0)
     return out
 
 
@@ -296,13 +299,102 @@ def test_lane_x2_packed_distance_vs_oracle(gpu, tables, user):
     pairs += [("A", "A"), ("G" * 512, "C" * 32), ("ACGU" * 128, "U"), ("C" * 511, "A" * 32)]
     plan = sedcost.build_plan(tables[user], [a for a, _ in pairs], [b for _, b in pairs])
     gpu.set_costs(plan)
+    gpu.set_option(sedgpu.SED_OPT_BITPAR, 2)  # (costs.json's unit costs would take the bit-parallel kernel)
+    try:
+        b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs],
+                                                 [plan.encode(y) for _, y in pairs]), False, no_len=True)
+        assert b.lane_pairs == len(pairs) and b.packed_pairs == len(pairs) and b.bitpar_pairs == 0
+        b.close()
+    finally:
+        gpu.set_option(sedgpu.SED_OPT_BITPAR, 0)
+    got = gpu_run(gpu, tables[user], pairs, script=False, no_len=True, bitpar=2)
+    _oracle_check(tables[user], pairs, got, no_len=True)
+    assert got == gpu_run(gpu, tables[user], pairs, script=False, no_len=True, pack=2, bitpar=2)
+
+
+def _unit_table():
+    """costs.json's ACGU block as its own table: insert = delete = 1, every mismatch 1 (unit costs)."""
+    sub = {a: {b: 1.0 for b in "ACGU"} for a in "ACGU"}
+    return {"insert": 1.0, "delete": 1.0, "update": sub}
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_lane_bitpar_unit_costs_vs_oracle(gpu, tables, seed):
+    """Unit costs (costs.json on ACGU), distance only: lane pairs (m <= 32, n <= 512) run one per lane
+    bit-parallel, mixed with wave-kernel pairs (m > 32 or n > 512).  Every ragged shape against the oracle,
+    and against the 16-bit packed lane kernel and the one-pair-per-lane DP kernel (SED_OPT_BITPAR = 2)."""
+    rng = np.random.default_rng(8080 + seed)
+    pairs = []
+    for _ in range(1500):
+        n = int(rng.choice([rng.integers(1, 17), rng.integers(15, 34), rng.integers(1, 513), rng.integers(500, 560)]))
+        m = int(rng.choice([rng.integers(1, 33), 32, 31, 1, 16, 17, 33, rng.integers(20, 60)]))
+        a = "".join(rng.choice(list("ACGU"), size=n))
+        if rng.random() < 0.4:  # related: long diagonals and ties
+            b = "".join(c if rng.random() > 0.1 else rng.choice(list("ACGU")) for c in (a * 40)[:m])
+        else:
+            b = "".join(rng.choice(list("ACGU"), size=m))
+        pairs.append((a, b))
+    pairs += [("A", "A"), ("A", "C"), ("G" * 512, "G" * 32), ("G" * 512, "C" * 32), ("ACGU" * 128, "U"),
+              ("U", "ACGU" * 8), ("C" * 511, "A" * 32), ("ACGU" * 8, "ACGU" * 8), ("A" * 513, "A" * 32)]
+    for table in (tables[False], _unit_table()):
+        plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
+        gpu.set_costs(plan)
+        b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs],
+                                                 [plan.encode(y) for _, y in pairs]), False, no_len=True)
+        lanes = b.lane_pairs
+        assert lanes > 800 and b.bitpar_pairs == lanes and b.packed_pairs < len(pairs) - lanes  # (wave pairs pack)
+        b.close()
+        got = gpu_run(gpu, table, pairs, script=False, no_len=True)
+        _oracle_check(table, pairs, got, no_len=True)
+        assert got == gpu_run(gpu, table, pairs, script=False, no_len=True, bitpar=2)
+        assert got == gpu_run(gpu, table, pairs, script=False, no_len=True, bitpar=2, pack=2)
+
+
+@pytest.mark.parametrize("alphabet,pn", [("ACGUN", 0.01), ("ACGUN", 0.2), ("AGCUYRWSKMDVHBN", 0.0)])
+def test_lane_f64_unit_subset_bitpar_vs_oracle(gpu, tables, alphabet, pn):
+    """fp64 distance-only batches (costs.json with N or IUPAC codes; config 5 with N): lane pairs whose symbols all
+    lie in a unit-cost subset of the table run bit-parallel inside the fp64 lane kernel, the others the fp64 DP.
+    Against the oracle and against SED_OPT_BITPAR = 2; the counts show both routes ran."""
+    rng = np.random.default_rng(6060 + int(100 * pn) + len(alphabet))
+    base = list(alphabet[:4]) if alphabet == "ACGUN" else list(alphabet)
+
+    def seq(k):
+        return "".join("N" if rng.random() < pn else rng.choice(base) for _ in range(k))
+    seqs = [seq(int(rng.integers(1, 33))) for _ in range(70)]
+    pairs = [(a, b) for a in seqs for b in seqs[:40]]
+    pairs += [(seq(int(rng.integers(1, 513))), seq(int(rng.integers(1, 33)))) for _ in range(200)]
+    pairs += [(seq(40), seq(40)) for _ in range(20)]  # wave-kernel pairs (m > 32)
+    table = tables[False]
+    plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
+    gpu.set_costs(plan)
     b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs],
                                              [plan.encode(y) for _, y in pairs]), False, no_len=True)
-    assert b.lane_pairs == len(pairs) and b.packed_pairs == len(pairs)
+    assert b.mode == "f64"
+    nbp, lanes = b.bitpar_pairs, b.lane_pairs
     b.close()
-    got = gpu_run(gpu, tables[user], pairs, script=False, no_len=True)
-    _oracle_check(tables[user], pairs, got, no_len=True)
-    assert got == gpu_run(gpu, tables[user], pairs, script=False, no_len=True, pack=2)
+    if alphabet == "ACGUN":
+        assert 0 < nbp < lanes or (pn == 0.2 and nbp > 0)
+    got = gpu_run(gpu, table, pairs, script=False, no_len=True)
+    _oracle_check(table, pairs, got, no_len=True)
+    assert got == gpu_run(gpu, table, pairs, script=False, no_len=True, bitpar=2)
+
+
+def test_lane_bitpar_needs_unit_costs(gpu, tables):
+    """user_costs (insert 2, delete 3), a unit table with one mismatch of cost 2, and script / length batches keep
+    the DP lane kernels."""
+    pairs = _random_pairs(99, 64, "ACGU", 1, 32)
+    off = _unit_table()
+    off["update"]["A"]["C"] = 2.0
+    for table, flags in ((tables[True], dict(script=False, no_len=True)), (off, dict(script=False, no_len=True)),
+                         (tables[False], dict(script=False)), (tables[False], dict(script=True))):
+        plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
+        gpu.set_costs(plan)
+        b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs],
+                                                 [plan.encode(y) for _, y in pairs]), flags["script"],
+                         no_len=flags.get("no_len", False))
+        assert b.lane_pairs == len(pairs) and b.bitpar_pairs == 0
+        b.close()
+        _oracle_check(table, pairs, gpu_run(gpu, table, pairs, **flags), no_len=flags.get("no_len", False))
 
 
 @pytest.mark.parametrize("R", [0, 4, 8, 16])
