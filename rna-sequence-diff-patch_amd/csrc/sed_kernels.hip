@@ -1405,20 +1405,8 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
                 if (TYPED) tnx = load_t(c + 1);
                 snx = load_sel(c + 1);
             }
-            // A chunk whose steps all have every lane inside columns 1..m runs its own loop of unmasked steps: with
-            // the masked and unmasked step in one loop, the register allocator copied the row state at the merge
-            // point after every group (~6 v_mov per cell in the ISA), as in the integer kernels.
-            if (s >= 63 && s + 63 < m) {
-                for (int g = 0; g < 64 / G; ++g, s += G) {
-#pragma unroll
-                    for (int u = 0; u < G; ++u)
-                        f64_step<R, TB, TYPED, false, FULL>(D, LK, T, rowbase, tab, dtop_prev, ltop_prev, ttop_prev,
-                                                            dbot, lbot, tbot, bsel, dch, lch, tch, sch, doutc, loutc,
-                                                            toutc, W, u, prm.ins, prm.del, tins, tdel, true, fo,
-                                                            row0 + 1, s + u - lane + 1);
-                    if constexpr (TB) store_tb(tbk + ((uint64_t)(s / G) * 64u + lane) * 4u, W);
-                }
-            } else
+            // (A separate loop for chunks of unmasked steps, as in the integer kernels, measured slower: iupac DP
+            // 4.89 against 4.81 ms, timing 4.60 against 4.47 ms; profiles/r03/f64_plain_dropped.)
             for (int g = 0; g < 64 / G && s < SG; ++g, s += G) {
                 const bool full = (s >= 63) && (s + G - 1 < m);
 #pragma unroll
