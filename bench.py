@@ -481,7 +481,8 @@ def main():
     ap.add_argument("--shape", default="", help="override the pair shape NxM (experiments; fixed-shape workloads)")
     ap.add_argument("--no-script", action="store_true", help="distance only (no traceback)")
     ap.add_argument("--no-pipeline", action="store_true",
-                    help="run DP and traceback back to back on one stream (no overlap across steps)")
+                    help="no overlap across steps: script batches run DP and traceback back to back on one stream, "
+                         "lane batches every step's kernel on one stream")
     ap.add_argument("--rows-per-lane", type=int, default=0)
     ap.add_argument("--no-lane", action="store_true", help="route short pairs to the wave kernels too (A/B)")
     ap.add_argument("--no-pack", action="store_true",
@@ -570,7 +571,7 @@ def main():
         ctx.set_option(sedgpu.SED_OPT_TB, args.tb)
     ctx.set_costs(plan)
     t0 = time.perf_counter()
-    pipeline = want_script and not args.no_pipeline
+    pipeline = not args.no_pipeline  # script batches: traceback(k) beside DP(k+1); lane batches: DP(k+1) beside DP(k)
     batch = sedgpu.Batch(ctx, packed, want_script, pipeline=pipeline, no_len=not want_script)
     log("rank %d: batch resident in %.1fs (mode %s, R=%d)" % (rank, time.perf_counter() - t0, batch.mode,
                                                              batch.rows_per_lane))

@@ -123,7 +123,15 @@ struct sed_batch {
     // per buffer: the event-log entry of the last run that used it (handles copied from `log`)
     std::array<hipEvent_t, 4> evk[3] = {};
     long runs = 0;
-    long chain_launches = 0;   // dynamic-CHAIN launches since the fill (the device counter's base)
+    // dynamic-CHAIN launches since the fill per buffer slot: each slot has its own device counter, whose base is
+    // slot launches x (list + waves)
+    long chain_launches[3] = {0, 0, 0};
+    // pipelined batches whose runs share no scratch (dynamic-CHAIN script batches, distance-only batches of lane
+    // pairs): odd runs' DP on dp2_stream, so run k+1's kernels fill the tail of run k's (CHAIN: persistent waves;
+    // lane kernels: the launch gap).  CHAIN slots have their own counters; a slot's runs are ordered through the
+    // wait of buffer reuse (run_batch)
+    bool alt_dp = false;
+    hipStream_t dp2_stream = nullptr;
     bool ran = false;
     // per-run event log (sed_batch_times): {dp start, dp end, tb start, tb end}
     std::vector<std::array<hipEvent_t, 4>> log;
@@ -141,6 +149,7 @@ struct sed_batch {
             d_res[i].release();
         }
         if (tb_stream) (void)hipStreamDestroy(tb_stream);
+        if (dp2_stream) (void)hipStreamDestroy(dp2_stream);
         for (hipStream_t &ps : part_stream)
             if (ps) (void)hipStreamDestroy(ps);
         if (ev_start) (void)hipEventDestroy(ev_start);
@@ -464,13 +473,15 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     if (!c->have_costs) return c->fail(SED_E_STATE, "sed_set_costs() was not called");
     for (hipStream_t ps : b->part_stream)  // (a refill must not overwrite a running part)
         if (ps) (void)hipStreamSynchronize(ps);
+    if (b->dp2_stream) (void)hipStreamSynchronize(b->dp2_stream);
+    if (b->tb_stream) (void)hipStreamSynchronize(b->tb_stream);
     if (npairs < 0 || (npairs > 0 && (!codes_a || !off_a || !len_a || !codes_b || !off_b || !len_b)))
         return c->fail(SED_E_ARG, "bad batch arguments");
     b->npairs = npairs;
     b->flags = flags;
     b->ran = false;
     b->runs = 0;
-    b->chain_launches = 0;
+    b->chain_launches[0] = b->chain_launches[1] = b->chain_launches[2] = 0;
     b->nbuf = (flags & SED_PIPELINE) ? 3 : 1;
     b->n.assign(len_a, len_a + npairs);
     b->m.assign(len_b, len_b + npairs);
@@ -773,7 +784,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
                    b->d_bnd.reserve(4 * std::max<uint64_t>(1, bndw)) &&
                    b->d_tasks.reserve(sizeof(int2) * std::max<size_t>(1, tasks.size())) &&
                    b->d_lane.reserve(4 * std::max<size_t>(1, lane_idx.size())) &&
-                   b->d_chain.reserve(4 * (chain_pairs.size() + chain_off.size() + 2)) &&
+                   b->d_chain.reserve(4 * (chain_pairs.size() + chain_off.size() + 4)) &&
                    b->d_x2.reserve(4 * std::max<size_t>(1, x2.size())) &&
                    b->d_tbmap.reserve(4 * std::max<uint64_t>(1, mapw));
     for (int i = 0; i < b->nbuf && okalloc; ++i)
@@ -893,6 +904,14 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     if (b->nbuf > 1 && !b->tb_stream &&
         (e = hipStreamCreateWithFlags(&b->tb_stream, hipStreamNonBlocking)) != hipSuccess)
         return c->hipfail(e, "traceback stream");
+    // SED_ALT_DP=0 keeps every DP on the context's stream (A/B)
+    static const int alt_env = [] { const char *e = getenv("SED_ALT_DP"); return e ? atoi(e) : 1; }();
+    b->alt_dp = alt_env != 0 && b->nbuf > 1 &&
+                ((b->chain_dyn && (flags & SED_WANT_SCRIPT)) ||
+                 (b->nwave == 0 && b->nwave_x2 == 0 && !(flags & SED_WANT_SCRIPT)));
+    if (b->alt_dp && !b->dp2_stream &&
+        (e = hipStreamCreateWithFlags(&b->dp2_stream, hipStreamNonBlocking)) != hipSuccess)
+        return c->hipfail(e, "second DP stream");
     // SED_CK_HALVES: parts per checkpoint batch of >= 1024 wave pairs per part (1 = off; default
     // SED_CK_HALVES_DEFAULT; at most 4, the hardware queues a process gets)
     static const int parts_env = [] { const char *e = getenv("SED_CK_HALVES"); return e ? atoi(e) : -1; }();
@@ -994,6 +1013,7 @@ int run_batch(sed_batch *b) {
     if (b->nlog == b->log.size() && (e = grow_log(b, 64)) != hipSuccess) return c->hipfail(e, "event create");
     const std::array<hipEvent_t, 4> lg = b->log[b->nlog++];
     hipStream_t ts = b->nbuf > 1 ? b->tb_stream : c->stream;
+    const hipStream_t ds = b->alt_dp && (b->runs & 1) ? b->dp2_stream : c->stream;  // this run's DP stream
     sed_launch L{};
     L.pd = (const sed_pair_desc *)b->d_pd.p;
     L.npairs = b->npairs;
@@ -1004,15 +1024,16 @@ int run_batch(sed_batch *b) {
     L.bnd = (uint32_t *)b->d_bnd.p;
     L.res = (sed_result *)b->d_res[k].p;
     L.R = b->R;
-    L.stream = c->stream;
+    L.stream = ds;
     L.tb_ladder = b->mode == SED_MODE_I32;
     L.ck = b->ck;
     L.tasks = b->split ? (const int2 *)b->d_tasks.p : nullptr;
     L.ntasks = b->split ? b->ntasks : 0;
-    // buffer k was last read by the traceback of run runs-3: wait for it unless it has finished already (a
-    // cross-queue wait is a barrier packet between this run's kernel and the previous one)
-    if (b->nbuf > 1 && want_tb && b->runs >= b->nbuf && hipEventQuery(b->evk[k][3]) != hipSuccess &&
-        (e = hipStreamWaitEvent(c->stream, b->evk[k][3], 0)) != hipSuccess)
+    // buffer k was last read by the traceback of run runs-3 (written by its DP, distance only): wait for it unless it
+    // has finished already (a cross-queue wait is a barrier packet between this run's kernel and the previous one)
+    const int kev = want_tb ? 3 : 1;
+    if (b->nbuf > 1 && (want_tb || b->alt_dp) && b->runs >= b->nbuf && hipEventQuery(b->evk[k][kev]) != hipSuccess &&
+        (e = hipStreamWaitEvent(ds, b->evk[k][kev], 0)) != hipSuccess)
         return c->hipfail(e, "stream wait");
     // The event log's timestamps ride on the kernels' own dispatch packets (SED_LAUNCH: the DP phase's first
     // kernel records lg[0] at its start and its last kernel lg[1] at its end; the same for the traceback phase
@@ -1026,14 +1047,14 @@ int run_batch(sed_batch *b) {
         L.ev1 = idp == ndp - 1 ? lg[1] : nullptr;
         ++idp;
     };
-    if (ndp == 0 && (e = hipEventRecord(lg[0], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
+    if (ndp == 0 && (e = hipEventRecord(lg[0], ds)) != hipSuccess) return c->hipfail(e, "event record");
     // SPLIT hand-off words carry the run's epoch (1..32767), so the buffer is zeroed only on a batch's first run
     // (runs restarts at 0 on every fill) and when the epoch wraps; every kernel writes all result fields, err
     // included
     sed_i32_params ip = b->ip;
     ip.epoch = (uint32_t)(b->runs % 32767u) + 1u;
     if (b->split && b->bnd_words && ip.epoch == 1 &&
-        (e = hipMemsetAsync(b->d_bnd.p, 0, 4 * b->bnd_words, c->stream)) != hipSuccess)
+        (e = hipMemsetAsync(b->d_bnd.p, 0, 4 * b->bnd_words, ds)) != hipSuccess)
         return c->hipfail(e, "memset hand-off words");
     const bool len = want_tb || !(b->flags & SED_NO_LEN);
     if (b->nparts > 1 && want_tb) return run_batch_parts(b, lg, L, ip, len);
@@ -1052,13 +1073,13 @@ int run_batch(sed_batch *b) {
             L.chain_counter = nullptr;
             if (b->chain_dyn) {  // zeroed on a batch's first launch only: a launch takes list + waves values
                 // (counted per launch, not per run: a run that fails after its CHAIN launch has still advanced it)
-                L.chain_counter = (uint32_t *)b->d_chain.p + b->chain_npairs + 1;
-                L.chain_base = (uint32_t)((uint64_t)b->chain_launches * (uint64_t)(b->chain_npairs + b->nchains));
-                if (b->chain_launches == 0 && (e = hipMemsetAsync(L.chain_counter, 0, 4, c->stream)) != hipSuccess)
+                L.chain_counter = (uint32_t *)b->d_chain.p + b->chain_npairs + 1 + k;
+                L.chain_base = (uint32_t)((uint64_t)b->chain_launches[k] * (uint64_t)(b->chain_npairs + b->nchains));
+                if (b->chain_launches[k] == 0 && (e = hipMemsetAsync(L.chain_counter, 0, 4, ds)) != hipSuccess)
                     return c->hipfail(e, "reset chain counter");
             }
             e = sed_launch_i32_chain(L, ip, len);
-            if (e == hipSuccess && b->chain_dyn) ++b->chain_launches;
+            if (e == hipSuccess && b->chain_dyn) ++b->chain_launches[k];
         } else if (b->mode == SED_MODE_I32)
             e = sed_launch_i32(L, ip, len);
         else
@@ -1078,7 +1099,7 @@ int run_batch(sed_batch *b) {
                                     c->del, c->K, b->umask);
         if (e != hipSuccess) return c->hipfail(e, "lane kernel launch");
     }
-    if (ndp == 0 && (e = hipEventRecord(lg[1], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
+    if (ndp == 0 && (e = hipEventRecord(lg[1], ds)) != hipSuccess) return c->hipfail(e, "event record");
     L.ev0 = L.ev1 = nullptr;
     if (want_tb && b->ck && c->opt_debug_corrupt > 0 && c->opt_debug_corrupt <= b->npairs) {
         // SED_OPT_DEBUG_CORRUPT: overwrite the column checkpoint of the sink's row in the chunk before the
@@ -1093,14 +1114,14 @@ int run_batch(sed_batch *b) {
             if (cs >= 1) {
                 uint32_t *w = (uint32_t *)b->d_tb[k].p + d.tb_off + sed_ck_col_word(R, nstripes - 1, nchunks, cs - 1, r, t);
                 // (dot keys are maximised: the largest key there instead)
-                if ((e = hipMemsetD32Async((hipDeviceptr_t)w, b->dot ? 0x3FFFFFFFu : 0x0000FFFCu, 1, c->stream)) !=
+                if ((e = hipMemsetD32Async((hipDeviceptr_t)w, b->dot ? 0x3FFFFFFFu : 0x0000FFFCu, 1, ds)) !=
                     hipSuccess)
                     return c->hipfail(e, "debug corrupt");
             }
         }
     }
     if (want_tb) {
-        if (ts != c->stream && (e = hipStreamWaitEvent(ts, lg[1], 0)) != hipSuccess) return c->hipfail(e, "stream wait");
+        if (ts != ds && (e = hipStreamWaitEvent(ts, lg[1], 0)) != hipSuccess) return c->hipfail(e, "stream wait");
         if (b->nwave == 0 && (e = hipEventRecord(lg[2], ts)) != hipSuccess) return c->hipfail(e, "event record");
         if (b->nwave > 0) {
             L.stream = ts;
@@ -1127,6 +1148,7 @@ int sync_batch(sed_batch *b) {
     sed_ctx *c = b->ctx;
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess && b->tb_stream) e = hipStreamSynchronize(b->tb_stream);
+    if (e == hipSuccess && b->dp2_stream) e = hipStreamSynchronize(b->dp2_stream);
     for (hipStream_t ps : b->part_stream)
         if (e == hipSuccess && ps) e = hipStreamSynchronize(ps);
     return e == hipSuccess ? SED_OK : c->hipfail(e, "kernel execution");
@@ -1349,13 +1371,14 @@ int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave)
     int32_t f = 0, mx = 0;
     if (b->nchains > 0 && b->npairs > 0) {
         hipError_t e;
-        if (b->chain_dyn && b->chain_launches > 0) {  // every persistent wave ends with one failed grab: a run takes list + waves
+        const int kk = (int)((b->runs + b->nbuf - 1) % b->nbuf);  // the last run's slot
+        if (b->chain_dyn && b->chain_launches[kk] > 0) {  // every persistent wave ends with one failed grab: a run takes list + waves
             uint32_t cnt = 0;
-            if ((e = hipMemcpy(&cnt, (uint32_t *)b->d_chain.p + b->chain_npairs + 1, 4, hipMemcpyDeviceToHost)) !=
+            if ((e = hipMemcpy(&cnt, (uint32_t *)b->d_chain.p + b->chain_npairs + 1 + kk, 4, hipMemcpyDeviceToHost)) !=
                 hipSuccess)
                 return c->hipfail(e, "download chain counter");
             const uint32_t base =
-                (uint32_t)((uint64_t)(b->chain_launches - 1) * (uint64_t)(b->chain_npairs + b->nchains));
+                (uint32_t)((uint64_t)(b->chain_launches[kk] - 1) * (uint64_t)(b->chain_npairs + b->nchains));
             f = (int32_t)(cnt - base) - b->nchains;
         }
         std::vector<sed_result> h(b->npairs);

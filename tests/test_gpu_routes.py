@@ -66,6 +66,46 @@ def _batch_run(ctx, packed, script, no_len=False, pipeline=False, runs=1):
         raise
 
 
+def test_dynamic_chain_pipelined_two_dp_streams(gpu, tables):
+    """A pipelined dynamic-CHAIN script batch (config 3's route) runs odd runs' DP on a second stream, so a run's
+    persistent waves start in the previous run's tail; each buffer slot has its own device counter.  Seven runs
+    (every slot reused, both streams, counters past their first base), every pair of the last run against the
+    oracle, and the counter accounting of the last run."""
+    A, B = _ragged(4242, 12000, 1, 512, 1, 700)
+    plan = _plan(tables[False])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs(A, B)
+    b, (d, ii, ln, ops) = _batch_run(gpu, packed, True, pipeline=True, runs=7)
+    try:
+        assert b.rows_per_lane == 8 and b.chains == 5120 and b.traceback_mode == 1
+        fetched, per_wave = b.chain_stats()
+        assert fetched == packed.npairs - b.lane_pairs and per_wave >= 2, (fetched, per_wave)
+    finally:
+        b.close()
+    _check_all(plan, packed, d, ii, ln, ops, script=True)
+
+
+@pytest.mark.parametrize("alphabet", ["ACGU", "ACGUN"])
+def test_lane_batches_pipelined_on_two_streams(gpu, tables, alphabet):
+    """Distance-only batches of lane pairs (config 5: bit-parallel; with N: the fp64 lane kernel) pipelined: odd runs
+    on a second stream beside the previous run, three result buffers.  Five runs, every pair of the last one
+    against the oracle (ACGUN exercises the fp64 mode, costs.json)."""
+    rng = np.random.default_rng(777 + len(alphabet))
+    seqs = ["".join(rng.choice(list(alphabet), p=None if alphabet == "ACGU" else [0.2475] * 4 + [0.01],
+                               size=int(rng.integers(20, 33)))) for _ in range(120)]
+    pairs = [(a, b) for a in seqs for b in seqs]
+    plan = sedcost.build_plan(tables[False], [a for a, _ in pairs], [b for _, b in pairs])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs], [plan.encode(b) for _, b in pairs])
+    b, (d, ii, ln, ops) = _batch_run(gpu, packed, False, no_len=True, pipeline=True, runs=5)
+    try:
+        assert b.lane_pairs == len(pairs) and b.bitpar_pairs > 0
+        assert b.mode == ("i32" if alphabet == "ACGU" else "f64")
+    finally:
+        b.close()
+    _check_all(plan, packed, d, ii, ln, ops, script=False, no_len=True)
+
+
 @pytest.mark.parametrize("user", [False, True])
 def test_dynamic_chain_config3_route(gpu, tables, user):
     """12 000 ragged single-stripe pairs (n 1..512, m 1..700): more than twice the 5120 resident waves, so
