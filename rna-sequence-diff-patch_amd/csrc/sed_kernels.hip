@@ -2407,7 +2407,7 @@ hipError_t sed_launch_f64(const sed_launch &L, const double *gtab, const sed_f64
         if (typed) return tb ? launch_f64_R<RR, true, true>(L, gtab, prm)                           \
                              : launch_f64_R<RR, false, true>(L, gtab, prm);                         \
         return tb ? launch_f64_R<RR, true, false>(L, gtab, prm) : launch_f64_R<RR, false, false>(L, gtab, prm);
-        CASE(4) CASE(8)
+        CASE(4) CASE(8)  // (R = 16: 206 VGPRs, 2 waves per SIMD, iupac 5.22-5.25 against 5.04-5.06 ms at R = 8)
 #undef CASE
     default: return hipErrorInvalidValue;
     }
