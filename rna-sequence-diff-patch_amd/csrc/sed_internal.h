@@ -150,7 +150,7 @@ __host__ __device__ inline uint64_t sed_ck_col_words(int R, int nstripes, int nc
 // served a two-pairs-per-wave traceback of 32-row tiles, measured and dropped in round 3: the forward kernel took
 // 9.87 instead of 9.18-9.32 ms and that traceback 2.43 instead of 2.20 ms (profiles/r03/ab_tb_tiles.jsonl).
 #ifndef SED_CK_HALVES_DEFAULT
-#define SED_CK_HALVES_DEFAULT 3  // checkpoint batches: parts on as many streams, >= 1024 wave pairs each (sed_runtime.cpp)
+#define SED_CK_HALVES_DEFAULT 2  // checkpoint batches: parts on as many streams, >= 1024 wave pairs each (sed_runtime.cpp)
 #endif
 #ifndef SED_CK_TILE
 #define SED_CK_TILE 64

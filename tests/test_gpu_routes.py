@@ -284,7 +284,7 @@ def test_checkpoint_traceback_reports_a_corrupt_checkpoint(gpu, tables):
 
 
 def test_checkpoint_parts_on_streams(gpu, tables):
-    """A checkpoint batch of >= 2048 wave pairs runs in parts on as many streams (SED_CK_HALVES, default 3 parts of
+    """A checkpoint batch of >= 2048 wave pairs runs in parts on as many streams (SED_CK_HALVES, default 2 parts of
     >= 1024 wave pairs: one part's traceback beside another part's forward, no join between runs).  3100 ragged wave
     pairs plus 101 lane-kernel pairs, shuffled (an odd count): three runs back to back, every pair vs the oracle;
     then a corrupted checkpoint of a last-part pair fails the run naming that pair, and the next run is right
@@ -302,7 +302,7 @@ def test_checkpoint_parts_on_streams(gpu, tables):
     try:
         b, (d, ii, ln, ops) = _batch_run(gpu, packed, True, runs=3)
         try:
-            assert b.traceback_mode == 2 and b.dp_launches == 3 and b.lane_pairs == 101
+            assert b.traceback_mode == 2 and b.dp_launches == 2 and b.lane_pairs == 101
         finally:
             b.close()
         _check_all(plan, packed, d, ii, ln, ops)
