@@ -11,18 +11,20 @@ table = json.load(open(os.path.join(REPO, "tests", "golden", "costs.json")))
 plan = sedcost.build_plan(table, [synth.ALPHABET], [synth.ALPHABET])
 ctx = sedgpu.Context(0)
 ctx.set_costs(plan)
-b = sedgpu.Batch(ctx, sedgpu.PackedPairs(qa, qb), False, no_len=True)
-for _ in range(5):
-    b.run()
-b.sync()
-for n in (10, 100, 400):
-    b.reset_times()
-    t0 = time.perf_counter()
-    for _ in range(n):
+for pipeline in (False, True):  # True: three result buffers, odd runs on a second stream
+    b = sedgpu.Batch(ctx, sedgpu.PackedPairs(qa, qb), False, no_len=True, pipeline=pipeline)
+    for _ in range(5):
         b.run()
-    t1 = time.perf_counter()
     b.sync()
-    t2 = time.perf_counter()
-    dp, _ = b.times()
-    print("runs %4d  enqueue %.1f us/run  total %.1f us/run  kernel %.1f us" %
-          (n, (t1 - t0) / n * 1e6, (t2 - t0) / n * 1e6, float(np.mean(dp)) * 1e3), flush=True)
+    for n in (10, 100, 400):
+        b.reset_times()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            b.run()
+        t1 = time.perf_counter()
+        b.sync()
+        t2 = time.perf_counter()
+        dp, _ = b.times()
+        print("pipeline %d runs %4d  enqueue %.1f us/run  total %.1f us/run  kernel %.1f us" %
+              (pipeline, n, (t1 - t0) / n * 1e6, (t2 - t0) / n * 1e6, float(np.mean(dp)) * 1e3), flush=True)
+    b.close()
