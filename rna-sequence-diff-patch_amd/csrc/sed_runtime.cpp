@@ -931,6 +931,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
 // traceback(part i).  The other streams start each run after stream 0's previous work, and nothing joins the
 // streams at a run's end, so the parts settle into a stagger: one part's traceback runs beside another part's
 // forward (config 4: 11.42-11.47 ms in one part, 10.85-11.0 in two, 10.77-10.83 in three, 11.6-11.8 in four;
+// with the select-free hold 9.86-9.93 in two against 10.30-10.54 in three, profiles/r03/parts2/;
 // joined at every run's end two halves ran in lockstep and gained nothing; profiles/r03/halves/, parts/).  The
 // parts share no buffer region (every pair has its own
 // checkpoints, bottom rows, script words and result), and sync_batch waits for every stream.  The run's event
