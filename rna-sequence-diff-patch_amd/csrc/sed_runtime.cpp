@@ -912,6 +912,9 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     if (b->alt_dp && !b->dp2_stream &&
         (e = hipStreamCreateWithFlags(&b->dp2_stream, hipStreamNonBlocking)) != hipSuccess)
         return c->hipfail(e, "second DP stream");
+    // distance-only lane batches on two streams use two result slots, one per stream: a slot's runs are then
+    // ordered by their stream and need no event query or cross-stream wait
+    if (b->alt_dp && !(flags & SED_WANT_SCRIPT)) b->nbuf = 2;
     // SED_CK_HALVES: parts per checkpoint batch of >= 1024 wave pairs per part (1 = off; default
     // SED_CK_HALVES_DEFAULT; at most 4, the hardware queues a process gets)
     static const int parts_env = [] { const char *e = getenv("SED_CK_HALVES"); return e ? atoi(e) : -1; }();
@@ -1033,7 +1036,8 @@ int run_batch(sed_batch *b) {
     // buffer k was last read by the traceback of run runs-3 (written by its DP, distance only): wait for it unless it
     // has finished already (a cross-queue wait is a barrier packet between this run's kernel and the previous one)
     const int kev = want_tb ? 3 : 1;
-    if (b->nbuf > 1 && (want_tb || b->alt_dp) && b->runs >= b->nbuf && hipEventQuery(b->evk[k][kev]) != hipSuccess &&
+    if (b->nbuf > 1 && (want_tb || (b->alt_dp && b->nbuf != 2)) && b->runs >= b->nbuf &&
+        hipEventQuery(b->evk[k][kev]) != hipSuccess &&
         (e = hipStreamWaitEvent(ds, b->evk[k][kev], 0)) != hipSuccess)
         return c->hipfail(e, "stream wait");
     // The event log's timestamps ride on the kernels' own dispatch packets (SED_LAUNCH: the DP phase's first
