@@ -43,6 +43,9 @@ SIMDS, CLOCK = 1024, 2.4e9
 # keys: perm + pk_add + 2 pk_min per 2 cells.  Checkpoint script batches (traceback mode 2) run the distance
 # keys (D << 16 - U carries the path length; the traceback recomputes the op tie-break): "nolen".
 VALU_CYCLES_PER_OP = 4.0
+# the dot-key cell (v_dot4_i32_i8 + v_max3_u32) measures 4.50-4.75 cycles per op in its dependent row
+# (profiles/r02_dot/ubench_valu_dot.txt: 72-75 cycles for 8 dot + 8 max): the model takes 4.5
+VALU_CYCLES_DOT = 4.5
 CELL_OPS = {"script": 5 + 3 / 16, "len": 4 + 3 / 16, "nolen": 3, "nolen_x2": 2, "dot": 2}
 # the bit-parallel unit-cost lane kernel: ~15 VALU per str1 symbol for a whole row of str2 (m <= 32), from its ISA
 BITPAR_OPS_PER_ROW = 15
@@ -320,6 +323,21 @@ def s8d_bytes(len_a, len_b, script):
     return float(per_pair.sum())
 
 
+def interval_union(iv):
+    """Total length of the union of intervals [(start, end), ...] (ms)."""
+    tot, cur_s, cur_e = 0.0, None, None
+    for s, e in sorted((float(a), float(b)) for a, b in iv if b > a):
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                tot += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        tot += cur_e - cur_s
+    return tot
+
+
 def launcher_cmd(n, argv, port):
     """The torch.distributed.run command bench.py starts for itself when run as `bench.py --gpus N` (N > 1)
     outside a launcher: one rank per GPU on this node, rendezvous on 127.0.0.1."""
@@ -590,6 +608,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     dp_ms, tb_ms = batch.times()
+    spans = batch.spans()  # [steps, parts, {dp start, dp end, tb start, tb end}] from HIP events
     cells_all = cells
     if dist is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
@@ -670,12 +689,16 @@ def main():
             dist.destroy_process_group()
         return
     dp_avg = float(np.mean(dp_ms))
-    # a checkpoint batch of >= 2048 pairs runs in parts on as many streams (SED_CK_HALVES): the run times are the
-    # mean launch over the parts, so bytes and cells are per launch too; the launches overlap each other's kernels,
-    # so frac_step (the whole step's bytes over the step time) is the aggregate
+    # A checkpoint batch of >= 2048 pairs runs in parts on as many streams (SED_CK_HALVES), and pipelined batches
+    # put consecutive runs' DP kernels on two streams: launches overlap.  The roofline therefore divides a step's
+    # bytes and cells by the DP kernels' busy time per step, the union of every DP launch's event interval over the
+    # timed steps / steps (<= ms_per_step).  The mean launch (what a rocprofv3 kernel trace averages) and the
+    # per-launch fraction it gives are kept beside it.
     launches = batch.dp_launches
     algo_launch, design_launch, cells_launch = algo_bytes / launches, design_bytes / launches, cells / launches
-    achieved = algo_launch / (dp_avg * 1e-3) / 1e9
+    dp_busy = interval_union([(s[0], s[1]) for run in spans for s in run]) / max(1, len(spans))
+    achieved = algo_bytes / (dp_busy * 1e-3) / 1e9
+    achieved_launch = algo_launch / (dp_avg * 1e-3) / 1e9
     nl, npk, nbp = batch.lane_pairs, batch.packed_pairs, batch.bitpar_pairs
     lane_x2 = batch.mode == "i32" and not want_script and nl > 0 and not args.no_pack and nbp == 0
     wave_x2 = npk - (nl if lane_x2 else 0)  # wave pairs computed two per wave
@@ -694,8 +717,10 @@ def main():
             ops_cell = BITPAR_OPS_PER_ROW * float(np.sum(packed.len_a[:P])) / max(cells, 1.0)
         else:
             ops_cell = CELL_OPS["nolen_x2" if npk == P else "nolen"]
-    valu_peak = SIMDS * CLOCK * 64 / (VALU_CYCLES_PER_OP * ops_cell) if ops_cell else None
-    rate = cells_launch / (dp_avg * 1e-3)
+    dot_cell = batch.mode == "i32" and want_script and batch.traceback_mode == 2 and batch.dot_keys
+    cyc = VALU_CYCLES_DOT if dot_cell else VALU_CYCLES_PER_OP
+    valu_peak = SIMDS * CLOCK * 64 / (cyc * ops_cell) if ops_cell else None
+    rate = cells / (dp_busy * 1e-3)
     if batch.mode != "i32":
         parts = (["sed_wf_f64_kernel"] if nl < P else []) + (["sed_lane_f64_kernel"] if nl else [])
     else:
@@ -734,20 +759,32 @@ def main():
                    "traceback": {0: None, 1: "per-cell codes", 2: "checkpoints + recompute",
                                  3: "per-cell codes, stripe-parallel walk"}[batch.traceback_mode],
                    "parallelism": "dp%d" % world, "env": env},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": kname, "kernel_ms": dp_avg, "launches_per_step": launches,
-                     "algo_bytes_per_launch": algo_launch,
+        # the kernels issue VALU on most cycles and move a fraction of the HBM peak: "bound" names the VALU; the
+        # HBM figures are the roofline the north star asks for (SURVEY.md 8(d) bytes), "valu" the binding one
+        "roofline": {"bound": "valu", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "time_basis": "DP kernels' busy time per step: union of every DP launch's HIP-event interval "
+                                   "over the timed steps / steps",
+                     "traffic": None if traffic is None else traffic * launches,
+                     "traffic_per_launch": traffic,
+                     "traffic_frac": None if traffic is None else
+                     traffic * launches / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "traffic_source": traffic_src,
+                     "kernel": kname, "kernel_ms_per_step": dp_busy, "kernel_ms_mean_launch": dp_avg,
+                     "launches_per_step": launches,
+                     "algo_bytes_per_step": algo_bytes, "algo_bytes_per_launch": algo_launch,
                      "algo_bytes_def": "SURVEY.md 8(d): per pair (n+m)/4 in + 8 out" +
                                        (" + 0.25 B/cell traceback + (n+m) reads + (n+m)/4 ops out" if want_script
                                         else ""),
+                     "frac_per_launch_overlapped": achieved_launch / HBM_PEAK_GBS,
                      "frac_step": algo_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "design_bytes_per_launch": design_launch,
-                     "design_frac": design_launch / (dp_avg * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                     "design_bytes_per_step": design_bytes,
+                     "design_frac": design_bytes / (dp_busy * 1e-3) / 1e9 / HBM_PEAK_GBS},
         "valu": None if valu_peak is None else {
-            "model": "%.4g VALU ops/cell x %.1f cycles/op per wave64 (tools/ubench/valu_row.hip), 1024 SIMDs, %.1f GHz"
-                     % (ops_cell, VALU_CYCLES_PER_OP, CLOCK / 1e9),
-            "achieved": rate, "peak": valu_peak, "unit": "cells/s", "frac": rate / valu_peak},
+            "model": "%.4g VALU ops/cell x %.2f cycles/op per wave64 (tools/ubench/valu_row.hip%s), 1024 SIMDs, "
+                     "%.1f GHz" % (ops_cell, cyc, ", ubench_valu_dot.txt" if dot_cell else "", CLOCK / 1e9),
+            "achieved": rate, "peak": valu_peak, "unit": "cells/s", "frac": rate / valu_peak,
+            "time_basis": "kernel_ms_per_step"},
         "issue": issue, "issue_source": issue_src,
         "traceback_ms": float(np.mean(tb_ms)) if want_script else None,
         "gather_ms": gather_ms,

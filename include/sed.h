@@ -47,10 +47,17 @@ enum {
 
 /* flags for sed_run_batch / sed_batch_create */
 #define SED_WANT_SCRIPT 1u
-/* sed_batch only, a hint: batches with per-cell traceback codes get three traceback/result buffers
- * and a second stream, so the traceback of run k overlaps the DP kernel of run k+1 (device memory
- * for the traceback triples).  Checkpoint batches (sed_batch_traceback_mode 2, the default for
- * script batches of > 256 pairs) ignore it and run DP then traceback on one stream. */
+/* sed_batch only, a hint:
+ *  - batches with per-cell traceback codes get three traceback/result buffers and a traceback stream, so the
+ *    traceback of run k overlaps the DP kernel of run k+1 (device memory for the traceback triples); dynamic-CHAIN
+ *    script batches also put odd runs' DP on a second DP stream (one device counter per buffer);
+ *  - distance-only batches of lane pairs alternate their runs over two streams with one result slot each;
+ *  - checkpoint batches (sed_batch_traceback_mode 2, the default for script batches of > 256 pairs) ignore it.
+ *    Instead, one of >= 2048 wave pairs always runs in parts: part i (a contiguous range of pairs, >= 1024 wave
+ *    pairs) runs forward then traceback on its own stream, 2 parts by default (environment SED_CK_HALVES = parts,
+ *    1..4: up to 4 streams, the hardware queues a process gets), and nothing joins the streams at a run's end, so
+ *    one part's traceback overlaps another part's forward (see sed_batch_dp_launches).
+ * sed_batch_sync / _results / _export / _times wait for every stream a batch uses, and a refill waits first. */
 #define SED_PIPELINE 2u
 /* distance only (no SED_WANT_SCRIPT): out_len is not computed (-1), which lets the integer
  * kernels drop the op-count field of their keys (3 instead of ~4.2 VALU ops per cell). */
@@ -144,17 +151,24 @@ int sed_batch_traceback_mode(const sed_batch *b);     /* 0 no script, 1 per-cell
 /* CHAIN diagnostics of the last run (waits for it): pairs handed out by the dynamic-CHAIN device counter, and
  * the most pairs one wave computed back to back (0 when CHAIN mode is off). */
 int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave);
-int sed_batch_run(sed_batch *b);                      /* enqueue on the context stream, returns at once */
+int sed_batch_run(sed_batch *b);                      /* enqueue on the batch's streams (SED_PIPELINE), returns at once */
 int sed_batch_sync(sed_batch *b);                     /* wait for the last run (every stream the batch uses) */
 /* Forward launches per run: a checkpoint batch of >= 2048 wave pairs runs in parts on as many streams
- * (SED_CK_HALVES = parts, default 3, >= 1024 wave pairs each), else 1.  With parts, the run times below are the mean
- * launch over the parts (the launches overlap each other's kernels). */
+ * (SED_CK_HALVES = parts, default 2, >= 1024 wave pairs each), else 1.  With parts, the run times below are the mean
+ * launch over the parts (the launches overlap each other's kernels); part 0's DP window includes the lane kernel
+ * of the batch's short pairs, if any. */
 int sed_batch_dp_launches(const sed_batch *b);
-/* device time of the last run, from HIP events on the launching stream (ms) */
+/* device time of the last run, from HIP events on the launching stream(s) (ms; with parts the mean over them) */
 int sed_batch_last_times(const sed_batch *b, float *dp_ms, float *traceback_ms);
 /* Device times of every run since the last sed_batch_reset_times (waits for them):
  * dp_ms[i] / traceback_ms[i] for run i; returns the number of runs reported (<= max_runs). */
 int sed_batch_times(sed_batch *b, float *dp_ms, float *traceback_ms, int max_runs);
+/* The same runs as intervals (waits for them): out[(i * parts + p) * 4 + k] for run i, part p
+ * (parts = sed_batch_dp_launches), k = {DP start, DP end, traceback start, traceback end} in ms from the DP start of
+ * the first run since sed_batch_reset_times (traceback fields 0 without SED_WANT_SCRIPT).  The union of the DP
+ * intervals is the time some forward kernel ran, which overlapping parts do not double-count.  Returns the number
+ * of runs reported (<= max_runs). */
+int sed_batch_spans(sed_batch *b, float *out, int max_runs);
 int sed_batch_reset_times(sed_batch *b);
 int sed_batch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32_t *out_len,
                       uint32_t *out_ops, const int64_t *ops_off);

@@ -136,6 +136,7 @@ struct sed_batch {
     // per-run event log (sed_batch_times): {dp start, dp end, tb start, tb end}
     std::vector<std::array<hipEvent_t, 4>> log;
     size_t nlog = 0;
+    long last_log = -1;  // the event-log entry of the last run (its parts' events: plog[last_log])
     sed_i32_params ip{};
     sed_f64_params fp{};
     std::vector<sed_result> h_res;
@@ -441,9 +442,12 @@ int choose_R(int mode, int max_n, int forced) {
 // stripes(R) * (m + 63) steps of R rows plus a per-step overhead worth ~0.6 rows (fitted to the iupac workload,
 // 1024^2: R = 8 5.01 ms, R = 4 5.34 ms).  The timing workload (lengths 10..500) then takes R = 4: 4.59 against
 // 4.82 ms at R = 8 (profiles/r03/fp64_R.jsonl).
-int choose_R_f64(const int32_t *len_a, const int32_t *len_b, int npairs) {
+// lane: the batch routes short pairs to the fp64 lane kernel (fill_batch: use_lane), which never runs the wave
+// kernel, so they are left out of the model.
+int choose_R_f64(const int32_t *len_a, const int32_t *len_b, int npairs, bool lane) {
     double cost[2] = {0, 0};
     for (int p = 0; p < npairs; ++p) {
+        if (lane && len_a[p] >= 1 && len_a[p] <= SED_LANE_MAXN && len_b[p] >= 1 && len_b[p] <= SED_LANE_MAXM) continue;
         for (int k = 0; k < 2; ++k) {
             const int R = 4 << k;
             cost[k] += (double)((len_a[p] + 64 * R - 1) / (64 * R)) * (len_b[p] + 63) * (R + 0.6);
@@ -453,7 +457,8 @@ int choose_R_f64(const int32_t *len_a, const int32_t *len_b, int npairs) {
 }
 
 // Event-log entries {DP start, DP end, traceback start, traceback end}, created ahead of the runs
-// that use them (outside any timed loop for up to `more` runs).
+// that use them (outside any timed loop for up to `more` runs).  Batches in parts also get the parts' entries
+// (plog), up to the same count, so no event is created while runs are being timed.
 hipError_t grow_log(sed_batch *b, size_t more) {
     for (size_t i = 0; i < more; ++i) {
         std::array<hipEvent_t, 4> a{};
@@ -463,6 +468,14 @@ hipError_t grow_log(sed_batch *b, size_t more) {
         }
         b->log.push_back(a);
     }
+    while (b->nparts > 1 && b->plog.size() < b->log.size()) {
+        std::array<hipEvent_t, 12> a{};
+        for (auto &x : a) {
+            hipError_t e = hipEventCreate(&x);
+            if (e != hipSuccess) return e;
+        }
+        b->plog.push_back(a);
+    }
     return hipSuccess;
 }
 
@@ -471,10 +484,14 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
                uint32_t flags) {
     sed_ctx *c = b->ctx;
     if (!c->have_costs) return c->fail(SED_E_STATE, "sed_set_costs() was not called");
-    for (hipStream_t ps : b->part_stream)  // (a refill must not overwrite a running part)
-        if (ps) (void)hipStreamSynchronize(ps);
-    if (b->dp2_stream) (void)hipStreamSynchronize(b->dp2_stream);
-    if (b->tb_stream) (void)hipStreamSynchronize(b->tb_stream);
+    {  // a refill must not overwrite a running part; a fault of the previous run is reported as such
+        hipError_t e = hipSuccess;
+        for (hipStream_t ps : b->part_stream)
+            if (e == hipSuccess && ps) e = hipStreamSynchronize(ps);
+        if (e == hipSuccess && b->dp2_stream) e = hipStreamSynchronize(b->dp2_stream);
+        if (e == hipSuccess && b->tb_stream) e = hipStreamSynchronize(b->tb_stream);
+        if (e != hipSuccess) return c->hipfail(e, "previous run");
+    }
     if (npairs < 0 || (npairs > 0 && (!codes_a || !off_a || !len_a || !codes_b || !off_b || !len_b)))
         return c->fail(SED_E_ARG, "bad batch arguments");
     b->npairs = npairs;
@@ -508,7 +525,10 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     case 3: mode = SED_MODE_F64_TYPED; break;
     default: mode = elig ? SED_MODE_I32 : (simple_typing(c) ? SED_MODE_F64 : SED_MODE_F64_TYPED);
     }
-    int R = (mode == SED_MODE_I32 || c->opt_R) ? choose_R(mode, max_n, c->opt_R) : choose_R_f64(len_a, len_b, npairs);
+    // fp64 batches whose short pairs go to the lane kernel (use_lane below: distance only, simple typing)
+    const bool f64_lane = c->opt_lane != 2 && !(flags & SED_WANT_SCRIPT) && (flags & SED_NO_LEN) && simple_typing(c);
+    int R = (mode == SED_MODE_I32 || c->opt_R) ? choose_R(mode, max_n, c->opt_R)
+                                                : choose_R_f64(len_a, len_b, npairs, f64_lane && mode == SED_MODE_F64);
     if (mode == SED_MODE_I32) {
         const int ROWS = 64 * R;
         bool fits = true;
@@ -523,7 +543,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         if (!fits) {
             if (c->opt_mode == 1) return c->fail(SED_E_RANGE, "integer key would overflow (D < 2^16, L < 2^14)");
             mode = simple_typing(c) ? SED_MODE_F64 : SED_MODE_F64_TYPED;
-            R = c->opt_R ? c->opt_R : choose_R_f64(len_a, len_b, npairs);
+            R = c->opt_R ? c->opt_R : choose_R_f64(len_a, len_b, npairs, f64_lane && mode == SED_MODE_F64);
         }
     } else if (c->K > SED_MAX_K) {
         return c->fail(SED_E_ALPHABET, "alphabet of %d symbols exceeds %d", c->K, SED_MAX_K);
@@ -899,6 +919,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // the event log is reused across refills (sed_run_batch's scratch batch): entries are created
     // only up to 64 ahead of the runs, and run_batch grows it on demand past that
     b->nlog = 0;
+    b->last_log = -1;
     if (b->log.size() < 64 && (e = grow_log(b, 64 - b->log.size())) != hipSuccess)
         return c->hipfail(e, "event create");
     if (b->nbuf > 1 && !b->tb_stream &&
@@ -927,6 +948,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
             return c->hipfail(e, "part stream");
     if (b->nparts > 1 && !b->ev_start && (e = hipEventCreateWithFlags(&b->ev_start, hipEventDisableTiming)) != hipSuccess)
         return c->hipfail(e, "event create");
+    if (b->nparts > 1 && (e = grow_log(b, 0)) != hipSuccess) return c->hipfail(e, "event create");  // the parts' entries
     return SED_OK;
 }
 
@@ -951,14 +973,10 @@ int run_batch_parts(sed_batch *b, const std::array<hipEvent_t, 4> &lg, sed_launc
     if ((e = hipEventRecord(b->ev_start, c->stream)) != hipSuccess) return c->hipfail(e, "stream fork");
     for (int i = 1; i < P; ++i)
         if ((e = hipStreamWaitEvent(stream(i), b->ev_start, 0)) != hipSuccess) return c->hipfail(e, "stream fork");
-    // every part's kernels carry their own events (sed_batch_times averages the parts' launches)
+    // every part's kernels carry their own events (sed_batch_times averages the parts' launches); grow_log created
+    // the parts' entries with the run's own
     const size_t li = b->nlog - 1;
-    while (b->plog.size() <= li) {
-        std::array<hipEvent_t, 12> a{};
-        for (auto &x : a)
-            if ((e = hipEventCreate(&x)) != hipSuccess) return c->hipfail(e, "event create");
-        b->plog.push_back(a);
-    }
+    if (b->plog.size() <= li) return c->fail(SED_E_STATE, "parts event log not grown");
     const std::array<hipEvent_t, 12> &pl = b->plog[li];
     auto part = [&](int i, int ph) {  // ph 0: forward, 1: traceback
         sed_launch Li = L;
@@ -970,11 +988,15 @@ int run_batch_parts(sed_batch *b, const std::array<hipEvent_t, 4> &lg, sed_launc
         Li.ev1 = i == 0 ? lg[2 * ph + 1] : pl[4 * (i - 1) + 2 * ph + 1];
         return Li;
     };
-    for (int i = 0; i < P; ++i)
-        if ((e = sed_launch_i32(part(i, 0), ip, len)) != hipSuccess) return c->hipfail(e, "DP kernel launch");
-    if (b->nlane > 0) {  // lane pairs (the whole batch's, by index) after part 0's forward
+    for (int i = 0; i < P; ++i) {
+        sed_launch Lp = part(i, 0);
+        if (i == 0 && b->nlane > 0) Lp.ev1 = nullptr;  // part 0's DP window ends with the lane kernel below
+        if ((e = sed_launch_i32(Lp, ip, len)) != hipSuccess) return c->hipfail(e, "DP kernel launch");
+    }
+    if (b->nlane > 0) {  // lane pairs (the whole batch's, by index) after part 0's forward, inside its DP window
         sed_launch Ll = L;
-        Ll.ev0 = Ll.ev1 = nullptr;
+        Ll.ev0 = nullptr;
+        Ll.ev1 = lg[1];
         if ((e = sed_launch_lane_i32(Ll, (const int32_t *)b->d_lane.p, b->nlane, ip, len)) != hipSuccess)
             return c->hipfail(e, "lane kernel launch");
     }
@@ -1015,6 +1037,7 @@ int run_batch(sed_batch *b) {
     const bool want_tb = (b->flags & SED_WANT_SCRIPT) != 0;
     hipError_t e;
     if (b->nlog == b->log.size() && (e = grow_log(b, 64)) != hipSuccess) return c->hipfail(e, "event create");
+    b->last_log = (long)b->nlog;
     const std::array<hipEvent_t, 4> lg = b->log[b->nlog++];
     hipStream_t ts = b->nbuf > 1 ? b->tb_stream : c->stream;
     const hipStream_t ds = b->alt_dp && (b->runs & 1) ? b->dp2_stream : c->stream;  // this run's DP stream
@@ -1420,14 +1443,49 @@ int sed_batch_sync(sed_batch *b) {
 int sed_batch_last_times(const sed_batch *b, float *dp_ms, float *tb_ms) {
     if (!b || !b->ran) return SED_E_STATE;
     float a = 0, t = 0;
+    const bool script = (b->flags & SED_WANT_SCRIPT) != 0;
     if (b->npairs) {
         const std::array<hipEvent_t, 4> &ev = b->evk[b->cur()];
         if (hipEventElapsedTime(&a, ev[0], ev[1]) != hipSuccess) return SED_E_DEVICE;
-        if ((b->flags & SED_WANT_SCRIPT) && hipEventElapsedTime(&t, ev[2], ev[3]) != hipSuccess) return SED_E_DEVICE;
+        if (script && hipEventElapsedTime(&t, ev[2], ev[3]) != hipSuccess) return SED_E_DEVICE;
+        if (b->nparts > 1 && b->last_log >= 0 && (size_t)b->last_log < b->plog.size()) {  // the mean over the parts
+            const std::array<hipEvent_t, 12> &pl = b->plog[b->last_log];
+            for (int p = 1; p < b->nparts; ++p) {
+                float ap = 0, tp = 0;
+                if (hipEventElapsedTime(&ap, pl[4 * (p - 1)], pl[4 * (p - 1) + 1]) != hipSuccess ||
+                    (script && hipEventElapsedTime(&tp, pl[4 * (p - 1) + 2], pl[4 * (p - 1) + 3]) != hipSuccess))
+                    return SED_E_DEVICE;
+                a += ap;
+                t += tp;
+            }
+            a /= b->nparts;
+            t /= b->nparts;
+        }
     }
     if (dp_ms) *dp_ms = a;
     if (tb_ms) *tb_ms = t;
     return SED_OK;
+}
+
+int sed_batch_spans(sed_batch *b, float *out, int max_runs) {
+    if (!b || (!out && max_runs > 0)) return SED_E_ARG;
+    int rc = sync_batch(b);
+    if (rc != SED_OK) return rc;
+    const int cnt = (int)std::min<size_t>(b->nlog, (size_t)std::max(0, max_runs));
+    const bool script = (b->flags & SED_WANT_SCRIPT) != 0;
+    const int P = b->nparts;
+    for (int i = 0; i < cnt; ++i)
+        for (int p = 0; p < P; ++p)
+            for (int k = 0; k < 4; ++k) {
+                float t = 0;
+                if (k < 2 || script) {
+                    const hipEvent_t ev = p == 0 ? b->log[i][k] : b->plog[i][4 * (p - 1) + k];
+                    if (hipEventElapsedTime(&t, b->log[0][0], ev) != hipSuccess)
+                        return b->ctx->fail(SED_E_DEVICE, "event timing");
+                }
+                out[((size_t)i * P + p) * 4 + k] = t;
+            }
+    return cnt;
 }
 
 int sed_batch_times(sed_batch *b, float *dp_ms, float *tb_ms, int max_runs) {

@@ -75,6 +75,7 @@ SIGNATURES = [
     ("sed_batch_sync", C.c_int, [C.c_void_p]),
     ("sed_batch_last_times", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("sed_batch_times", C.c_int, [C.c_void_p, _f32p, _f32p, C.c_int]),
+    ("sed_batch_spans", C.c_int, [C.c_void_p, _f32p, C.c_int]),
     ("sed_batch_reset_times", C.c_int, [C.c_void_p]),
     ("sed_batch_results", C.c_int, [C.c_void_p, _f64p, _u8p, _i32p, C.c_void_p, C.c_void_p]),
     ("sed_batch_dp_launches", C.c_int, [C.c_void_p]),
@@ -339,6 +340,16 @@ class Batch:
             self.ctx._check(cnt, "sed_batch_times")
         return a[:cnt].astype(np.float64), b[:cnt].astype(np.float64)
 
+    def spans(self, max_runs=4096):
+        """Every run since reset_times() as intervals: array [runs, parts, 4] of {DP start, DP end, traceback start,
+        traceback end} in ms from the first run's DP start (HIP events on the launching streams)."""
+        P = max(1, self.dp_launches)
+        out = np.zeros(max_runs * P * 4, np.float32)
+        cnt = self._lib.sed_batch_spans(self.ptr, out, max_runs)
+        if cnt < 0:
+            self.ctx._check(cnt, "sed_batch_spans")
+        return out[:cnt * P * 4].reshape(cnt, P, 4).astype(np.float64)
+
     def reset_times(self):
         self._lib.sed_batch_reset_times(self.ptr)
 
@@ -349,8 +360,9 @@ class Batch:
 
     @property
     def dp_launches(self):
-        """Forward launches per run (2: a checkpoint batch in two halves on two streams; the run times are then
-        the first half's kernels)."""
+        """Forward launches per run: a checkpoint batch of >= 2048 wave pairs runs in parts on as many streams
+        (SED_CK_HALVES, default 2), else 1.  With parts, times() and last_times() are the mean launch over the parts
+        (which overlap each other's kernels); spans() gives every part's intervals."""
         return self._lib.sed_batch_dp_launches(self.ptr)
 
     def device_results(self):

@@ -100,3 +100,14 @@ def test_s8d_bytes_config4():
     b = bench.s8d_bytes(np.full(8192, 4096), np.full(8192, 4096), True)
     assert abs(b - 34.46e9) < 0.01e9
     assert bench.s8d_bytes([4096], [4096], False) == 2048 + 8
+
+
+def test_interval_union():
+    """The roofline's time basis: overlapping launches (parts on streams, pipelined runs) are counted once."""
+    assert bench.interval_union([]) == 0.0
+    assert bench.interval_union([(0, 2), (1, 3), (5, 6)]) == pytest.approx(4.0)
+    assert bench.interval_union([(5, 6), (0, 10)]) == pytest.approx(10.0)
+    assert bench.interval_union([(0, 1), (1, 2), (3, 3)]) == pytest.approx(2.0)  # touching; empty ignored
+    # two parts staggered over 3 steps: part 0 [0,7], [10,17], [20,27]; part 1 [3,10], [13,20], [23,30]
+    spans = [(10 * k, 10 * k + 7) for k in range(3)] + [(10 * k + 3, 10 * k + 10) for k in range(3)]
+    assert bench.interval_union(spans) == pytest.approx(30.0)

@@ -322,6 +322,65 @@ def test_checkpoint_parts_on_streams(gpu, tables):
         gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
 
 
+def test_headline_config4_route(gpu, tables):
+    """The exact route of the bench's headline (config 4's shard) under automatic options: R = 16, checkpoints +
+    recompute, dot keys, 2 parts on 2 streams (>= 2048 wave pairs), user_costs.  The batch mixes
+      - 2100 ragged wave pairs of 64..1100 (related and unrelated),
+      - 48 pairs of 4096 x 4096 (the headline's shape; 48 rather than fewer so that the automatic rule
+        sum n*m >= 512 * sum (n + m) still picks checkpoints with the short pairs in the batch),
+      - 6 pairs with min(n, m) in 4097..4319, which must still take dot keys (user_costs' A = 2880 orders a cell's
+        candidates while min(n, m) < 4320),
+    shuffled, run 3 times back to back, every pair vs the oracle op by op (StringEditDistance.py:133-271).  The same
+    batch plus 2 pairs with min(n, m) >= 4320 must fall back to the perm-based distance keys, still in 2 parts, with
+    the same results for the common pairs and the oracle's for the 2 new ones."""
+    rng = np.random.default_rng(4400)
+    A1, B1 = _ragged(4401, 2100, 64, 1100, 64, 1100)
+    A2, B2 = _ragged(4402, 48, 4096, 4096, 4096, 4096)
+    A3, B3 = [], []
+    for k in range(6):
+        n, m = int(rng.integers(4097, 4320)), int(rng.integers(4097, 4320))
+        a, b = _ragged(4403 + k, 1, n, n, m, m, related=float(k % 2))
+        A3 += a
+        B3 += b
+    A, B = A1 + A2 + A3, B1 + B2 + B3
+    order = rng.permutation(len(A))
+    A, B = [A[i] for i in order], [B[i] for i in order]
+    la = np.array([len(x) for x in A], np.float64)
+    lb = np.array([len(x) for x in B], np.float64)
+    assert (la * lb).sum() >= 512 * (la + lb).sum()  # the automatic checkpoint rule (sed_runtime.cpp: b->ck)
+    assert np.minimum(la, lb).max() < 4320 and (np.minimum(la, lb) > 4096).sum() == 6
+    plan = _plan(tables[True])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs(A, B)
+    b, (d, ii, ln, ops) = _batch_run(gpu, packed, True, runs=3)
+    try:
+        assert b.mode == "i32" and b.rows_per_lane == 16 and b.traceback_mode == 2
+        assert b.dp_launches == 2 and b.dot_keys and b.chains == 0 and b.lane_pairs == 0
+    finally:
+        b.close()
+    _check_all(plan, packed, d, ii, ln, ops)
+    # + 2 pairs past the dot-key bound: the whole batch keeps the distance keys
+    a4, b4 = _ragged(4410, 1, 4320, 4320, 4350, 4350, related=1.0)
+    a5, b5 = _ragged(4411, 1, 4400, 4400, 4330, 4330, related=0.0)
+    A6, B6 = A + a4 + a5, B + b4 + b5
+    packed6 = sedgpu.PackedPairs(A6, B6)
+    b, (d6, ii6, ln6, ops6) = _batch_run(gpu, packed6, True, runs=3)
+    try:
+        assert b.rows_per_lane == 16 and b.traceback_mode == 2 and b.dp_launches == 2 and not b.dot_keys
+    finally:
+        b.close()
+    P = len(A)
+    assert np.array_equal(d6[:P], d) and np.array_equal(ii6[:P], ii) and np.array_equal(ln6[:P], ln)
+    bad = [p for p in range(P) if not np.array_equal(sedgpu.unpack_ops(ops6, packed6.ops_off, p, int(ln[p])),
+                                                     sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln[p])))]
+    assert not bad, bad[:10]
+    tail = sedgpu.PackedPairs(a4 + a5, b4 + b5)
+    o = tail.ops_off
+    _check_all(plan, tail, d6[P:], ii6[P:], ln6[P:],
+               np.concatenate([ops6[packed6.ops_off[P + q]:packed6.ops_off[P + q + 1]] for q in range(2)]))
+    assert o[2] == packed6.ops_off[P + 2] - packed6.ops_off[P]
+
+
 def test_repeated_runs_reuse_the_context(gpu, tables):
     """sed_run_batch refills one scratch batch per call (event log reused, not grown): many small calls in
     a row stay correct."""
