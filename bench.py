@@ -507,6 +507,8 @@ def main():
                     help="distance-only pairs one per lane / wave (no packed 16-bit cells; A/B)")
     ap.add_argument("--no-bitpar", action="store_true",
                     help="unit-cost distance-only lane pairs on the DP lane kernels instead of bit-parallel (A/B)")
+    ap.add_argument("--no-scaled", action="store_true",
+                    help="fp64 lane pairs on the fp64 DP instead of the scaled-integer DP of dyadic costs (A/B)")
     ap.add_argument("--split", type=int, default=0, help="SED_OPT_SPLIT: 0 auto, 1 force, 2 off (A/B)")
     ap.add_argument("--tb", type=int, default=0,
                     help="SED_OPT_TB: 0 auto, 1 per-cell traceback codes, 2 checkpoints + recompute (A/B)")
@@ -581,6 +583,8 @@ def main():
         ctx.set_option(sedgpu.SED_OPT_PACK, 2)
     if args.no_bitpar:
         ctx.set_option(sedgpu.SED_OPT_BITPAR, 2)
+    if args.no_scaled:
+        ctx.set_option(sedgpu.SED_OPT_SCALED, 2)
     if args.chain:
         ctx.set_option(sedgpu.SED_OPT_CHAIN, args.chain)
     if args.split:
@@ -722,7 +726,8 @@ def main():
     valu_peak = SIMDS * CLOCK * 64 / (cyc * ops_cell) if ops_cell else None
     rate = cells / (dp_busy * 1e-3)
     if batch.mode != "i32":
-        parts = (["sed_wf_f64_kernel"] if nl < P else []) + (["sed_lane_f64_kernel"] if nl else [])
+        parts = (["sed_wf_f64_kernel"] if nl < P else []) + \
+            ([("sed_lane_scaled_kernel" if batch.scaled_pairs else "sed_lane_f64_kernel")] if nl else [])
     else:
         wave_k = "sed_wf_i32_chain_kernel" if batch.chains else "sed_wf_i32_kernel"
         parts = ((["sed_wf_i32x2_kernel"] if wave_x2 else []) + ([wave_k] if nl + wave_x2 < P else []) +
@@ -755,6 +760,7 @@ def main():
         "config": {"workload": desc, "pairs_per_gpu": P, "n": n, "m": m, "costs": costs_file,
                    "script": want_script, "pipeline": pipeline and batch.traceback_mode != 2, "mode": batch.mode,
                    "rows_per_lane": R, "lane_pairs": nl, "packed_pairs": npk, "bitpar_pairs": nbp,
+                   "scaled_pairs": batch.scaled_pairs,
                    "chains": batch.chains, "dot_keys": batch.dot_keys, "ladder_dot_keys": batch.ladder_dot_keys,
                    "traceback": {0: None, 1: "per-cell codes", 2: "checkpoints + recompute",
                                  3: "per-cell codes, stripe-parallel walk"}[batch.traceback_mode],

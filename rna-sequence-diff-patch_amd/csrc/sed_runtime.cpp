@@ -61,6 +61,7 @@ struct sed_ctx {
     int opt_mode = 0, opt_R = 0, opt_split = 0, opt_lane = 0, opt_chain = 0, opt_pack = 0, opt_tb = 0;
     int opt_chain_waves = 0;
     int opt_bitpar = 0;         // SED_OPT_BITPAR: 0 auto (unit-cost distance-only lane pairs), 2 never
+    int opt_scaled = 0;         // SED_OPT_SCALED: 0 auto (fp64 lane pairs under dyadic costs), 2 never
     int opt_dot = 0;            // SED_OPT_DOT: 0 auto, 2 never (checkpoint batches keep the perm-based distance keys)    // SED_OPT_CHAIN_WAVES: cap on the persistent waves of dynamic CHAIN mode
     int opt_debug_corrupt = 0;  // SED_OPT_DEBUG_CORRUPT: pair + 1 whose sink-tile checkpoint is overwritten
     DevBuf selftest;
@@ -101,6 +102,8 @@ struct sed_batch {
     bool lane_bitpar = false;  // lane pairs run the bit-parallel unit-cost kernel (distance only)
     uint32_t umask = 0;        // fp64 lane kernel: codes of the unit-cost subset; its pairs run bit-parallel
     int nbitpar_f64 = 0;       // fp64 lane pairs flagged for it (pd.pad[0])
+    bool scaled = false;       // fp64 lane pairs on the scaled-integer kernel (dyadic costs, scaled_costs)
+    sed_scaled_params sp{};
     int nwave_x2 = 0;          // distance-only wave pairs of equal shape run two per wave, in this many waves
     int nchains = 0;           // CHAIN mode: wave pairs run as nchains back-to-back chains (0 = off)
     size_t chain_npairs = 0;   // d_chain = [chain_pairs (chain_npairs) | chain_off (nchains + 1) | counter]
@@ -422,6 +425,35 @@ uint32_t unit_subset(const sed_ctx *c) {
     return cnt >= 2 ? S : 0;
 }
 
+// Dyadic costs over at most 8 symbols (sed_lane.hip: sed_lane_scaled_kernel): the smallest S = 2^k (k <= 8) that makes
+// insert, delete and every update cost integral, with 1 <= insert * S, delete * S, 0 <= cost * S <= (insert + delete)
+// * S <= 255 (the offset keys' update byte) and the lane block's n * delete + 32 * insert within the 16-bit D field.
+// Simple typing is the caller's condition (every value a float, or the int 0 of a match).
+bool scaled_costs(const sed_ctx *c, sed_scaled_params *sp) {
+    if (c->K > 8) return false;
+    for (int k = 0; k <= 8; ++k) {
+        const double S = std::ldexp(1.0, k);
+        auto integral = [&](double v) { const double x = v * S; return x == std::floor(x) && x >= 0 && x <= 255; };
+        bool ok = integral(c->ins) && integral(c->del) && c->ins * S >= 1 && c->del * S >= 1 &&
+                  (c->ins + c->del) * S <= 255;
+        for (int e = 0; e < c->K * c->K && ok; ++e) ok = integral(c->sub[e]) && c->sub[e] <= c->ins + c->del;
+        if (!ok) continue;
+        const uint32_t ins = (uint32_t)(c->ins * S), del = (uint32_t)(c->del * S);
+        if ((double)SED_LANE_MAXN * del + (SED_LANE_MAXM + 1) * (double)ins > 65533.0) return false;
+        *sp = sed_scaled_params{};
+        sp->ins = ins;
+        sp->del = del;
+        sp->inv_scale = std::ldexp(1.0, -k);
+        for (int b = 0; b < 8; ++b)
+            for (int a = 0; a < 8; ++a) {
+                const uint32_t v = (a < c->K && b < c->K) ? (uint32_t)(c->sub[a * c->K + b] * S) : 0u;
+                sp->col[b][a >> 2] |= ((v - ins - del - 1u) & 0xFFu) << (8 * (a & 3));
+            }
+        return true;
+    }
+    return false;
+}
+
 // "simple typing": a cell's value is an int exactly when it equals 0.
 bool simple_typing(const sed_ctx *c) {
     if (c->ins_int || c->del_int || !(c->ins > 0) || !(c->del > 0)) return false;
@@ -681,6 +713,10 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
             }
         std::stable_partition(lane_idx.begin(), lane_idx.end(), [&](int32_t x) { return b->pd[x].pad[0] != 0; });
     }
+    // fp64 lane pairs under dyadic costs over <= 8 symbols: the scaled-integer lane kernel (exact, 3 VALU per cell)
+    b->scaled = mode == SED_MODE_F64 && use_lane && !want_tb && (flags & SED_NO_LEN) && c->opt_scaled != 2 &&
+                !lane_idx.empty() && scaled_costs(c, &b->sp);
+    if (b->scaled) b->sp.umask = b->umask;
     const bool x2_ok = mode == SED_MODE_I32 && x2_costs_ok(c);
     // 16-bit offset keys: n*delete + 32*insert (the lane kernel's whole block) within 0xFFFF
     bool lane_fit16 = true;
@@ -1122,6 +1158,8 @@ int run_batch(sed_batch *b) {
             e = sed_launch_lane_i32x2(L, (const int32_t *)b->d_lane.p, b->nlane_x2, ip);
         else if (b->mode == SED_MODE_I32)
             e = sed_launch_lane_i32(L, (const int32_t *)b->d_lane.p, b->nlane, ip, len);
+        else if (b->scaled)
+            e = sed_launch_lane_scaled(L, (const int32_t *)b->d_lane.p, b->nlane, b->sp);
         else
             e = sed_launch_lane_f64(L, (const int32_t *)b->d_lane.p, b->nlane, (const double *)c->gtab.p, c->ins,
                                     c->del, c->K, b->umask);
@@ -1285,6 +1323,10 @@ int sed_set_option(sed_ctx *c, int key, int value) {
         c->opt_bitpar = value;
         return SED_OK;
     }
+    if (key == SED_OPT_SCALED && (value == 0 || value == 2)) {
+        c->opt_scaled = value;
+        return SED_OK;
+    }
     if (key == SED_OPT_DOT && (value == 0 || value == 2)) {
         c->opt_dot = value;
         return SED_OK;
@@ -1423,6 +1465,10 @@ int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave)
 
 int sed_batch_bitpar_pairs(const sed_batch *b) {
     return b ? (b->lane_bitpar ? b->nlane : b->nbitpar_f64) : SED_E_ARG;
+}
+
+int sed_batch_scaled_pairs(const sed_batch *b) {
+    return b ? (b->scaled ? b->nlane - b->nbitpar_f64 : 0) : SED_E_ARG;
 }
 
 int sed_batch_packed_pairs(const sed_batch *b) {

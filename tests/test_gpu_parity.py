@@ -5,6 +5,7 @@ Bar: bit-exact — fp64 distance bits, Python int/float typing, script length
 and every op of the canonical edit script.
 """
 import hashlib
+import json
 
 import numpy as np
 import pytest
@@ -21,7 +22,7 @@ IUPAC = "AGCUYRWSKMDVHBN"
 
 
 def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len=False, chain=0, pack=0, tb=0,
-            bitpar=0):
+            bitpar=0, scaled=0):
     """Run (s1, s2) pairs through the engine; returns [(dist, is_int, len, opstr)]."""
     plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
     ctx.set_mode(mode)
@@ -32,6 +33,7 @@ def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len
     ctx.set_option(sedgpu.SED_OPT_PACK, pack)
     ctx.set_option(sedgpu.SED_OPT_TB, tb)
     ctx.set_option(sedgpu.SED_OPT_BITPAR, bitpar)
+    ctx.set_option(sedgpu.SED_OPT_SCALED, scaled)
     ctx.set_costs(plan)
     packed = sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs], [plan.encode(b) for _, b in pairs])
     dist, is_int, ln, ops = ctx.run(packed, script, no_len=no_len)
@@ -49,6 +51,7 @@ def gpu_run(ctx, table, pairs, mode=0, R=0, script=True, split=0, lane=0, no_len
     ctx.set_option(sedgpu.SED_OPT_PACK, 0)
     ctx.set_option(sedgpu.SED_OPT_TB, 0)
     ctx.set_option(sedgpu.SED_OPT_BITPAR, 0)
+    ctx.set_option(sedgpu.SED_OPT_SCALED, 0)
     return out
 
 
@@ -377,6 +380,67 @@ def test_lane_f64_unit_subset_bitpar_vs_oracle(gpu, tables, alphabet, pn):
     got = gpu_run(gpu, table, pairs, script=False, no_len=True)
     _oracle_check(table, pairs, got, no_len=True)
     assert got == gpu_run(gpu, table, pairs, script=False, no_len=True, bitpar=2)
+
+
+def _dyadic_tables(tables):
+    """(name, table, alphabet, scaled expected) for the scaled-integer lane route."""
+    out = [("costs.json ACGUN", tables[False], "ACGUN", True), ("user_costs ACGUN", tables[True], "ACGUN", True)]
+    # 8 symbols, eighths, insert != delete
+    al = "ACGUNRYS"
+    t = {"insert": 0.625, "delete": 1.25, "update": {}}
+    rng = np.random.default_rng(77)
+    for a in al:
+        t["update"][a] = {b: (0.0 if a == b else float(rng.integers(1, 15)) / 8.0) for b in al}
+    out.append(("eighths 8 symbols", t, al, True))
+    # N at 0.66 (costs.json's IUPAC values are not dyadic): the fp64 lane kernel
+    t2 = json.loads(json.dumps(tables[False]))
+    for a in "ACGU":
+        t2["update"][a]["N"] = 0.66
+    out.append(("N at 0.66", t2, "ACGUN", False))
+    # a substitution dearer than insert + delete: the offset keys' update byte cannot hold it
+    t3 = json.loads(json.dumps(tables[False]))
+    t3["update"]["A"]["N"] = 2.5
+    out.append(("A->N 2.5", t3, "ACGUN", False))
+    # 9 symbols of the same kind: beyond the 8-byte column table
+    al9 = al + "K"
+    t4 = {"insert": 0.625, "delete": 1.25, "update": {}}
+    for a in al9:
+        t4["update"][a] = {b: (0.0 if a == b else float(rng.integers(1, 15)) / 8.0) for b in al9}
+    out.append(("9 symbols", t4, al9, False))
+    return out
+
+
+@pytest.mark.parametrize("pn", [0.01, 0.2])
+def test_lane_scaled_dyadic_vs_oracle(gpu, tables, pn):
+    """fp64 distance-only lane pairs under dyadic costs over <= 8 symbols (config 5 with N: costs.json's ACGUN block is
+    1.0 but 0.75 for N) run an exact integer DP of the costs scaled by 2^k (sed_lane_scaled_kernel).  Against the
+    oracle, against the fp64 lane kernel (SED_OPT_SCALED = 2) and without the bit-parallel pairs (SED_OPT_BITPAR = 2);
+    non-dyadic tables, a cost above insert + delete and 9 symbols keep the fp64 lane kernel."""
+    for name, table, al, want in _dyadic_tables(tables):
+        rng = np.random.default_rng(7070 + int(100 * pn) + len(name))
+        base = list(al[:4]) if al.startswith("ACGUN") and len(al) == 5 else list(al)
+
+        def seq(k):
+            return "".join("N" if rng.random() < pn else rng.choice(base) for _ in range(k))
+        seqs = [seq(int(rng.integers(1, 33))) for _ in range(60)]
+        pairs = [(a, b) for a in seqs for b in seqs[:30]]
+        pairs += [(seq(int(rng.integers(1, 513))), seq(int(rng.integers(1, 33)))) for _ in range(150)]
+        pairs += [(seq(40), seq(40)) for _ in range(10)]  # wave-kernel pairs (m > 32)
+        plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
+        gpu.set_costs(plan)
+        b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs],
+                                                 [plan.encode(y) for _, y in pairs]), False, no_len=True)
+        try:
+            assert b.mode == "f64", name
+            assert (b.scaled_pairs > 0) == want, (name, b.scaled_pairs)
+            if want:
+                assert b.scaled_pairs + b.bitpar_pairs == b.lane_pairs, name
+        finally:
+            b.close()
+        got = gpu_run(gpu, table, pairs, script=False, no_len=True)
+        _oracle_check(table, pairs, got, no_len=True)
+        assert got == gpu_run(gpu, table, pairs, script=False, no_len=True, scaled=2), name
+        assert got == gpu_run(gpu, table, pairs, script=False, no_len=True, bitpar=2), name
 
 
 def test_lane_bitpar_needs_unit_costs(gpu, tables):
