@@ -509,6 +509,9 @@ def main():
                     help="unit-cost distance-only lane pairs on the DP lane kernels instead of bit-parallel (A/B)")
     ap.add_argument("--no-scaled", action="store_true",
                     help="fp64 lane pairs on the fp64 DP instead of the scaled-integer DP of dyadic costs (A/B)")
+    ap.add_argument("--timing-every", type=int, default=1,
+                    help="timing events on every run (1), every k-th run, or none (0) in the timed region; with k != 1 "
+                         "the roofline's kernel times come from an instrumented pass of the same steps afterwards")
     ap.add_argument("--split", type=int, default=0, help="SED_OPT_SPLIT: 0 auto, 1 force, 2 off (A/B)")
     ap.add_argument("--tb", type=int, default=0,
                     help="SED_OPT_TB: 0 auto, 1 per-cell traceback codes, 2 checkpoints + recompute (A/B)")
@@ -604,6 +607,8 @@ def main():
         batch.run()
     batch.sync()
     batch.reset_times()
+    if args.timing_every != 1:
+        batch.set_timing(args.timing_every)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -611,6 +616,15 @@ def main():
     batch.sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    time_pass = "the timed region"
+    if args.timing_every != 1:  # kernel times from an instrumented pass of the same steps (untimed by the bench)
+        batch.set_timing(1)
+        batch.reset_times()
+        for _ in range(args.steps):
+            batch.run()
+        batch.sync()
+        time_pass = "an instrumented pass of %d steps after the timed region (which had timing events on %s)" % (
+            args.steps, "no run" if args.timing_every == 0 else "every %d-th run" % args.timing_every)
     dp_ms, tb_ms = batch.times()
     spans = batch.spans()  # [steps, parts, {dp start, dp end, tb start, tb end}] from HIP events
     cells_all = cells
@@ -770,7 +784,7 @@ def main():
         "roofline": {"bound": "valu", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "time_basis": "DP kernels' busy time per step: union of every DP launch's HIP-event interval "
-                                   "over the timed steps / steps",
+                                   "over the steps of %s / steps" % time_pass,
                      "traffic": None if traffic is None else traffic * launches,
                      "traffic_per_launch": traffic,
                      "traffic_frac": None if traffic is None else

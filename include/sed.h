@@ -129,6 +129,14 @@ int sed_run_batch(sed_ctx *ctx,
                   double *out_dist, uint8_t *out_is_int, int32_t *out_len,
                   uint32_t *out_ops, const int64_t *ops_off);
 
+/* One pair, blocking: sed_run_batch with npairs = 1 and plain pointers (the drop-in module's per-call path:
+ * wagnerFisher of one (str1, str2), StringEditDistance.py:133-224, as IRMethods.wf_score calls it per document,
+ * IRMethods.py:435-440,469-470).  out_len may be NULL; with SED_WANT_SCRIPT, out_ops receives ceil((n+m)/16) words.
+ * Small batches like this one go to the device as one blob from pinned staging and come back in one download, and
+ * one-shot runs carry no timing events. */
+int sed_run_pair(sed_ctx *ctx, const uint8_t *codes_a, int32_t n, const uint8_t *codes_b, int32_t m, uint32_t flags,
+                 double *out_dist, uint8_t *out_is_int, int32_t *out_len, uint32_t *out_ops);
+
 /* Device-resident batch: upload once, run many times (bench), fetch results. */
 sed_batch *sed_batch_create(sed_ctx *ctx,
                             const uint8_t *codes_a, const int64_t *off_a, const int32_t *len_a,
@@ -174,6 +182,10 @@ int sed_batch_times(sed_batch *b, float *dp_ms, float *traceback_ms, int max_run
  * of runs reported (<= max_runs). */
 int sed_batch_spans(sed_batch *b, float *out, int max_runs);
 int sed_batch_reset_times(sed_batch *b);
+/* Timing events on the batch's kernels: every = 1 on every run (default), k > 1 on every k-th run, 0 never.  Untimed
+ * runs are left out of sed_batch_times / _spans / _last_times (SED_E_STATE when the last run was untimed).  Pipelined
+ * batches that order buffer reuse through their events keep them on every run. */
+int sed_batch_set_timing(sed_batch *b, int every);
 int sed_batch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32_t *out_len,
                       uint32_t *out_ops, const int64_t *ops_off);
 /* Device pointers of the result arrays (for an RCCL gather); any may be NULL.  Call sed_batch_sync first: the

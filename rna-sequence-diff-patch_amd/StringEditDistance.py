@@ -205,7 +205,8 @@ class DPMatrix:
         self.str1, self.str2 = str1, str2
         self.n, self.m = len(str1), len(str2)
         self._plan = plan
-        self._codes = (plan.encode(str1), plan.encode(str2))
+        self._bcodes = (plan.encode_bytes(str1), plan.encode_bytes(str2))
+        self._ncodes = None
         self._final = None
         self._full = None
         self._script = None
@@ -213,16 +214,20 @@ class DPMatrix:
         self._edges = {}
         self._rows = {}
 
+    @property
+    def _codes(self):
+        if self._ncodes is None:
+            self._ncodes = tuple(np.frombuffer(b, np.uint8) for b in self._bcodes)
+        return self._ncodes
+
     # -- engine calls --
     def _run(self, want_script):
         ctx = sedgpu.context()
         ctx.set_costs(self._plan)
-        packed = sedgpu.PackedPairs([self._codes[0]], [self._codes[1]])
-        dist, is_int, ln, ops = ctx.run(packed, want_script, no_len=not want_script)
-        d = float(dist[0])
-        self._final = int(d) if is_int[0] else d
+        d, is_int, ln, ops = ctx.run_pair(self._bcodes[0], self._bcodes[1], want_script, no_len=not want_script)
+        self._final = int(d) if is_int else d
         if want_script:
-            self._script = sedgpu.unpack_ops(ops, packed.ops_off, 0, int(ln[0]))
+            self._script = sedgpu.unpack_ops(ops, (0,), 0, int(ln))
 
     def _materialise(self):
         if self._full is None:
@@ -318,8 +323,12 @@ def wagnerFisher(str1, str2, userCosts=False):
     """Weighted Wagner–Fischer matrix of str1 (rows) -> str2 (columns) (reference :133-224)."""
     global _script_hint
     table = _table(userCosts)
-    sedcost.check_pair(table, str1, str2)
-    dp = DPMatrix(str1, str2, sedcost.build_plan(table, [str1], [str2]))
+    if type(str1) is str and type(str2) is str and str1 and str2:
+        plan = sedcost.pair_plan(table, str1, str2)  # check_pair + build_plan, cached by the resolved costs
+    else:
+        sedcost.check_pair(table, str1, str2)
+        plan = sedcost.build_plan(table, [str1], [str2])
+    dp = DPMatrix(str1, str2, plan)
     want, _script_hint = _script_hint, False
     dp._run(want)
     return dp

@@ -132,14 +132,14 @@ hipError_t sed_launch_lane_f64(const sed_launch &L, const int32_t *idx, int nidx
 // Scaled-integer lane kernel for fp64 distance-only batches whose costs are dyadic over at most 8 symbols (costs.json
 // with N: multiples of 1/4): every cost times S = 2^shift is an integer, and the reference's fp64 sums of such values
 // are exact, so an integer DP of the scaled costs gives D * S exactly (sed_lane.hip: sed_lane_scaled_kernel).
-// col[b] = the 8 bytes (cost(a -> b) * S - ins - del - 1) & 0xFF for a = 0..7 (a = 0..3 in col[b][0]); ins / del
-// scaled; pairs with pd.pad[0] run bit-parallel as in sed_lane_f64_kernel.
+// row[a] = the 8 bytes (cost(a -> b) * S - ins - del - 1) & 0xFF for b = 0..7 (b = 0..3 in row[a][0]); ins / del
+// scaled; pairs with pd.pad[0] run bit-parallel as in sed_lane_f64_kernel (umap: the 2-bit unit-subset code of every
+// code < 8 at bits 2c).  Byte-coded sequences start 16-byte aligned (fill_batch).
 struct sed_scaled_params {
-    uint32_t col[8][2];
+    uint32_t row[8][2];
     uint32_t ins, del;
     double inv_scale;  // 2^-shift
-    uint32_t umask;
-    uint32_t pad;
+    uint32_t umask, umap;
 };
 hipError_t sed_launch_lane_scaled(const sed_launch &L, const int32_t *idx, int nidx, const sed_scaled_params &sp);
 hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops);

@@ -393,63 +393,90 @@ __global__ __launch_bounds__(256) void sed_lane_f64_kernel(const sed_pair_desc *
 // updates 1 and 0.75; the reference maps X -> N on ingest, fa_import.py:61-62, so config 5 on real data meets N).
 // Every cost times S = 2^k is an integer and the reference's fp64 sums of such values are exact (far below 2^53),
 // so D * S is the integer DP of the scaled costs: the sed_lane_i32_kernel distance keys (offset keys, 3 VALU per
-// cell: v_perm, v_add, v_min3), with the cost table widened to 8 symbols.  Per column j the lane keeps the 8 bytes
-// cost(a -> b_j) in two registers (a = 0..3 low, 4..7 high), and one v_perm with the row symbol a as the selector
-// byte reads cost(a -> b_j) for any a < 8: selector bytes 0..3 pick S1's bytes, 4..7 S0's.  The distance is D / S,
-// a Python int exactly when it is 0, as in the fp64 path ("simple typing").  Pairs flagged by the host
-// (d.pad[0]) run bit-parallel, as in sed_lane_f64_kernel.
+// cell: v_perm, v_add, v_min3), with an 8-symbol cost table.  The row symbol a_i picks its table row (8 bytes
+// cost(a_i -> b), two registers, one LDS read per row, in flight during the row before), and each column keeps a
+// perm selector whose byte 2 is its symbol b_j (0..3 select S1's bytes, 4..7 S0's): one v_perm per cell reads
+// cost(a_i -> b_j).  The distance is D / S, a Python int exactly when it is 0, as in the fp64 path ("simple
+// typing").  Pairs flagged by the host (d.pad[0]) run bit-parallel, as in sed_lane_f64_kernel.  Sequences are byte
+// codes, each starting 16-byte aligned: str2 is two 16-byte loads, str1 one word per 4 rows.
 template <int MM>
 __global__ __launch_bounds__(256) void sed_lane_scaled_kernel(const sed_pair_desc *__restrict__ pd,
                                                               const int32_t *__restrict__ idx, int nidx,
                                                               const uint8_t *__restrict__ seqa,
                                                               const uint8_t *__restrict__ seqb,
                                                               sed_result *__restrict__ res, sed_scaled_params sp) {
+    static_assert(MM == 32, "str2 is read as two 16-byte words");
+    __shared__ uint2 tab[8];
+    if (threadIdx.x < 8) tab[threadIdx.x] = make_uint2(sp.row[threadIdx.x][0], sp.row[threadIdx.x][1]);
+    __syncthreads();
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nidx) return;
     const int pair = idx[t];
     const sed_pair_desc d = pd[pair];
     const int n = d.n, m = d.m;  // host guarantees 1 <= n <= SED_LANE_MAXN, 1 <= m <= MM, codes < 8
-    const uint8_t *pa = seqa + d.a_off, *pb = seqb + d.b_off;
+    const uint4 *pb4 = reinterpret_cast<const uint4 *>(seqb + d.b_off);
+    const uint4 q0 = pb4[0], q1 = pb4[1];  // (bytes past m: padding or the next sequence's codes, all < 8)
+    const uint32_t bw[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+    const uint32_t *pa4 = reinterpret_cast<const uint32_t *>(seqa + d.a_off);
+    uint32_t w0 = pa4[0], w1 = pa4[1];  // rows 0..3 and 4..7 (the upload pads the buffer)
     sed_result r;
     r.len = -1;
     r.err = 0;
     r.seq = 0;
-    if (d.pad[0]) {
-        const uint32_t Dv = bitpar_bytes(pa, pb, n, m, sp.umask);
+    if (d.pad[0]) {  // unit costs over this pair's symbols: sed_lane_bitpar_kernel's recurrence
+        uint32_t E0 = 0, E1 = 0;
+#pragma unroll
+        for (int j = 0; j < MM; ++j) {
+            const uint32_t u = __builtin_amdgcn_ubfe(sp.umap, 2 * ((bw[j >> 2] >> (8 * (j & 3))) & 7u), 2);
+            E0 |= (u & 1u) << j;
+            E1 |= (u >> 1) << j;
+        }
+        uint32_t Pv = ~0u, Mv = 0u;
+        for (int i = 0; i < n; ++i) {
+            const uint32_t a = (w0 >> (8 * (i & 3))) & 7u;
+            if ((i & 3) == 3) {
+                w0 = w1;
+                w1 = pa4[(i >> 2) + 2];
+            }
+            const uint32_t u = __builtin_amdgcn_ubfe(sp.umap, 2 * a, 2);
+            const uint32_t tq = (E0 ^ (0u - (u & 1u))) | (E1 ^ (0u - (u >> 1)));  // ~Eq
+            const uint32_t Xv = Mv | ~tq;
+            const uint32_t Xh = (((Pv & ~tq) + Pv) ^ Pv) | ~tq;
+            const uint32_t Ph = (Mv | ~(Xh | Pv)) << 1 | 1u;
+            const uint32_t Mh = (Pv & Xh) << 1;
+            Pv = Mh | ~(Xv | Ph);
+            Mv = Ph & Xv;
+        }
+        const uint32_t keep = m >= 32 ? ~0u : (1u << m) - 1u;
+        const uint32_t Dv = (uint32_t)n + (uint32_t)__builtin_popcount(Pv & keep) - (uint32_t)__builtin_popcount(Mv & keep);
         r.dist = (double)Dv;
         r.is_int = (Dv == 0);
         res[pair] = r;
         return;
     }
-    uint32_t lo[MM], hi[MM], V[MM + 1];
+    uint32_t sel[MM], V[MM + 1];
 #pragma unroll
-    for (int j = 0; j < MM; ++j) {
-        const uint32_t b = j < m ? (uint32_t)pb[j] : 0u;  // columns past m: don't-care
-        // the 8 x 2 table entries by selects on b's bits (a runtime index into the kernel argument would copy it to
-        // scratch)
-        const uint32_t l01 = (b & 1u) ? sp.col[1][0] : sp.col[0][0], l23 = (b & 1u) ? sp.col[3][0] : sp.col[2][0];
-        const uint32_t l45 = (b & 1u) ? sp.col[5][0] : sp.col[4][0], l67 = (b & 1u) ? sp.col[7][0] : sp.col[6][0];
-        const uint32_t h01 = (b & 1u) ? sp.col[1][1] : sp.col[0][1], h23 = (b & 1u) ? sp.col[3][1] : sp.col[2][1];
-        const uint32_t h45 = (b & 1u) ? sp.col[5][1] : sp.col[4][1], h67 = (b & 1u) ? sp.col[7][1] : sp.col[6][1];
-        const uint32_t l03 = (b & 2u) ? l23 : l01, l47 = (b & 2u) ? l67 : l45;
-        const uint32_t h03 = (b & 2u) ? h23 : h01, h47 = (b & 2u) ? h67 : h45;
-        lo[j] = (b & 4u) ? l47 : l03;
-        hi[j] = (b & 4u) ? h47 : h03;
-    }
+    for (int j = 0; j < MM; ++j)  // perm: byte 3 <- 0xFF, byte 2 <- table byte b_j, bytes 1:0 <- 0xFF
+        sel[j] = 0x0D000D0Du | (((bw[j >> 2] >> (8 * (j & 3))) & 7u) << 16);
 #pragma unroll
     for (int j = 0; j <= MM; ++j) V[j] = SED_KB;  // row 0 and column 0: the offset key B
-    uint32_t a_next = pa[0];
+    uint2 rt = tab[w0 & 7u];
     for (int i = 0; i < n; ++i) {
-        // perm: byte 3 <- 0xFF, byte 2 <- cost byte a, bytes 1:0 <- 0xFF: the addend ((cost - ins - del) << 16) - 1
-        const uint32_t sel = 0x0D000D0Du | (a_next << 16);
-        if (i + 1 < n) a_next = pa[i + 1];  // in flight during this row
-        uint32_t dg = V[0] + __builtin_amdgcn_perm(hi[0], lo[0], sel);
+        const uint2 cur = rt;  // row i's costs; row i + 1's are read during this row
+        const int i1 = i + 1;
+        if ((i1 & 3) == 0) {
+            w0 = w1;
+            w1 = pa4[(i1 >> 2) + 1];
+        }
+        rt = tab[(w0 >> (8 * (i1 & 3))) & 7u];
+        // the addend ((cost - ins - del) << 16) - 1 of the update candidate; candidates left (insert), up (delete)
+        uint32_t dg = V[0] + __builtin_amdgcn_perm(cur.y, cur.x, sel[0]);
         uint32_t left = V[0];  // stays B
 #pragma unroll
         for (int j = 1; j <= MM; ++j) {
             const uint32_t up = V[j];
-            const uint32_t dnext = j < MM ? up + __builtin_amdgcn_perm(hi[j], lo[j], sel) : 0u;
-            const uint32_t v = umin3(left, up, dg);  // insert, delete, update (distance keys: no op field)
+            const uint32_t dnext = j < MM ? up + __builtin_amdgcn_perm(cur.y, cur.x, sel[j]) : 0u;
+            const uint32_t v = umin3(left, up, dg);
             dg = dnext;
             V[j] = v;
             left = v;

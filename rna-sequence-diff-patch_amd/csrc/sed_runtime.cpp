@@ -45,6 +45,9 @@ bool is_integral_small(double v, int lim) { return v == std::floor(v) && v >= 0 
 
 }  // namespace
 
+// Batches whose input arrays and results fit this many bytes go up as one blob from pinned staging (fill_batch)
+#define SED_SMALL_BATCH_BYTES (4u << 20)
+
 struct sed_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -66,6 +69,10 @@ struct sed_ctx {
     int opt_debug_corrupt = 0;  // SED_OPT_DEBUG_CORRUPT: pair + 1 whose sink-tile checkpoint is overwritten
     DevBuf selftest;
     sed_batch *scratch = nullptr;
+    // pinned host staging (hipHostMalloc) of small batches: the upload blob, then the results' download
+    void *pin = nullptr;
+    size_t pin_cap = 0;
+    bool pin_busy = false;  // a copy from / to `pin` may still be in flight on `stream`
 
     int fail(int code, const char *fmt, ...) {
         char buf[512];
@@ -81,6 +88,27 @@ struct sed_ctx {
     }
 };
 
+struct sed_batch;
+namespace {
+// grow the context's pinned staging to `bytes` (first waiting for a copy still in flight from it)
+hipError_t pin_reserve(sed_ctx *c, size_t bytes) {
+    hipError_t e = hipSuccess;
+    if (c->pin_busy && (e = hipStreamSynchronize(c->stream)) != hipSuccess) return e;
+    c->pin_busy = false;
+    if (bytes <= c->pin_cap) return hipSuccess;
+    if (c->pin) (void)hipHostFree(c->pin);
+    c->pin = nullptr;
+    c->pin_cap = 0;
+    const size_t want = std::max<size_t>(bytes, 1u << 20);
+    if ((e = hipHostMalloc(&c->pin, want, hipHostMallocDefault)) != hipSuccess) {
+        c->pin = nullptr;
+        return e;
+    }
+    c->pin_cap = want;
+    return hipSuccess;
+}
+}  // namespace
+
 struct sed_batch {
     sed_ctx *ctx = nullptr;
     int npairs = 0;
@@ -91,6 +119,16 @@ struct sed_batch {
     uint64_t tb_words = 0, bnd_words = 0, ops_words = 0;
     double cells = 0, algo_bytes = 0;
     DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops, d_tasks, d_lane, d_chain, d_x2, d_tbmap;
+    // small batches (fill_batch: SED_SMALL_BATCH_BYTES) keep every input array and the results in one blob, d_small;
+    // the kernels' pointers (p_*) point into it or at the per-array buffers above
+    DevBuf d_small;
+    bool small = false;
+    size_t o_ops_small = 0;  // small batches: the scripts' offset from the results in d_small
+    void *p_pd = nullptr, *p_seqa = nullptr, *p_seqb = nullptr, *p_tasks = nullptr, *p_lane = nullptr,
+         *p_chain = nullptr, *p_x2 = nullptr, *p_ops = nullptr, *p_res[3] = {nullptr, nullptr, nullptr};
+    // timing events: 1 on every run (default), k > 1 on every k-th run, 0 never (sed_batch_set_timing; runs that
+    // order buffer reuse through their events always record them)
+    int time_every = 1;
     bool tbpar = false;        // stripe-parallel traceback (few long pairs, per-cell codes; sed_tb_stripe*_kernel)
     int tbpar_items = 0, tbpar_kmax = 0;
     bool split = false;
@@ -147,7 +185,7 @@ struct sed_batch {
     int cur() const { return (int)((runs - 1) % nbuf); }
     ~sed_batch() {
         d_pd.release(); d_seqa.release(); d_seqb.release(); d_bnd.release(); d_ops.release(); d_tbmap.release();
-        d_tasks.release(); d_lane.release(); d_chain.release(); d_x2.release();
+        d_tasks.release(); d_lane.release(); d_chain.release(); d_x2.release(); d_small.release();
         for (int i = 0; i < 3; ++i) {
             d_tb[i].release();
             d_res[i].release();
@@ -444,10 +482,10 @@ bool scaled_costs(const sed_ctx *c, sed_scaled_params *sp) {
         sp->ins = ins;
         sp->del = del;
         sp->inv_scale = std::ldexp(1.0, -k);
-        for (int b = 0; b < 8; ++b)
-            for (int a = 0; a < 8; ++a) {
+        for (int a = 0; a < 8; ++a)
+            for (int b = 0; b < 8; ++b) {
                 const uint32_t v = (a < c->K && b < c->K) ? (uint32_t)(c->sub[a * c->K + b] * S) : 0u;
-                sp->col[b][a >> 2] |= ((v - ins - del - 1u) & 0xFFu) << (8 * (a & 3));
+                sp->row[a][b >> 2] |= ((v - ins - del - 1u) & 0xFFu) << (8 * (b & 3));
             }
         return true;
     }
@@ -639,9 +677,9 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         if (packed) {
             aw += (nn + 15) / 16;
             bw += (mm + 15) / 16;
-        } else {
-            aw += nn;
-            bw += mm;
+        } else {  // bytes, each sequence 16-byte aligned (the lane kernels read str2 as two 16-byte words)
+            aw += ((uint64_t)nn + 15) & ~(uint64_t)15;
+            bw += ((uint64_t)mm + 15) & ~(uint64_t)15;
         }
         d.tb_off = tbw;
         d.bnd_off = bndw;
@@ -716,7 +754,12 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // fp64 lane pairs under dyadic costs over <= 8 symbols: the scaled-integer lane kernel (exact, 3 VALU per cell)
     b->scaled = mode == SED_MODE_F64 && use_lane && !want_tb && (flags & SED_NO_LEN) && c->opt_scaled != 2 &&
                 !lane_idx.empty() && scaled_costs(c, &b->sp);
-    if (b->scaled) b->sp.umask = b->umask;
+    if (b->scaled) {
+        b->sp.umask = b->umask;
+        b->sp.umap = 0;  // 2-bit unit-subset code of every code < 8 (the bit-parallel pairs)
+        for (uint32_t cc = 0; cc < 8; ++cc)
+            if ((b->umask >> cc) & 1u) b->sp.umap |= (uint32_t)__builtin_popcount(b->umask & ((1u << cc) - 1u)) << (2 * cc);
+    }
     const bool x2_ok = mode == SED_MODE_I32 && x2_costs_ok(c);
     // 16-bit offset keys: n*delete + 32*insert (the lane kernel's whole block) within 0xFFFF
     bool lane_fit16 = true;
@@ -835,50 +878,97 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         }
     }
     const size_t sa = packed ? ha.size() * 4 : ha8.size(), sb = packed ? hb.size() * 4 : hb8.size();
-    bool okalloc = b->d_pd.reserve(sizeof(sed_pair_desc) * std::max(1, npairs)) && b->d_seqa.reserve(sa) &&
-                   b->d_seqb.reserve(sb) && b->d_ops.reserve(4 * std::max<uint64_t>(1, opw)) &&
-                   b->d_bnd.reserve(4 * std::max<uint64_t>(1, bndw)) &&
-                   b->d_tasks.reserve(sizeof(int2) * std::max<size_t>(1, tasks.size())) &&
-                   b->d_lane.reserve(4 * std::max<size_t>(1, lane_idx.size())) &&
-                   b->d_chain.reserve(4 * (chain_pairs.size() + chain_off.size() + 4)) &&
-                   b->d_x2.reserve(4 * std::max<size_t>(1, x2.size())) &&
-                   b->d_tbmap.reserve(4 * std::max<uint64_t>(1, mapw));
-    for (int i = 0; i < b->nbuf && okalloc; ++i)
-        okalloc = b->d_res[i].reserve(sizeof(sed_result) * std::max(1, npairs)) &&
-                  (!want_tb || b->d_tb[i].reserve(4 * std::max<uint64_t>(1, tbw)));
+    const void *hsa = packed ? (const void *)ha.data() : (const void *)ha8.data();
+    const void *hsb = packed ? (const void *)hb.data() : (const void *)hb8.data();
+    b->chain_npairs = chain_pairs.size();
+    // Small batches (the drop-in module's per-call pairs, sed_run_batch): every input array and the zeroed results go
+    // up as one blob from the context's pinned staging buffer, with no upload sync (the staging buffer is not
+    // rewritten before that copy has completed: pin_busy), instead of one pageable copy per array and a memset.
+    const size_t s_pd = sizeof(sed_pair_desc) * std::max(1, npairs), s_tasks = sizeof(int2) * std::max<size_t>(1, tasks.size()),
+                 s_chain = 4 * (chain_pairs.size() + chain_off.size() + 4), s_lane = 4 * std::max<size_t>(1, lane_idx.size()),
+                 s_x2 = 4 * std::max<size_t>(1, x2.size()), s_res = sizeof(sed_result) * std::max(1, npairs);
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    size_t o_pd = 0, o_sa = o_pd + al(s_pd), o_sb = o_sa + al(sa), o_tasks = o_sb + al(sb), o_chain = o_tasks + al(s_tasks),
+           o_lane = o_chain + al(s_chain), o_x2 = o_lane + al(s_lane), o_res = o_x2 + al(s_x2), o_ops = o_res + al(s_res),
+           total = o_ops + al(4 * std::max<uint64_t>(1, opw));  // (results and scripts adjacent: one download)
+    b->small = b->nbuf == 1 && total <= SED_SMALL_BATCH_BYTES;
+    bool okalloc = b->d_bnd.reserve(4 * std::max<uint64_t>(1, bndw)) && b->d_tbmap.reserve(4 * std::max<uint64_t>(1, mapw));
+    if (b->small) {
+        okalloc = okalloc && b->d_small.reserve(total);
+    } else {
+        okalloc = okalloc && b->d_ops.reserve(4 * std::max<uint64_t>(1, opw)) && b->d_pd.reserve(s_pd) && b->d_seqa.reserve(sa) && b->d_seqb.reserve(sb) &&
+                  b->d_tasks.reserve(s_tasks) && b->d_lane.reserve(s_lane) && b->d_chain.reserve(s_chain) &&
+                  b->d_x2.reserve(s_x2);
+        for (int i = 0; i < b->nbuf && okalloc; ++i) okalloc = b->d_res[i].reserve(s_res);
+    }
+    for (int i = 0; i < b->nbuf && okalloc; ++i) okalloc = !want_tb || b->d_tb[i].reserve(4 * std::max<uint64_t>(1, tbw));
     if (!okalloc)
         return c->fail(SED_E_OOM, "device allocation failed (traceback %d x %.3f GB)", b->nbuf, 4.0 * tbw / 1e9);
     hipError_t e;
-    if ((e = hipMemcpyAsync(b->d_pd.p, b->pd.data(), sizeof(sed_pair_desc) * npairs, hipMemcpyHostToDevice,
-                            c->stream)) != hipSuccess)
-        return c->hipfail(e, "upload descriptors");
-    if ((e = hipMemcpyAsync(b->d_seqa.p, packed ? (void *)ha.data() : (void *)ha8.data(), sa, hipMemcpyHostToDevice,
-                            c->stream)) != hipSuccess)
-        return c->hipfail(e, "upload str1");
-    if ((e = hipMemcpyAsync(b->d_seqb.p, packed ? (void *)hb.data() : (void *)hb8.data(), sb, hipMemcpyHostToDevice,
-                            c->stream)) != hipSuccess)
-        return c->hipfail(e, "upload str2");
-    if (!tasks.empty() && (e = hipMemcpyAsync(b->d_tasks.p, tasks.data(), sizeof(int2) * tasks.size(),
-                                              hipMemcpyHostToDevice, c->stream)) != hipSuccess)
-        return c->hipfail(e, "upload tasks");
-    if (b->nchains &&
-        ((e = hipMemcpyAsync(b->d_chain.p, chain_pairs.data(), 4 * chain_pairs.size(), hipMemcpyHostToDevice,
-                             c->stream)) != hipSuccess ||
-         (!chain_off.empty() &&
-          (e = hipMemcpyAsync((int32_t *)b->d_chain.p + chain_pairs.size(), chain_off.data(), 4 * chain_off.size(),
-                              hipMemcpyHostToDevice, c->stream)) != hipSuccess)))
-        return c->hipfail(e, "upload chains");
-    b->chain_npairs = chain_pairs.size();
-    if (!lane_idx.empty() && (e = hipMemcpyAsync(b->d_lane.p, lane_idx.data(), 4 * lane_idx.size(),
-                                                 hipMemcpyHostToDevice, c->stream)) != hipSuccess)
-        return c->hipfail(e, "upload lane list");
-    if (!x2.empty() && (e = hipMemcpyAsync(b->d_x2.p, x2.data(), 4 * x2.size(), hipMemcpyHostToDevice, c->stream)) !=
-                           hipSuccess)
-        return c->hipfail(e, "upload packed-wave list");
-    for (int i = 0; i < b->nbuf; ++i)
-        if ((e = hipMemsetAsync(b->d_res[i].p, 0, sizeof(sed_result) * std::max(1, npairs), c->stream)) != hipSuccess)
-            return c->hipfail(e, "zero results");
-    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hipfail(e, "upload sync");
+    if (b->small) {
+        if ((e = pin_reserve(c, total)) != hipSuccess) return c->hipfail(e, "pinned staging");
+        char *h = (char *)c->pin, *d = (char *)b->d_small.p;
+        memcpy(h + o_pd, b->pd.data(), sizeof(sed_pair_desc) * npairs);
+        memcpy(h + o_sa, hsa, sa);
+        memcpy(h + o_sb, hsb, sb);
+        if (!tasks.empty()) memcpy(h + o_tasks, tasks.data(), sizeof(int2) * tasks.size());
+        memset(h + o_chain, 0, s_chain);
+        if (!chain_pairs.empty()) memcpy(h + o_chain, chain_pairs.data(), 4 * chain_pairs.size());
+        if (!chain_off.empty()) memcpy(h + o_chain + 4 * chain_pairs.size(), chain_off.data(), 4 * chain_off.size());
+        if (!lane_idx.empty()) memcpy(h + o_lane, lane_idx.data(), 4 * lane_idx.size());
+        if (!x2.empty()) memcpy(h + o_x2, x2.data(), 4 * x2.size());
+        memset(h + o_res, 0, s_res);
+        if ((e = hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+            return c->hipfail(e, "upload");
+        c->pin_busy = true;
+        b->p_pd = d + o_pd;
+        b->p_seqa = d + o_sa;
+        b->p_seqb = d + o_sb;
+        b->p_tasks = d + o_tasks;
+        b->p_chain = d + o_chain;
+        b->p_lane = d + o_lane;
+        b->p_x2 = d + o_x2;
+        b->p_res[0] = d + o_res;
+        b->p_ops = d + o_ops;
+        b->o_ops_small = o_ops - o_res;
+    } else {
+        b->p_ops = b->d_ops.p;
+        b->p_pd = b->d_pd.p;
+        b->p_seqa = b->d_seqa.p;
+        b->p_seqb = b->d_seqb.p;
+        b->p_tasks = b->d_tasks.p;
+        b->p_chain = b->d_chain.p;
+        b->p_lane = b->d_lane.p;
+        b->p_x2 = b->d_x2.p;
+        for (int i = 0; i < 3; ++i) b->p_res[i] = b->d_res[i].p;
+        if ((e = hipMemcpyAsync(b->p_pd, b->pd.data(), sizeof(sed_pair_desc) * npairs, hipMemcpyHostToDevice,
+                                c->stream)) != hipSuccess)
+            return c->hipfail(e, "upload descriptors");
+        if ((e = hipMemcpyAsync(b->p_seqa, hsa, sa, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+            return c->hipfail(e, "upload str1");
+        if ((e = hipMemcpyAsync(b->p_seqb, hsb, sb, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+            return c->hipfail(e, "upload str2");
+        if (!tasks.empty() && (e = hipMemcpyAsync(b->p_tasks, tasks.data(), sizeof(int2) * tasks.size(),
+                                                  hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+            return c->hipfail(e, "upload tasks");
+        if (b->nchains &&
+            ((e = hipMemcpyAsync(b->p_chain, chain_pairs.data(), 4 * chain_pairs.size(), hipMemcpyHostToDevice,
+                                 c->stream)) != hipSuccess ||
+             (!chain_off.empty() &&
+              (e = hipMemcpyAsync((int32_t *)b->p_chain + chain_pairs.size(), chain_off.data(), 4 * chain_off.size(),
+                                  hipMemcpyHostToDevice, c->stream)) != hipSuccess)))
+            return c->hipfail(e, "upload chains");
+        if (!lane_idx.empty() && (e = hipMemcpyAsync(b->p_lane, lane_idx.data(), 4 * lane_idx.size(),
+                                                     hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+            return c->hipfail(e, "upload lane list");
+        if (!x2.empty() &&
+            (e = hipMemcpyAsync(b->p_x2, x2.data(), 4 * x2.size(), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+            return c->hipfail(e, "upload packed-wave list");
+        for (int i = 0; i < b->nbuf; ++i)
+            if ((e = hipMemsetAsync(b->p_res[i], 0, s_res, c->stream)) != hipSuccess) return c->hipfail(e, "zero results");
+        if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hipfail(e, "upload sync");
+        c->pin_busy = false;
+    }
 
     // ---- kernel parameters ----
     if (mode == SED_MODE_I32) {
@@ -1011,9 +1101,12 @@ int run_batch_parts(sed_batch *b, const std::array<hipEvent_t, 4> &lg, sed_launc
         if ((e = hipStreamWaitEvent(stream(i), b->ev_start, 0)) != hipSuccess) return c->hipfail(e, "stream fork");
     // every part's kernels carry their own events (sed_batch_times averages the parts' launches); grow_log created
     // the parts' entries with the run's own
-    const size_t li = b->nlog - 1;
-    if (b->plog.size() <= li) return c->fail(SED_E_STATE, "parts event log not grown");
-    const std::array<hipEvent_t, 12> &pl = b->plog[li];
+    std::array<hipEvent_t, 12> pl{};  // (an untimed run: none)
+    if (lg[0]) {
+        const size_t li = b->nlog - 1;
+        if (b->plog.size() <= li) return c->fail(SED_E_STATE, "parts event log not grown");
+        pl = b->plog[li];
+    }
     auto part = [&](int i, int ph) {  // ph 0: forward, 1: traceback
         sed_launch Li = L;
         Li.pd = L.pd + first(i);
@@ -1033,7 +1126,7 @@ int run_batch_parts(sed_batch *b, const std::array<hipEvent_t, 4> &lg, sed_launc
         sed_launch Ll = L;
         Ll.ev0 = nullptr;
         Ll.ev1 = lg[1];
-        if ((e = sed_launch_lane_i32(Ll, (const int32_t *)b->d_lane.p, b->nlane, ip, len)) != hipSuccess)
+        if ((e = sed_launch_lane_i32(Ll, (const int32_t *)b->p_lane, b->nlane, ip, len)) != hipSuccess)
             return c->hipfail(e, "lane kernel launch");
     }
     if (c->opt_debug_corrupt > 0 && c->opt_debug_corrupt <= b->npairs) {
@@ -1054,7 +1147,7 @@ int run_batch_parts(sed_batch *b, const std::array<hipEvent_t, 4> &lg, sed_launc
         }
     }
     for (int i = 0; i < P; ++i)
-        if ((e = sed_launch_traceback_ck(part(i, 1), (uint32_t *)b->d_ops.p, ip)) != hipSuccess)
+        if ((e = sed_launch_traceback_ck(part(i, 1), (uint32_t *)b->p_ops, ip)) != hipSuccess)
             return c->hipfail(e, "traceback kernel launch");
     b->evk[0] = lg;
     ++b->runs;
@@ -1072,25 +1165,32 @@ int run_batch(sed_batch *b) {
     const int k = (int)(b->runs % b->nbuf);
     const bool want_tb = (b->flags & SED_WANT_SCRIPT) != 0;
     hipError_t e;
-    if (b->nlog == b->log.size() && (e = grow_log(b, 64)) != hipSuccess) return c->hipfail(e, "event create");
-    b->last_log = (long)b->nlog;
-    const std::array<hipEvent_t, 4> lg = b->log[b->nlog++];
+    // The run's events time it (sed_batch_times) and, when buffers rotate, order their reuse (evk below; two-slot lane
+    // batches order by stream instead).  Untimed runs (sed_batch_set_timing) launch without them.
+    const bool need_ev = b->nbuf > 1 && !(b->alt_dp && b->nbuf == 2 && !want_tb);
+    const bool timed = need_ev || b->time_every == 1 || (b->time_every > 1 && b->runs % b->time_every == 0);
+    std::array<hipEvent_t, 4> lg{};
+    if (timed) {
+        if (b->nlog == b->log.size() && (e = grow_log(b, 64)) != hipSuccess) return c->hipfail(e, "event create");
+        b->last_log = (long)b->nlog;
+        lg = b->log[b->nlog++];
+    }
     hipStream_t ts = b->nbuf > 1 ? b->tb_stream : c->stream;
     const hipStream_t ds = b->alt_dp && (b->runs & 1) ? b->dp2_stream : c->stream;  // this run's DP stream
     sed_launch L{};
-    L.pd = (const sed_pair_desc *)b->d_pd.p;
+    L.pd = (const sed_pair_desc *)b->p_pd;
     L.npairs = b->npairs;
-    L.seqa = b->d_seqa.p;
-    L.seqb = b->d_seqb.p;
+    L.seqa = b->p_seqa;
+    L.seqb = b->p_seqb;
     L.tb = want_tb ? (uint32_t *)b->d_tb[k].p : nullptr;
-    L.ops = (uint32_t *)b->d_ops.p;
+    L.ops = (uint32_t *)b->p_ops;
     L.bnd = (uint32_t *)b->d_bnd.p;
-    L.res = (sed_result *)b->d_res[k].p;
+    L.res = (sed_result *)b->p_res[k];
     L.R = b->R;
     L.stream = ds;
     L.tb_ladder = b->mode == SED_MODE_I32;
     L.ck = b->ck;
-    L.tasks = b->split ? (const int2 *)b->d_tasks.p : nullptr;
+    L.tasks = b->split ? (const int2 *)b->p_tasks : nullptr;
     L.ntasks = b->split ? b->ntasks : 0;
     // buffer k was last read by the traceback of run runs-3 (written by its DP, distance only): wait for it unless it
     // has finished already (a cross-queue wait is a barrier packet between this run's kernel and the previous one)
@@ -1111,7 +1211,7 @@ int run_batch(sed_batch *b) {
         L.ev1 = idp == ndp - 1 ? lg[1] : nullptr;
         ++idp;
     };
-    if (ndp == 0 && (e = hipEventRecord(lg[0], ds)) != hipSuccess) return c->hipfail(e, "event record");
+    if (ndp == 0 && lg[0] && (e = hipEventRecord(lg[0], ds)) != hipSuccess) return c->hipfail(e, "event record");
     // SPLIT hand-off words carry the run's epoch (1..32767), so the buffer is zeroed only on a batch's first run
     // (runs restarts at 0 on every fill) and when the epoch wraps; every kernel writes all result fields, err
     // included
@@ -1124,20 +1224,20 @@ int run_batch(sed_batch *b) {
     if (b->nparts > 1 && want_tb) return run_batch_parts(b, lg, L, ip, len);
     if (b->nwave_x2 > 0) {
         dp_events();
-        if ((e = sed_launch_i32x2(L, (const int32_t *)b->d_x2.p, b->nwave_x2, ip)) != hipSuccess)
+        if ((e = sed_launch_i32x2(L, (const int32_t *)b->p_x2, b->nwave_x2, ip)) != hipSuccess)
             return c->hipfail(e, "packed DP kernel launch");
     }
     if (b->nwave > 0) {
         dp_events();
         if (b->mode == SED_MODE_I32 && b->nchains) {
-            L.chain_pairs = (const int32_t *)b->d_chain.p;
-            L.chain_off = (const int32_t *)b->d_chain.p + b->chain_npairs;
+            L.chain_pairs = (const int32_t *)b->p_chain;
+            L.chain_off = (const int32_t *)b->p_chain + b->chain_npairs;
             L.nchains = b->nchains;
             L.chain_list = (int)b->chain_npairs;
             L.chain_counter = nullptr;
             if (b->chain_dyn) {  // zeroed on a batch's first launch only: a launch takes list + waves values
                 // (counted per launch, not per run: a run that fails after its CHAIN launch has still advanced it)
-                L.chain_counter = (uint32_t *)b->d_chain.p + b->chain_npairs + 1 + k;
+                L.chain_counter = (uint32_t *)b->p_chain + b->chain_npairs + 1 + k;
                 L.chain_base = (uint32_t)((uint64_t)b->chain_launches[k] * (uint64_t)(b->chain_npairs + b->nchains));
                 if (b->chain_launches[k] == 0 && (e = hipMemsetAsync(L.chain_counter, 0, 4, ds)) != hipSuccess)
                     return c->hipfail(e, "reset chain counter");
@@ -1153,19 +1253,19 @@ int run_batch(sed_batch *b) {
     if (b->nlane > 0) {
         dp_events();
         if (b->lane_bitpar)
-            e = sed_launch_lane_bitpar(L, (const int32_t *)b->d_lane.p, b->nlane);
+            e = sed_launch_lane_bitpar(L, (const int32_t *)b->p_lane, b->nlane);
         else if (b->nlane_x2 > 0)
-            e = sed_launch_lane_i32x2(L, (const int32_t *)b->d_lane.p, b->nlane_x2, ip);
+            e = sed_launch_lane_i32x2(L, (const int32_t *)b->p_lane, b->nlane_x2, ip);
         else if (b->mode == SED_MODE_I32)
-            e = sed_launch_lane_i32(L, (const int32_t *)b->d_lane.p, b->nlane, ip, len);
+            e = sed_launch_lane_i32(L, (const int32_t *)b->p_lane, b->nlane, ip, len);
         else if (b->scaled)
-            e = sed_launch_lane_scaled(L, (const int32_t *)b->d_lane.p, b->nlane, b->sp);
+            e = sed_launch_lane_scaled(L, (const int32_t *)b->p_lane, b->nlane, b->sp);
         else
-            e = sed_launch_lane_f64(L, (const int32_t *)b->d_lane.p, b->nlane, (const double *)c->gtab.p, c->ins,
+            e = sed_launch_lane_f64(L, (const int32_t *)b->p_lane, b->nlane, (const double *)c->gtab.p, c->ins,
                                     c->del, c->K, b->umask);
         if (e != hipSuccess) return c->hipfail(e, "lane kernel launch");
     }
-    if (ndp == 0 && (e = hipEventRecord(lg[1], ds)) != hipSuccess) return c->hipfail(e, "event record");
+    if (ndp == 0 && lg[1] && (e = hipEventRecord(lg[1], ds)) != hipSuccess) return c->hipfail(e, "event record");
     L.ev0 = L.ev1 = nullptr;
     if (want_tb && b->ck && c->opt_debug_corrupt > 0 && c->opt_debug_corrupt <= b->npairs) {
         // SED_OPT_DEBUG_CORRUPT: overwrite the column checkpoint of the sink's row in the chunk before the
@@ -1188,21 +1288,21 @@ int run_batch(sed_batch *b) {
     }
     if (want_tb) {
         if (ts != ds && (e = hipStreamWaitEvent(ts, lg[1], 0)) != hipSuccess) return c->hipfail(e, "stream wait");
-        if (b->nwave == 0 && (e = hipEventRecord(lg[2], ts)) != hipSuccess) return c->hipfail(e, "event record");
+        if (b->nwave == 0 && lg[2] && (e = hipEventRecord(lg[2], ts)) != hipSuccess) return c->hipfail(e, "event record");
         if (b->nwave > 0) {
             L.stream = ts;
             L.ev0 = lg[2];
             L.ev1 = lg[3];
             if (b->tbpar) {  // (the map kernel zeroes the scripts the segments OR into)
-                e = sed_launch_traceback_stripes(L, (uint32_t *)b->d_ops.p, (uint32_t *)b->d_tbmap.p, b->tbpar_items,
+                e = sed_launch_traceback_stripes(L, (uint32_t *)b->p_ops, (uint32_t *)b->d_tbmap.p, b->tbpar_items,
                                                  b->tbpar_kmax);
             } else {
-                e = b->ck ? sed_launch_traceback_ck(L, (uint32_t *)b->d_ops.p, ip)
-                          : sed_launch_traceback(L, (uint32_t *)b->d_ops.p);
+                e = b->ck ? sed_launch_traceback_ck(L, (uint32_t *)b->p_ops, ip)
+                          : sed_launch_traceback(L, (uint32_t *)b->p_ops);
             }
             if (e != hipSuccess) return c->hipfail(e, "traceback kernel launch");
         }
-        if (b->nwave == 0 && (e = hipEventRecord(lg[3], ts)) != hipSuccess) return c->hipfail(e, "event record");
+        if (b->nwave == 0 && lg[3] && (e = hipEventRecord(lg[3], ts)) != hipSuccess) return c->hipfail(e, "event record");
     }
     b->evk[k] = lg;
     ++b->runs;
@@ -1226,15 +1326,40 @@ int fetch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32_t *
     if (!b->ran) return c->fail(SED_E_STATE, "batch has not been run");
     const int np = b->npairs;
     hipError_t e;
-    int rc = sync_batch(b);
-    if (rc != SED_OK) return rc;
-    b->h_res.resize(np);
-    if (np && (e = hipMemcpy(b->h_res.data(), b->d_res[b->cur()].p, sizeof(sed_result) * np,
-                             hipMemcpyDeviceToHost)) !=
-                  hipSuccess)
-        return c->hipfail(e, "download results");
+    const bool want_ops = out_ops && ops_off && (b->flags & SED_WANT_SCRIPT) && np;
+    const sed_result *hr = nullptr;
+    const uint32_t *hops = nullptr;
+    std::vector<uint32_t> h;
+    if (b->small && b->nbuf == 1 && b->nparts == 1 && !b->alt_dp) {
+        // every kernel ran on the context's stream: one download of the adjacent results and scripts into the pinned
+        // staging, ordered after them, and one wait
+        const size_t bytes = b->o_ops_small + (want_ops ? 4 * b->ops_words : 0);
+        if (bytes > c->pin_cap && (e = pin_reserve(c, bytes)) != hipSuccess) return c->hipfail(e, "pinned staging");
+        if (np && (e = hipMemcpyAsync(c->pin, b->p_res[0], bytes, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+            return c->hipfail(e, "download results");
+        c->pin_busy = true;
+        int rc = sync_batch(b);
+        if (rc != SED_OK) return rc;
+        c->pin_busy = false;
+        hr = (const sed_result *)c->pin;
+        hops = (const uint32_t *)((const char *)c->pin + b->o_ops_small);
+    } else {
+        int rc = sync_batch(b);
+        if (rc != SED_OK) return rc;
+        b->h_res.resize(np);
+        if (np && (e = hipMemcpy(b->h_res.data(), b->p_res[b->cur()], sizeof(sed_result) * np, hipMemcpyDeviceToHost)) !=
+                      hipSuccess)
+            return c->hipfail(e, "download results");
+        hr = b->h_res.data();
+        if (want_ops) {
+            h.resize(b->ops_words);
+            if ((e = hipMemcpy(h.data(), b->p_ops, 4 * b->ops_words, hipMemcpyDeviceToHost)) != hipSuccess)
+                return c->hipfail(e, "download scripts");
+            hops = h.data();
+        }
+    }
     for (int p = 0; p < np; ++p) {
-        switch (b->h_res[p].err) {
+        switch (hr[p].err) {
         case 0: break;
         case SED_ERR_SPLIT_TIMEOUT: return c->fail(SED_E_DEVICE, "pair %d: inter-workgroup hand-off timed out", p);
         case SED_ERR_TB_CHECK:
@@ -1244,23 +1369,19 @@ int fetch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32_t *
         case SED_ERR_TB_GUARD: return c->fail(SED_E_DEVICE, "pair %d: traceback failed: too many tile visits", p);
         case SED_ERR_TB_LENGTH:
             return c->fail(SED_E_DEVICE, "pair %d: traceback failed: script length differs from the sink's", p);
-        default: return c->fail(SED_E_DEVICE, "pair %d: device error code %d", p, (int)b->h_res[p].err);
+        default: return c->fail(SED_E_DEVICE, "pair %d: device error code %d", p, (int)hr[p].err);
         }
     }
     for (int p = 0; p < np; ++p) {
-        if (out_dist) out_dist[p] = b->h_res[p].dist;
-        if (out_is_int) out_is_int[p] = b->h_res[p].is_int;
-        if (out_len) out_len[p] = b->h_res[p].len;
+        if (out_dist) out_dist[p] = hr[p].dist;
+        if (out_is_int) out_is_int[p] = hr[p].is_int;
+        if (out_len) out_len[p] = hr[p].len;
     }
-    if (out_ops && ops_off && (b->flags & SED_WANT_SCRIPT) && np) {
-        std::vector<uint32_t> h(b->ops_words);
-        if ((e = hipMemcpy(h.data(), b->d_ops.p, 4 * b->ops_words, hipMemcpyDeviceToHost)) != hipSuccess)
-            return c->hipfail(e, "download scripts");
+    if (want_ops)
         for (int p = 0; p < np; ++p) {
             const uint64_t words = (uint64_t)(b->n[p] + b->m[p] + 15) / 16;
-            memcpy(out_ops + ops_off[p], h.data() + b->pd[p].ops_off, 4 * words);
+            memcpy(out_ops + ops_off[p], hops + b->pd[p].ops_off, 4 * words);
         }
-    }
     return SED_OK;
 }
 
@@ -1289,6 +1410,7 @@ void sed_destroy(sed_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     delete c->scratch;
+    if (c->pin) (void)hipHostFree(c->pin);
     c->gtab.release();
     c->selftest.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1444,7 +1566,7 @@ int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave)
         const int kk = (int)((b->runs + b->nbuf - 1) % b->nbuf);  // the last run's slot
         if (b->chain_dyn && b->chain_launches[kk] > 0) {  // every persistent wave ends with one failed grab: a run takes list + waves
             uint32_t cnt = 0;
-            if ((e = hipMemcpy(&cnt, (uint32_t *)b->d_chain.p + b->chain_npairs + 1 + kk, 4, hipMemcpyDeviceToHost)) !=
+            if ((e = hipMemcpy(&cnt, (uint32_t *)b->p_chain + b->chain_npairs + 1 + kk, 4, hipMemcpyDeviceToHost)) !=
                 hipSuccess)
                 return c->hipfail(e, "download chain counter");
             const uint32_t base =
@@ -1452,7 +1574,7 @@ int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave)
             f = (int32_t)(cnt - base) - b->nchains;
         }
         std::vector<sed_result> h(b->npairs);
-        if ((e = hipMemcpy(h.data(), b->d_res[b->cur()].p, sizeof(sed_result) * b->npairs, hipMemcpyDeviceToHost)) !=
+        if ((e = hipMemcpy(h.data(), b->p_res[b->cur()], sizeof(sed_result) * b->npairs, hipMemcpyDeviceToHost)) !=
             hipSuccess)
             return c->hipfail(e, "download results");
         for (int p = 0; p < b->npairs; ++p)
@@ -1492,6 +1614,7 @@ int sed_batch_last_times(const sed_batch *b, float *dp_ms, float *tb_ms) {
     const bool script = (b->flags & SED_WANT_SCRIPT) != 0;
     if (b->npairs) {
         const std::array<hipEvent_t, 4> &ev = b->evk[b->cur()];
+        if (!ev[0]) return SED_E_STATE;  // the last run was not timed (sed_batch_set_timing)
         if (hipEventElapsedTime(&a, ev[0], ev[1]) != hipSuccess) return SED_E_DEVICE;
         if (script && hipEventElapsedTime(&t, ev[2], ev[3]) != hipSuccess) return SED_E_DEVICE;
         if (b->nparts > 1 && b->last_log >= 0 && (size_t)b->last_log < b->plog.size()) {  // the mean over the parts
@@ -1564,6 +1687,12 @@ int sed_batch_times(sed_batch *b, float *dp_ms, float *tb_ms, int max_runs) {
     return cnt;
 }
 
+int sed_batch_set_timing(sed_batch *b, int every) {
+    if (!b || every < 0) return SED_E_ARG;
+    b->time_every = every;
+    return SED_OK;
+}
+
 int sed_batch_reset_times(sed_batch *b) {
     if (!b) return SED_E_ARG;
     b->nlog = 0;
@@ -1582,11 +1711,11 @@ int sed_batch_dp_launches(const sed_batch *b) { return b ? b->nparts : SED_E_ARG
 int sed_batch_device_results(const sed_batch *b, uint64_t *d_dist, uint64_t *d_is_int, uint64_t *d_len,
                              uint64_t *d_ops, uint64_t *ops_words) {
     if (!b) return SED_E_ARG;
-    const uint64_t base = (uint64_t)(uintptr_t)b->d_res[b->runs ? b->cur() : 0].p;
+    const uint64_t base = (uint64_t)(uintptr_t)b->p_res[b->runs ? b->cur() : 0];
     if (d_dist) *d_dist = base + offsetof(sed_result, dist);
     if (d_len) *d_len = base + offsetof(sed_result, len);
     if (d_is_int) *d_is_int = base + offsetof(sed_result, is_int);
-    if (d_ops) *d_ops = (uint64_t)(uintptr_t)b->d_ops.p;
+    if (d_ops) *d_ops = (uint64_t)(uintptr_t)b->p_ops;
     if (ops_words) *ops_words = b->ops_words;
     return SED_OK;
 }
@@ -1599,7 +1728,7 @@ int sed_batch_export(sed_batch *b, uint64_t d_dist, uint64_t d_len, uint64_t d_o
     const int np = b->npairs;
     int rc = sync_batch(b);
     if (rc != SED_OK) return rc;
-    const void *resp = b->d_res[b->cur()].p;
+    const void *resp = b->p_res[b->cur()];
     hipError_t e = hipSuccess;
     if (np && d_dist)
         e = hipMemcpy2DAsync((void *)(uintptr_t)d_dist, sizeof(double), (const char *)resp + offsetof(sed_result, dist),
@@ -1608,7 +1737,7 @@ int sed_batch_export(sed_batch *b, uint64_t d_dist, uint64_t d_len, uint64_t d_o
         e = hipMemcpy2DAsync((void *)(uintptr_t)d_len, sizeof(int32_t), (const char *)resp + offsetof(sed_result, len),
                              sizeof(sed_result), sizeof(int32_t), np, hipMemcpyDeviceToDevice, c->stream);
     if (e == hipSuccess && d_ops && (b->flags & SED_WANT_SCRIPT) && b->ops_words)
-        e = hipMemcpyAsync((void *)(uintptr_t)d_ops, b->d_ops.p, 4 * b->ops_words, hipMemcpyDeviceToDevice, c->stream);
+        e = hipMemcpyAsync((void *)(uintptr_t)d_ops, b->p_ops, 4 * b->ops_words, hipMemcpyDeviceToDevice, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     return e == hipSuccess ? SED_OK : c->hipfail(e, "export results");
 }
@@ -1629,6 +1758,7 @@ int sed_run_batch(sed_ctx *c, const uint8_t *codes_a, const int64_t *off_a, cons
     if (!c->scratch) {
         c->scratch = new sed_batch();
         c->scratch->ctx = c;
+        c->scratch->time_every = 0;  // nobody reads a one-shot run's times: no timing events on its kernels
     }
     if (npairs < 0 || (npairs > 0 && (!off_a || !len_a || !off_b || !len_b)))
         return c->fail(SED_E_ARG, "bad batch arguments");
@@ -1664,6 +1794,18 @@ int sed_run_batch(sed_ctx *c, const uint8_t *codes_a, const int64_t *off_a, cons
     return SED_OK;
 }
 
+int sed_run_pair(sed_ctx *c, const uint8_t *codes_a, int32_t n, const uint8_t *codes_b, int32_t m, uint32_t flags,
+                 double *out_dist, uint8_t *out_is_int, int32_t *out_len, uint32_t *out_ops) {
+    if (!c) return SED_E_ARG;
+    if (n < 0 || m < 0 || (n && !codes_a) || (m && !codes_b)) return c->fail(SED_E_ARG, "bad pair arguments");
+    static const uint8_t none = 0;
+    const int64_t off = 0;
+    int32_t len = 0;
+    return sed_run_batch(c, n ? codes_a : &none, &off, &n, m ? codes_b : &none, &off, &m, 1, flags, out_dist, out_is_int,
+                         out_len ? out_len : &len, (flags & SED_WANT_SCRIPT) ? out_ops : nullptr,
+                         (flags & SED_WANT_SCRIPT) && out_ops ? &off : nullptr);
+}
+
 int sed_full_matrix(sed_ctx *c, const uint8_t *codes_a, int32_t n, const uint8_t *codes_b, int32_t m, double *D,
                     uint8_t *M) {
     if (!c) return SED_E_ARG;
@@ -1688,13 +1830,13 @@ int sed_full_matrix(sed_ctx *c, const uint8_t *codes_a, int32_t n, const uint8_t
         return c->fail(SED_E_OOM, "full matrix allocation (%zu cells)", cells);
     }
     sed_launch L{};
-    L.pd = (const sed_pair_desc *)tmp.d_pd.p;
+    L.pd = (const sed_pair_desc *)tmp.p_pd;
     L.npairs = 1;
-    L.seqa = tmp.d_seqa.p;
-    L.seqb = tmp.d_seqb.p;
+    L.seqa = tmp.p_seqa;
+    L.seqb = tmp.p_seqb;
     L.tb = nullptr;
     L.bnd = (uint32_t *)tmp.d_bnd.p;
-    L.res = (sed_result *)tmp.d_res[0].p;
+    L.res = (sed_result *)tmp.p_res[0];
     L.R = 4;
     L.tasks = nullptr;
     L.ntasks = 0;

@@ -24,7 +24,7 @@ def _is_py_int(v):
 class CostPlan:
     """Alphabet + resolved cost matrix for a set of (str1, str2) pairs."""
 
-    __slots__ = ("alphabet", "code", "sub", "sub_int", "ins", "ins_int", "dele", "del_int", "_key", "_lut")
+    __slots__ = ("alphabet", "code", "sub", "sub_int", "ins", "ins_int", "dele", "del_int", "_key", "_lut", "_trans")
 
     def __init__(self, alphabet, sub, sub_int, ins, ins_int, dele, del_int):
         self.alphabet = alphabet
@@ -38,6 +38,7 @@ class CostPlan:
             if len(c) == 1 and ord(c) < 256:
                 lut[ord(c)] = k
         self._lut = lut
+        self._trans = lut.tobytes()  # str.encode('latin-1').translate: characters -> codes (255 = not in the alphabet)
 
     @property
     def K(self):
@@ -57,6 +58,17 @@ class CostPlan:
             except UnicodeEncodeError:
                 pass
         return np.fromiter((self.code[c] for c in s), dtype=np.uint8, count=len(s))
+
+    def encode_bytes(self, s):
+        """The codes of encode(s) as bytes (one translate for latin-1 strings)."""
+        if isinstance(s, str) and self.K < 255:
+            try:
+                out = s.encode("latin-1").translate(self._trans)
+                if b"\xff" not in out:
+                    return out
+            except UnicodeEncodeError:
+                pass
+        return self.encode(s).tobytes()
 
 
 def _scalar(table, key):
@@ -112,6 +124,46 @@ def check_pair(table, s1, s2):
     for a in s1:
         if a in bad:
             raise bad[a][1]
+
+
+_PLANS = {}  # pair_plan's cache: resolved costs -> CostPlan
+
+
+def pair_plan(table, s1, s2):
+    """check_pair(table, s1, s2) then build_plan(table, [s1], [s2]) for one pair of non-empty strs, with the plan
+    cached by the costs the pair resolves to.  The table is read on every call (the GUI edits user_costs in place,
+    gui.py:193-252), and any lookup that fails goes through check_pair, which raises the reference's exception."""
+    d1 = dict.fromkeys(s1 if len(s1) <= 256 else distinct(s1))
+    d2 = dict.fromkeys(s2 if len(s2) <= 256 else distinct(s2))
+    try:
+        ins, dele = table[INSERT], table[DELETE]
+        vals = []
+        upd = None
+        for a in d1:
+            la = a.lower()
+            row = None
+            for b in d2:
+                if la != b.lower():
+                    if row is None:
+                        if upd is None:
+                            upd = table[UPDATE]
+                        row = upd[a]
+                    vals.append(row[b])
+    except (KeyError, TypeError, IndexError, AttributeError):
+        check_pair(table, s1, s2)  # the reference's exception, if any
+        return build_plan(table, [s1], [s2])
+    # (the symbols of both strings in first-occurrence order fix the alphabet and which combinations are resolved)
+    key = (tuple(d1), tuple(d2), tuple(vals), tuple(type(v) for v in vals), ins, type(ins), dele, type(dele))
+    try:
+        plan = _PLANS.get(key)
+    except TypeError:  # unhashable cost values
+        return build_plan(table, [s1], [s2])
+    if plan is None:
+        plan = build_plan(table, [s1], [s2])
+        if len(_PLANS) > 512:
+            _PLANS.clear()
+        _PLANS[key] = plan
+    return plan
 
 
 def build_plan(table, strs1, strs2):

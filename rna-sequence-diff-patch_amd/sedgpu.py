@@ -79,6 +79,9 @@ SIGNATURES = [
     ("sed_batch_times", C.c_int, [C.c_void_p, _f32p, _f32p, C.c_int]),
     ("sed_batch_spans", C.c_int, [C.c_void_p, _f32p, C.c_int]),
     ("sed_batch_reset_times", C.c_int, [C.c_void_p]),
+    ("sed_batch_set_timing", C.c_int, [C.c_void_p, C.c_int]),
+    ("sed_run_pair", C.c_int, [C.c_void_p, C.c_char_p, C.c_int32, C.c_char_p, C.c_int32, C.c_uint32, C.c_void_p,
+                               C.c_void_p, C.c_void_p, C.c_void_p]),
     ("sed_batch_results", C.c_int, [C.c_void_p, _f64p, _u8p, _i32p, C.c_void_p, C.c_void_p]),
     ("sed_batch_dp_launches", C.c_int, [C.c_void_p]),
     ("sed_batch_device_results", C.c_int, [C.c_void_p] + [C.POINTER(C.c_uint64)] * 5),
@@ -132,6 +135,8 @@ class Context:
         if not self.ptr:
             raise SedError("sed_create(%d) failed: no usable HIP device" % device)
         self._cost_key = None
+        self._cost_plan = None
+        self._pair_out = None
 
     def close(self):
         # a forked child must not call into the parent's HIP context (it would destroy or hang on it)
@@ -159,16 +164,22 @@ class Context:
         """0 auto, 1 integer, 2 fp64, 3 fp64 with int typing."""
         self.set_option(SED_OPT_MODE, mode)
         self._cost_key = None
+        self._cost_plan = None
 
     def set_costs(self, plan):
+        if plan is self._cost_plan:  # (sedcost.pair_plan hands out the same plan object for the same costs)
+            return
         key = plan.key()
         if key == self._cost_key:
+            self._cost_plan = plan
             return
+        self._cost_plan = None
         sub = np.ascontiguousarray(plan.sub, dtype=np.float64).ravel()
         sub_int = np.ascontiguousarray(plan.sub_int, dtype=np.uint8).ravel()
         self._check(self._lib.sed_set_costs(self.ptr, plan.K, sub, sub_int, plan.ins, plan.ins_int,
                                             plan.dele, plan.del_int), "sed_set_costs")
         self._cost_key = key
+        self._cost_plan = plan
 
     def selftest(self):
         return self._lib.sed_selftest(self.ptr)
@@ -192,6 +203,26 @@ class Context:
                                      dist, is_int, ln, ops_ptr, ops_off_ptr)
         self._check(rc, "sed_run_batch")
         return dist[:np_], is_int[:np_], ln[:np_], ops
+
+    def run_pair(self, codes_a, codes_b, want_script, no_len=False):
+        """One pair (codes as bytes): (dist, is_int, len, ops u32[] | None) through sed_run_pair, the per-call path of
+        the drop-in module (no numpy arrays on the way in, preallocated result cells on the way out)."""
+        if self._pid != os.getpid():
+            self._check(0, "sed_run_pair")
+        r = self._pair_out
+        if r is None:
+            r = self._pair_out = (C.c_double(), C.c_uint8(), C.c_int32())
+        ops = None
+        ops_ptr = None
+        if want_script:
+            ops = np.zeros(max(1, (len(codes_a) + len(codes_b) + 15) // 16), np.uint32)
+            ops_ptr = ops.ctypes.data
+        flags = SED_WANT_SCRIPT if want_script else (SED_NO_LEN if no_len else 0)
+        rc = self._lib.sed_run_pair(self.ptr, codes_a, len(codes_a), codes_b, len(codes_b), flags, C.addressof(r[0]),
+                                    C.addressof(r[1]), C.addressof(r[2]), ops_ptr)
+        if rc != 0:
+            self._check(rc, "sed_run_pair")
+        return r[0].value, r[1].value, r[2].value, ops
 
     def full_matrix(self, codes_a, codes_b):
         n, m = len(codes_a), len(codes_b)
@@ -360,6 +391,10 @@ class Batch:
     def reset_times(self):
         self._lib.sed_batch_reset_times(self.ptr)
 
+    def set_timing(self, every):
+        """Timing events on every run (1), every k-th run (k), or none (0)."""
+        self.ctx._check(self._lib.sed_batch_set_timing(self.ptr, int(every)), "sed_batch_set_timing")
+
     def work(self):
         a, b = C.c_double(), C.c_double()
         self._lib.sed_batch_work(self.ptr, C.byref(a), C.byref(b))
@@ -477,6 +512,9 @@ class EngineClient:
     def run(self, packed, want_script, no_len=False):
         return self._call("run", packed, want_script, no_len)
 
+    def run_pair(self, codes_a, codes_b, want_script, no_len=False):
+        return self._call("run_pair", codes_a, codes_b, want_script, no_len)
+
     def full_matrix(self, codes_a, codes_b):
         return self._call("full_matrix", np.asarray(codes_a, np.uint8), np.asarray(codes_b, np.uint8))
 
@@ -516,6 +554,8 @@ def _engine_worker(device, rfd, wfd):
                 val = ctx.selftest()
             elif op == "run":
                 val = ctx.run(*args)
+            elif op == "run_pair":
+                val = ctx.run_pair(*args)
             elif op == "full_matrix":
                 val = ctx.full_matrix(*args)
             else:

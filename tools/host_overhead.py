@@ -11,11 +11,12 @@ table = json.load(open(os.path.join(REPO, "tests", "golden", "costs.json")))
 plan = sedcost.build_plan(table, [synth.ALPHABET], [synth.ALPHABET])
 ctx = sedgpu.Context(0)
 ctx.set_costs(plan)
-for pipeline in (False, True):  # True: three result buffers, odd runs on a second stream
+for pipeline, every in ((False, 1), (True, 1), (False, 0), (True, 0)):  # pipeline: odd runs on a second stream
     b = sedgpu.Batch(ctx, sedgpu.PackedPairs(qa, qb), False, no_len=True, pipeline=pipeline)
     for _ in range(5):
         b.run()
     b.sync()
+    b.set_timing(every)  # 0: no timing events on the kernels
     for n in (10, 100, 400):
         b.reset_times()
         t0 = time.perf_counter()
@@ -25,6 +26,7 @@ for pipeline in (False, True):  # True: three result buffers, odd runs on a seco
         b.sync()
         t2 = time.perf_counter()
         dp, _ = b.times()
-        print("pipeline %d runs %4d  enqueue %.1f us/run  total %.1f us/run  kernel %.1f us" %
-              (pipeline, n, (t1 - t0) / n * 1e6, (t2 - t0) / n * 1e6, float(np.mean(dp)) * 1e3), flush=True)
+        print("pipeline %d events %d runs %4d  enqueue %.1f us/run  total %.1f us/run  kernel %.1f us" %
+              (pipeline, every, n, (t1 - t0) / n * 1e6, (t2 - t0) / n * 1e6,
+               float(np.mean(dp)) * 1e3 if len(dp) else float("nan")), flush=True)
     b.close()
