@@ -507,6 +507,8 @@ def main():
                     help="distance-only pairs one per lane / wave (no packed 16-bit cells; A/B)")
     ap.add_argument("--no-bitpar", action="store_true",
                     help="unit-cost distance-only lane pairs on the DP lane kernels instead of bit-parallel (A/B)")
+    ap.add_argument("--seg", type=int, default=0,
+                    help="SED_OPT_SEG: fp64 pairs in 16-lane segments: 0 auto, 1 every eligible pair, 2 never (A/B)")
     ap.add_argument("--no-scaled", action="store_true",
                     help="fp64 lane pairs on the fp64 DP instead of the scaled-integer DP of dyadic costs (A/B)")
     ap.add_argument("--timing-every", type=int, default=-1,
@@ -590,6 +592,8 @@ def main():
         ctx.set_option(sedgpu.SED_OPT_BITPAR, 2)
     if args.no_scaled:
         ctx.set_option(sedgpu.SED_OPT_SCALED, 2)
+    if args.seg:
+        ctx.set_option(sedgpu.SED_OPT_SEG, args.seg)
     if args.chain:
         ctx.set_option(sedgpu.SED_OPT_CHAIN, args.chain)
     if args.split:
@@ -785,7 +789,7 @@ def main():
         "config": {"workload": desc, "pairs_per_gpu": P, "timing_every": args.timing_every, "n": n, "m": m, "costs": costs_file,
                    "script": want_script, "pipeline": pipeline and batch.traceback_mode != 2, "mode": batch.mode,
                    "rows_per_lane": R, "lane_pairs": nl, "packed_pairs": npk, "bitpar_pairs": nbp,
-                   "scaled_pairs": batch.scaled_pairs,
+                   "scaled_pairs": batch.scaled_pairs, "segment_pairs": batch.segment_pairs,
                    "chains": batch.chains, "dot_keys": batch.dot_keys, "ladder_dot_keys": batch.ladder_dot_keys,
                    "traceback": {0: None, 1: "per-cell codes", 2: "checkpoints + recompute",
                                  3: "per-cell codes, stripe-parallel walk"}[batch.traceback_mode],

@@ -90,6 +90,9 @@ enum {
 #define SED_OPT_SCALED 12       /* distance-only fp64 batches whose costs are dyadic over <= 8 symbols (costs.json with N:
                                    multiples of 1/4): lane pairs run an exact integer DP of the costs scaled by 2^k
                                    (3 VALU per cell instead of the fp64 cell): 0 auto (on), 2 never */
+#define SED_OPT_SEG 13          /* fp64 batches of > 256 wave pairs: pairs whose cost model favours it run in 16-lane
+                                   segments, four per wave (stripes of 16 R rows, a 15-step ramp instead of 63: the
+                                   timing.py sweep's short pairs): 0 auto, 1 every such pair, 2 never */
 #define SED_OPT_DEBUG_CORRUPT 9 /* testing only: p + 1 overwrites one checkpoint word of pair p before its traceback,
                                    which must then fail with SED_E_DEVICE naming the pair; 0 off */
 
@@ -150,6 +153,7 @@ int sed_batch_chains(const sed_batch *b);             /* CHAIN mode: number of c
 int sed_batch_packed_pairs(const sed_batch *b);       /* pairs computed two per lane / wave (SED_OPT_PACK) */
 int sed_batch_bitpar_pairs(const sed_batch *b);       /* lane pairs computed bit-parallel (SED_OPT_BITPAR) */
 int sed_batch_scaled_pairs(const sed_batch *b);       /* fp64 lane pairs on the scaled-integer DP (SED_OPT_SCALED) */
+int sed_batch_segment_pairs(const sed_batch *b);      /* fp64 wave pairs run in 16-lane segments (SED_OPT_SEG) */
 /* The byte factorisation behind SED_OPT_DOT, without a device (tests): for the 4 x 4 table sub (a -> b, row-major)
  * and insert/delete costs, the dot keys for pairs with min(n, m) <= maxmin (ladder_maxsum = 0) or the ladder dot
  * keys for n + m <= ladder_maxsum.  out[0..3] = row vectors, out[4..7] = column vectors (4 signed bytes each),

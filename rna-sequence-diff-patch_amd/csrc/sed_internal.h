@@ -112,6 +112,11 @@ hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm, bool l
 // CHAIN mode (single-stripe pairs, R in {4, 8, 16}): one wave per chain of pairs.
 hipError_t sed_launch_i32_chain(const sed_launch &L, const sed_i32_params &prm, bool len);
 hipError_t sed_launch_f64(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed);
+// fp64 wave kernel in 16-lane segments, four pairs per wave (pairs idx[0 .. nidx), pd.pad[1] = 1; the SW = 64 kernel and
+// traceback skip them), and their per-cell-code traceback
+hipError_t sed_launch_f64_seg(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed,
+                              const int32_t *idx, int nidx);
+hipError_t sed_launch_traceback_seg(const sed_launch &L, uint32_t *ops, const int32_t *idx, int nidx);
 hipError_t sed_launch_f64_full(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed,
                                const sed_full_out &fo);
 // Lane-per-pair integer kernel (sed_lane.hip): pairs idx[0..nidx) with 1 <= m <= SED_LANE_MAXM.

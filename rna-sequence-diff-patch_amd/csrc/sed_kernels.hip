@@ -82,6 +82,41 @@ __device__ __forceinline__ double dpp_rol1_f64(double src) {
     return __longlong_as_double(((uint64_t)hi << 32) | lo);
 }
 
+// The same moves inside segments of SW lanes (SW = 64: the whole wave; SW = 16: each DPP row, so a wave runs four
+// independent segments, the fp64 kernel's short pairs): shr = lane i <- lane i-1 (the segment's lane 0 keeps `old`,
+// row_shr:1), shl = lane i <- lane i+1 (the segment's last lane keeps `old`, row_shl:1), rol = lane i <- lane i+1
+// mod SW (row_ror:15).
+#define DPP_ROW_SHL1 0x101
+#define DPP_ROW_SHR1 0x111
+#define DPP_ROW_ROR15 0x12F
+template <int SW> __device__ __forceinline__ uint32_t seg_shr1(uint32_t old, uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)src, SW == 64 ? DPP_WAVE_SHR1 : DPP_ROW_SHR1, 0xf, 0xf,
+                                                 false);
+}
+template <int SW> __device__ __forceinline__ uint32_t seg_shl1(uint32_t old, uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)src, SW == 64 ? DPP_WAVE_SHL1 : DPP_ROW_SHL1, 0xf, 0xf,
+                                                 false);
+}
+template <int SW> __device__ __forceinline__ uint32_t seg_rol1(uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)src, (int)src, SW == 64 ? DPP_WAVE_ROL1 : DPP_ROW_ROR15, 0xf, 0xf,
+                                                 false);
+}
+template <int SW> __device__ __forceinline__ double seg_shr1_f64(double old, double src) {
+    const uint64_t o = __double_as_longlong(old), s = __double_as_longlong(src);
+    const uint32_t lo = seg_shr1<SW>((uint32_t)o, (uint32_t)s), hi = seg_shr1<SW>((uint32_t)(o >> 32), (uint32_t)(s >> 32));
+    return __longlong_as_double(((uint64_t)hi << 32) | lo);
+}
+template <int SW> __device__ __forceinline__ double seg_shl1_f64(double old, double src) {
+    const uint64_t o = __double_as_longlong(old), s = __double_as_longlong(src);
+    const uint32_t lo = seg_shl1<SW>((uint32_t)o, (uint32_t)s), hi = seg_shl1<SW>((uint32_t)(o >> 32), (uint32_t)(s >> 32));
+    return __longlong_as_double(((uint64_t)hi << 32) | lo);
+}
+template <int SW> __device__ __forceinline__ double seg_rol1_f64(double src) {
+    const uint64_t s = __double_as_longlong(src);
+    const uint32_t lo = seg_rol1<SW>((uint32_t)s), hi = seg_rol1<SW>((uint32_t)(s >> 32));
+    return __longlong_as_double(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) { return min(min(a, b), c); }
 __device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) { return max(max(a, b), c); }
 // the dot keys' update candidate: diag + dot4(row vector, column vector) over signed bytes (v_dot4_i32_i8)
@@ -1211,7 +1246,7 @@ struct f64_cell_in {
     uint32_t t;
 };
 
-template <int R, bool TB, bool TYPED, bool MASKED, bool FULL>
+template <int R, bool TB, bool TYPED, bool MASKED, bool FULL, int SW = 64>
 __device__ __forceinline__ void f64_step(double (&D)[R], uint32_t (&LK)[R], uint32_t (&T)[R],
                                          const uint32_t (&rowbase)[R], const double2 *__restrict__ tab,
                                          double &dtop_prev, uint32_t &ltop_prev, uint32_t &ttop_prev,
@@ -1221,15 +1256,15 @@ __device__ __forceinline__ void f64_step(double (&D)[R], uint32_t (&LK)[R], uint
                                          const double cins, const double cdel, const uint32_t tins,
                                          const uint32_t tdel, const bool active, const sed_full_out &fo,
                                          const int i0, const int j) {
-    const double dtop = dpp_shr1_f64(dch, dbot);
-    const uint32_t ltop = dpp_shr1(lch, lbot);
+    const double dtop = seg_shr1_f64<SW>(dch, dbot);
+    const uint32_t ltop = seg_shr1<SW>(lch, lbot);
     uint32_t ttop = 0;
-    if constexpr (TYPED) ttop = dpp_shr1(tch, tbot);
-    bsel = dpp_shr1(sch, bsel);
-    dch = dpp_rol1_f64(dch);
-    lch = dpp_rol1(lch);
-    if constexpr (TYPED) tch = dpp_rol1(tch);
-    sch = dpp_rol1(sch);
+    if constexpr (TYPED) ttop = seg_shr1<SW>(tch, tbot);
+    bsel = seg_shr1<SW>(sch, bsel);
+    dch = seg_rol1_f64<SW>(dch);
+    lch = seg_rol1<SW>(lch);
+    if constexpr (TYPED) tch = seg_rol1<SW>(tch);
+    sch = seg_rol1<SW>(sch);
     double dup = dtop, ddiag = dtop_prev;
     uint32_t lup = ltop, ldiag = ltop_prev, tup = ttop, tdiag = ttop_prev;
 #pragma unroll
@@ -1291,32 +1326,46 @@ __device__ __forceinline__ void f64_step(double (&D)[R], uint32_t (&LK)[R], uint
     dbot = D[R - 1];
     lbot = LK[R - 1];
     if constexpr (TYPED) tbot = T[R - 1];
-    doutc = dpp_shl1_f64(dbot, doutc);
-    loutc = dpp_shl1(lbot, loutc);
-    if constexpr (TYPED) toutc = dpp_shl1(tbot, toutc);
+    doutc = seg_shl1_f64<SW>(dbot, doutc);
+    loutc = seg_shl1<SW>(lbot, loutc);
+    if constexpr (TYPED) toutc = seg_shl1<SW>(tbot, toutc);
 }
 
-template <int R, bool TB, bool TYPED, bool FULL>
+// SW = 64: one wave per pair (pairs with d.seg set are skipped: they run in segments).  SW = 16 (short pairs of
+// large batches): each DPP row of 16 lanes runs its own pair (items idx[0 .. nidx), four per wave, the
+// host sorts them so a wave's four pairs have similar shapes): stripes of 16 R rows, 16-step chunks, a 15-step ramp
+// instead of 63, and every lane move a row DPP (seg_*), so the four segments never exchange data.  The loop bounds
+// are then per lane (uniform within a segment), and a segment whose pair is done sits out with its lanes masked.
+template <int R, bool TB, bool TYPED, bool FULL, int SW = 64>
 __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
                                                          const uint8_t *__restrict__ seqa,
                                                          const uint8_t *__restrict__ seqb,
                                                          uint32_t *__restrict__ tb, uint32_t *__restrict__ bnd,
                                                          sed_result *__restrict__ res,
                                                          const double *__restrict__ gtab, sed_f64_params prm,
-                                                         sed_full_out fo) {
-    constexpr int ROWS = 64 * R;
+                                                         sed_full_out fo, const int32_t *__restrict__ idx) {
+    static_assert(SW == 64 || (SW == 16 && !FULL), "segments of 16 lanes: no full-matrix output");
+    constexpr int ROWS = SW * R;
     constexpr int G = Grp<R>::G;
+    static_assert(SW % G == 0, "a group of G steps never crosses a chunk");
     __shared__ double2 tab[SED_MAX_K * SED_MAX_K];
     const int K = prm.K;
     for (int e = threadIdx.x; e < K * K; e += blockDim.x)
         tab[e] = make_double2(gtab[2 * e], gtab[2 * e + 1]);
     __syncthreads();
 
-    const int lane = threadIdx.x & 63;
-    const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (pair >= npairs) return;
+    const int lane = SW == 64 ? (threadIdx.x & 63) : (threadIdx.x & (SW - 1));  // lane within the segment
+    int pair;
+    if constexpr (SW == 64) {
+        pair = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+        if (pair >= npairs) return;
+    } else {
+        const int item = (blockIdx.x * 256 + threadIdx.x) / SW;
+        if (item >= npairs) return;  // (npairs = the item count)
+        pair = idx[item];
+    }
     const sed_pair_desc d = pd[pair];
-    if (d.lane) return;  // short str2, distance only: sed_lane.hip
+    if (d.lane || (SW == 64 && d.pad[1])) return;  // short str2, distance only: sed_lane.hip; segments: the SW = 16 launch
     const int n = d.n, m = d.m;
     if constexpr (FULL) {  // border cells: row 0 (insert edges) and column 0 (delete edges)
         for (int j = lane; j <= m; j += 64) {
@@ -1342,10 +1391,10 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
         return;
     }
     const int nstripes = (n + ROWS - 1) / ROWS;
-    const int SG = (m + 63 + G - 1) / G * G;
-    const int nchunks = (SG + 63) >> 6;
-    // bottom-row buffer of a pair: [D as u64 | L as u32 | T as u32] planes
-    const uint64_t bwords = (uint64_t)(nchunks + 2) * 64u;
+    const int SG = (m + SW - 1 + G - 1) / G * G;
+    const int nchunks = (SG + SW - 1) / SW;
+    // bottom-row buffer of a pair: [D as u64 | L as u32 | T as u32] planes; column j at index j + SW
+    const uint64_t bwords = (uint64_t)(nchunks + 2) * SW;
     uint64_t *bndD = reinterpret_cast<uint64_t *>(bnd + d.bnd_off);
     uint32_t *bndL = bnd + d.bnd_off + 2 * bwords;
     uint32_t *bndT = bndL + bwords;
@@ -1374,26 +1423,26 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
         uint32_t W[4] = {0, 0, 0, 0};
 
         auto load_d = [&](int c) -> double {
-            const int j = 64 * c + lane + 1;
+            const int j = SW * c + lane + 1;
             if (k == 0) return (double)j * prm.ins;
-            return __longlong_as_double((long long)load_sc1_u64(bndD + j + 64));
+            return __longlong_as_double((long long)load_sc1_u64(bndD + j + SW));
         };
         auto load_l = [&](int c) -> uint32_t {
-            const int j = 64 * c + lane + 1;
+            const int j = SW * c + lane + 1;
             if (k == 0) return (uint32_t)j << 2;
-            return load_sc1(bndL + j + 64);
+            return load_sc1(bndL + j + SW);
         };
         auto load_t = [&](int c) -> uint32_t {
             if (k == 0) return tins;
-            return load_sc1(bndT + 64 * c + lane + 65);
+            return load_sc1(bndT + SW * c + lane + SW + 1);
         };
         auto load_sel = [&](int c) -> uint32_t {
-            const int ci = 64 * c + lane;
+            const int ci = SW * c + lane;
             return (ci < m) ? (uint32_t)pb[ci] : 0u;
         };
         double dch = load_d(0);
         uint32_t lch = load_l(0), tch = TYPED ? load_t(0) : 0u, sch = load_sel(0);
-        uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * 256u;
+        uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * (SW * 4u);
         const bool last = (k == nstripes - 1);
         int s = 0;
         for (int c = 0; c < nchunks; ++c) {
@@ -1407,29 +1456,30 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
             }
             // (A separate loop for chunks of unmasked steps, as in the integer kernels, measured slower: iupac DP
             // 4.89 against 4.81 ms, timing 4.60 against 4.47 ms; profiles/r03/f64_plain_dropped.)
-            for (int g = 0; g < 64 / G && s < SG; ++g, s += G) {
-                const bool full = (s >= 63) && (s + G - 1 < m);
+            for (int g = 0; g < SW / G && s < SG; ++g, s += G) {
+                const bool full = (s >= SW - 1) && (s + G - 1 < m);
 #pragma unroll
                 for (int u = 0; u < G; ++u) {
                     const int j = s + u - lane + 1;
                     const bool active = (j >= 1) && (j <= m);
                     if (full)
-                        f64_step<R, TB, TYPED, false, FULL>(D, LK, T, rowbase, tab, dtop_prev, ltop_prev, ttop_prev,
-                                                            dbot, lbot, tbot, bsel, dch, lch, tch, sch, doutc, loutc,
-                                                            toutc, W, u, prm.ins, prm.del, tins, tdel, active, fo,
-                                                            row0 + 1, j);
+                        f64_step<R, TB, TYPED, false, FULL, SW>(D, LK, T, rowbase, tab, dtop_prev, ltop_prev, ttop_prev,
+                                                                dbot, lbot, tbot, bsel, dch, lch, tch, sch, doutc, loutc,
+                                                                toutc, W, u, prm.ins, prm.del, tins, tdel, active, fo,
+                                                                row0 + 1, j);
                     else
-                        f64_step<R, TB, TYPED, true, FULL>(D, LK, T, rowbase, tab, dtop_prev, ltop_prev, ttop_prev,
-                                                           dbot, lbot, tbot, bsel, dch, lch, tch, sch, doutc, loutc,
-                                                           toutc, W, u, prm.ins, prm.del, tins, tdel, active, fo,
-                                                           row0 + 1, j);
+                        f64_step<R, TB, TYPED, true, FULL, SW>(D, LK, T, rowbase, tab, dtop_prev, ltop_prev, ttop_prev,
+                                                               dbot, lbot, tbot, bsel, dch, lch, tch, sch, doutc, loutc,
+                                                               toutc, W, u, prm.ins, prm.del, tins, tdel, active, fo,
+                                                               row0 + 1, j);
                 }
-                if constexpr (TB) store_tb(tbk + ((uint64_t)(s / G) * 64u + lane) * 4u, W);
+                if constexpr (TB) store_tb(tbk + ((uint64_t)(s / G) * SW + lane) * 4u, W);
             }
+            // lane i holds the segment's last lane's bottom cell of step s - SW + i, i.e. column s - 2 SW + 2 + i
             if (!last) {
-                bndD[s - 62 + lane] = (uint64_t)__double_as_longlong(doutc);
-                bndL[s - 62 + lane] = loutc;
-                if (TYPED) bndT[s - 62 + lane] = toutc;
+                bndD[s - SW + 2 + lane] = (uint64_t)__double_as_longlong(doutc);
+                bndL[s - SW + 2 + lane] = loutc;
+                if (TYPED) bndT[s - SW + 2 + lane] = toutc;
             }
             dch = dnx;
             lch = lnx;
@@ -1465,19 +1515,23 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
 // 16-byte aligned block of codes last read is kept in registers: a diagonal
 // run stays in it for up to four steps.
 // ---------------------------------------------------------------------------
-template <int R>
+// SW = 16: the fp64 kernel's segment pairs (idx[0 .. npairs)), whose codes have the stripe layout of 16 lanes; SW = 64
+// skips them (d.pad[1]).
+template <int R, int SW = 64>
 __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
                                                            const uint32_t *__restrict__ tb,
                                                            sed_result *__restrict__ res,
-                                                           uint32_t *__restrict__ ops, const uint64_t pat) {
+                                                           uint32_t *__restrict__ ops, const uint64_t pat,
+                                                           const int32_t *__restrict__ idx) {
     constexpr int G = Grp<R>::G, P = Ladder<R>::P;
-    const int pair = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pair >= npairs) return;
+    const int item = blockIdx.x * blockDim.x + threadIdx.x;
+    if (item >= npairs) return;
+    const int pair = SW == 64 ? item : idx[item];
     const sed_pair_desc d = pd[pair];
-    if (d.lane) return;  // scripted by sed_lane.hip
+    if (d.lane || (SW == 64 && d.pad[1])) return;  // scripted by sed_lane.hip / by the SW = 16 launch
     const int n = d.n, m = d.m;
-    const int SG = (m + 63 + G - 1) / G * G;
-    const uint64_t stripe_words = (uint64_t)(SG / G) * 256u;
+    const int SG = (m + SW - 1 + G - 1) / G * G;
+    const uint64_t stripe_words = (uint64_t)(SG / G) * (SW * 4u);
     uint32_t *out = ops + d.ops_off;
     int q = res[pair].len;  // ops in the script; written from position q-1 down to 0
     int i = n, j = m;
@@ -1496,8 +1550,8 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
     };
     if (i > 0 && j > 0) {
         const int rr = i - 1;
-        int k = rr / (64 * R);
-        int t = (rr >> __builtin_ctz(R)) & 63;
+        int k = rr / (SW * R);
+        int t = (rr >> __builtin_ctz(R)) & (SW - 1);
         int r = rr & (R - 1);
         const uint32_t *base = tb + d.tb_off + (uint64_t)k * stripe_words;
         uint64_t cached = ~0ull;
@@ -1505,7 +1559,7 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
         while (true) {
             const int s = j - 1 + t;
             const int c = (s % G) * R + r;  // code index inside the lane's 16-byte group block
-            const uint64_t blk = ((uint64_t)(s / G) * 64u + t) * 4u;
+            const uint64_t blk = ((uint64_t)(s / G) * SW + t) * 4u;
             if (blk != cached) {
                 cached = blk;
                 cw = *reinterpret_cast<const uint4 *>(base + blk);
@@ -1521,7 +1575,7 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
                 if (--r < 0) {
                     r = R - 1;
                     if (--t < 0) {
-                        t = 63;
+                        t = SW - 1;
                         --k;
                         base -= stripe_words;
                         cached = ~0ull;
@@ -2284,6 +2338,11 @@ __global__ void sed_selftest_kernel(uint32_t *out) {
     if (p != (0xFF00FFFEu | (((0x44332211u >> (8 * (lane & 3))) & 0xFFu) << 16))) fail |= 8;
     const uint32_t ab = __builtin_amdgcn_alignbit(0x3u + (lane << 2), 0x80000000u, 2);
     if (ab != (0xE0000000u | 0x20000000u)) fail |= 16;
+    // the 16-lane segment moves of the fp64 kernel's short-pair route (row_shr:1, row_shl:1, row_ror:15)
+    const uint32_t sl = lane & 15u;
+    if (seg_shr1<16>(7u, v) != (sl == 0 ? 7u : 999u + lane)) fail |= 32;
+    if (seg_shl1<16>(9u, v) != (sl == 15 ? 9u : 1001u + lane)) fail |= 64;
+    if (seg_rol1<16>(v) != 1000u + (lane & ~15u) + ((sl + 1) & 15u)) fail |= 128;
     atomicOr(out, fail);
 }
 
@@ -2383,12 +2442,14 @@ hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm, bool l
     }
 }
 
-template <int R, bool TB, bool TYPED, bool FULL = false>
+template <int R, bool TB, bool TYPED, bool FULL = false, int SW = 64>
 static hipError_t launch_f64_R(const sed_launch &L, const double *gtab, const sed_f64_params &prm,
-                               const sed_full_out &fo = sed_full_out{}) {
-    const int grid = (L.npairs + 3) / 4;
-    SED_LAUNCH((sed_wf_f64_kernel<R, TB, TYPED, FULL>), dim3(grid), dim3(256), 0, L, L.pd, L.npairs,
-                       (const uint8_t *)L.seqa, (const uint8_t *)L.seqb, L.tb, L.bnd, L.res, gtab, prm, fo);
+                               const sed_full_out &fo = sed_full_out{}, const int32_t *idx = nullptr, int nidx = 0) {
+    const int items = SW == 64 ? L.npairs : nidx;
+    const int grid = (items * SW + 255) / 256;
+    if (items <= 0) return hipSuccess;
+    SED_LAUNCH((sed_wf_f64_kernel<R, TB, TYPED, FULL, SW>), dim3(grid), dim3(256), 0, L, L.pd, items,
+                       (const uint8_t *)L.seqa, (const uint8_t *)L.seqb, L.tb, L.bnd, L.res, gtab, prm, fo, idx);
     return hipGetLastError();
 }
 
@@ -2411,6 +2472,34 @@ hipError_t sed_launch_f64(const sed_launch &L, const double *gtab, const sed_f64
 #undef CASE
     default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t sed_launch_f64_seg(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed,
+                              const int32_t *idx, int nidx) {
+    const bool tb = L.tb != nullptr;
+    const sed_full_out none{};
+    switch (L.R) {
+#define CASE(RR)                                                                                               \
+    case RR:                                                                                                   \
+        if (typed) return tb ? launch_f64_R<RR, true, true, false, 16>(L, gtab, prm, none, idx, nidx)          \
+                             : launch_f64_R<RR, false, true, false, 16>(L, gtab, prm, none, idx, nidx);        \
+        return tb ? launch_f64_R<RR, true, false, false, 16>(L, gtab, prm, none, idx, nidx)                    \
+                  : launch_f64_R<RR, false, false, false, 16>(L, gtab, prm, none, idx, nidx);
+        CASE(4) CASE(8)
+#undef CASE
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t sed_launch_traceback_seg(const sed_launch &L, uint32_t *ops, const int32_t *idx, int nidx) {
+    if (nidx <= 0) return hipSuccess;
+    const int grid = (nidx + 63) / 64;
+    switch (L.R) {
+    case 4: SED_LAUNCH((sed_traceback_kernel<4, 16>), dim3(grid), dim3(64), 0, L, L.pd, nidx, L.tb, L.res, ops, 0ull, idx); break;
+    case 8: SED_LAUNCH((sed_traceback_kernel<8, 16>), dim3(grid), dim3(64), 0, L, L.pd, nidx, L.tb, L.res, ops, 0ull, idx); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t sed_launch_traceback_ck(const sed_launch &L, uint32_t *ops, const sed_i32_params &prm) {
@@ -2438,7 +2527,7 @@ hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops) {
                                L.npairs, L.tb, L.res, ops, pat);                                                \
         else                                                                                                     \
             SED_LAUNCH((sed_traceback_kernel<RR>), dim3(grid), dim3(64), 0, L, L.pd,              \
-                               L.npairs, L.tb, L.res, ops, pat);                                                \
+                               L.npairs, L.tb, L.res, ops, pat, nullptr);                                       \
         break;                                                                                                   \
     }
         CASE(4) CASE(8) CASE(16) CASE(32)

@@ -65,6 +65,8 @@ struct sed_ctx {
     int opt_chain_waves = 0;
     int opt_bitpar = 0;         // SED_OPT_BITPAR: 0 auto (unit-cost distance-only lane pairs), 2 never
     int opt_scaled = 0;         // SED_OPT_SCALED: 0 auto (fp64 lane pairs under dyadic costs), 2 never
+    int opt_seg = 0;            // SED_OPT_SEG: 0 auto (fp64 pairs the cost model prefers in 16-lane segments), 1 every
+                                // eligible pair, 2 never
     int opt_dot = 0;            // SED_OPT_DOT: 0 auto, 2 never (checkpoint batches keep the perm-based distance keys)    // SED_OPT_CHAIN_WAVES: cap on the persistent waves of dynamic CHAIN mode
     int opt_debug_corrupt = 0;  // SED_OPT_DEBUG_CORRUPT: pair + 1 whose sink-tile checkpoint is overwritten
     DevBuf selftest;
@@ -118,14 +120,15 @@ struct sed_batch {
     std::vector<int32_t> n, m;
     uint64_t tb_words = 0, bnd_words = 0, ops_words = 0;
     double cells = 0, algo_bytes = 0;
-    DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops, d_tasks, d_lane, d_chain, d_x2, d_tbmap;
+    DevBuf d_pd, d_seqa, d_seqb, d_bnd, d_ops, d_tasks, d_lane, d_chain, d_x2, d_tbmap, d_seg;
+    int nseg = 0;              // fp64 wave pairs in 16-lane segments (pd.pad[1]), listed in d_seg
     // small batches (fill_batch: SED_SMALL_BATCH_BYTES) keep every input array and the results in one blob, d_small;
     // the kernels' pointers (p_*) point into it or at the per-array buffers above
     DevBuf d_small;
     bool small = false;
     size_t o_ops_small = 0;  // small batches: the scripts' offset from the results in d_small
     void *p_pd = nullptr, *p_seqa = nullptr, *p_seqb = nullptr, *p_tasks = nullptr, *p_lane = nullptr,
-         *p_chain = nullptr, *p_x2 = nullptr, *p_ops = nullptr, *p_res[3] = {nullptr, nullptr, nullptr};
+         *p_chain = nullptr, *p_x2 = nullptr, *p_ops = nullptr, *p_seg = nullptr, *p_res[3] = {nullptr, nullptr, nullptr};
     // timing events: 1 on every run (default), k > 1 on every k-th run, 0 never (sed_batch_set_timing; runs that
     // order buffer reuse through their events always record them)
     int time_every = 1;
@@ -185,7 +188,7 @@ struct sed_batch {
     int cur() const { return (int)((runs - 1) % nbuf); }
     ~sed_batch() {
         d_pd.release(); d_seqa.release(); d_seqb.release(); d_bnd.release(); d_ops.release(); d_tbmap.release();
-        d_tasks.release(); d_lane.release(); d_chain.release(); d_x2.release(); d_small.release();
+        d_tasks.release(); d_lane.release(); d_chain.release(); d_x2.release(); d_small.release(); d_seg.release();
         for (int i = 0; i < 3; ++i) {
             d_tb[i].release();
             d_res[i].release();
@@ -514,13 +517,20 @@ int choose_R(int mode, int max_n, int forced) {
 // 4.82 ms at R = 8 (profiles/r03/fp64_R.jsonl).
 // lane: the batch routes short pairs to the fp64 lane kernel (fill_batch: use_lane), which never runs the wave
 // kernel, so they are left out of the model.
-int choose_R_f64(const int32_t *len_a, const int32_t *len_b, int npairs, bool lane) {
+// seg: pairs may run in 16-lane segments, four per wave (sed_kernels.hip: sed_wf_f64_kernel SW = 16): stripes of 16 R
+// rows and a 15-step ramp, at a quarter of a wave: stripes16(R) * (m + 15) * (R + 0.6) / 4.
+double f64_cost(int n, int m, int R, int SW) {
+    return (double)((n + SW * R - 1) / (SW * R)) * (m + SW - 1) * (R + 0.6) * SW / 64.0;
+}
+bool f64_seg_better(int n, int m, int R) { return f64_cost(n, m, R, 16) < f64_cost(n, m, R, 64); }
+int choose_R_f64(const int32_t *len_a, const int32_t *len_b, int npairs, bool lane, bool seg) {
     double cost[2] = {0, 0};
     for (int p = 0; p < npairs; ++p) {
         if (lane && len_a[p] >= 1 && len_a[p] <= SED_LANE_MAXN && len_b[p] >= 1 && len_b[p] <= SED_LANE_MAXM) continue;
         for (int k = 0; k < 2; ++k) {
             const int R = 4 << k;
-            cost[k] += (double)((len_a[p] + 64 * R - 1) / (64 * R)) * (len_b[p] + 63) * (R + 0.6);
+            const double c64 = f64_cost(len_a[p], len_b[p], R, 64);
+            cost[k] += seg ? std::min(c64, f64_cost(len_a[p], len_b[p], R, 16)) : c64;
         }
     }
     return cost[1] < cost[0] ? 8 : 4;
@@ -597,8 +607,15 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     }
     // fp64 batches whose short pairs go to the lane kernel (use_lane below: distance only, simple typing)
     const bool f64_lane = c->opt_lane != 2 && !(flags & SED_WANT_SCRIPT) && (flags & SED_NO_LEN) && simple_typing(c);
+    // fp64 batches of more than 256 wave pairs may run short pairs in 16-lane segments (SED_OPT_SEG; the window
+    // traceback of smaller batches reads the 64-lane layout only)
+    int nwave_f64 = 0;
+    for (int p = 0; p < npairs; ++p)
+        if (len_a[p] > 0 && len_b[p] > 0 && !(f64_lane && len_a[p] <= SED_LANE_MAXN && len_b[p] <= SED_LANE_MAXM))
+            ++nwave_f64;
+    const bool seg_ok = c->opt_seg != 2 && nwave_f64 > 256;
     int R = (mode == SED_MODE_I32 || c->opt_R) ? choose_R(mode, max_n, c->opt_R)
-                                                : choose_R_f64(len_a, len_b, npairs, f64_lane && mode == SED_MODE_F64);
+                                                : choose_R_f64(len_a, len_b, npairs, f64_lane && mode == SED_MODE_F64, seg_ok);
     if (mode == SED_MODE_I32) {
         const int ROWS = 64 * R;
         bool fits = true;
@@ -613,7 +630,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         if (!fits) {
             if (c->opt_mode == 1) return c->fail(SED_E_RANGE, "integer key would overflow (D < 2^16, L < 2^14)");
             mode = simple_typing(c) ? SED_MODE_F64 : SED_MODE_F64_TYPED;
-            R = c->opt_R ? c->opt_R : choose_R_f64(len_a, len_b, npairs, f64_lane && mode == SED_MODE_F64);
+            R = c->opt_R ? c->opt_R : choose_R_f64(len_a, len_b, npairs, f64_lane && mode == SED_MODE_F64, seg_ok);
         }
     } else if (c->K > SED_MAX_K) {
         return c->fail(SED_E_ALPHABET, "alphabet of %d symbols exceeds %d", c->K, SED_MAX_K);
@@ -660,7 +677,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // ---- layout ----
     b->pd.assign(npairs, sed_pair_desc{});
     std::vector<int2> tasks;
-    std::vector<int32_t> lane_idx;
+    std::vector<int32_t> lane_idx, seg_idx;
     // lane-per-pair kernels: integer keys (any flags), or fp64 distance-only in "simple typing" mode
     const bool use_lane = !split && c->opt_lane != 2 &&
                           (mode == SED_MODE_I32 || (mode == SED_MODE_F64 && !want_tb && (flags & SED_NO_LEN)));
@@ -690,17 +707,24 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
             lane_idx.push_back(p);
             if (want_tb) tbw += 2 * (uint64_t)nn;  // one uint2 of 2-bit ops per row
         } else if (nn > 0 && mm > 0) {
+            // fp64 pairs the cost model prefers in 16-lane segments (sed_kernels.hip: sed_wf_f64_kernel SW = 16)
+            const bool seg = !packed && seg_ok && (c->opt_seg == 1 || f64_seg_better(nn, mm, R));
+            const uint64_t SW = seg ? 16 : 64;
+            if (seg) {
+                d.pad[1] = 1;
+                seg_idx.push_back(p);
+            }
             const uint64_t G = 64 / R;  // steps per 16-byte traceback group (sed_kernels.hip: Grp)
-            const uint64_t nstripes = (nn + ROWS - 1) / ROWS;
-            const uint64_t SG = (mm + 63 + G - 1) / G * G;
-            const uint64_t nchunks = (SG + 63) / 64;
+            const uint64_t nstripes = (nn + SW * R - 1) / (SW * R);
+            const uint64_t SG = (mm + SW - 1 + G - 1) / G * G;
+            const uint64_t nchunks = (SG + SW - 1) / SW;
             if (want_tb) {  // CK: per stripe nchunks x (R+1) x 64 column checkpoints + (SG/G) x 64 row checkpoints
-                const uint64_t w = b->ck ? nstripes * (nchunks * (R + 1) * 64 + (SG / G) * SED_CK_RW) : nstripes * (SG / G) * 64 * 4;
+                const uint64_t w = b->ck ? nstripes * (nchunks * (R + 1) * 64 + (SG / G) * SED_CK_RW) : nstripes * (SG / G) * SW * 4;
                 tbw += w;
                 ck_bytes += 4.0 * (double)w;
             }
             // SPLIT: 64-bit {epoch tag, value} words per column and stripe (the tagged hand-off, sed_kernels.hip)
-            if (nstripes > 1) bndw += (nchunks + 2) * 64 * (packed ? (split ? 2 : 1) : 4) * (split ? nstripes : 1);
+            if (nstripes > 1) bndw += (nchunks + 2) * SW * (packed ? (split ? 2 : 1) : 4) * (split ? nstripes : 1);
             if (b->tbpar && nstripes >= 3) {  // {exit column, ops} per stripe and column
                 mapw += nstripes * (uint64_t)(mm + 1) * 2;
                 // workgroups of 256 columns per middle stripe, and one for the sink's stripe
@@ -727,6 +751,11 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     b->bnd_words = bndw;
     b->nlane = (int)lane_idx.size();
     b->nwave = npairs - b->nlane;
+    // segment pairs by shape, so the four pairs of a wave run alike
+    std::stable_sort(seg_idx.begin(), seg_idx.end(), [&](int32_t x, int32_t y) {
+        return len_a[x] != len_a[y] ? len_a[x] < len_a[y] : len_b[x] < len_b[y];
+    });
+    b->nseg = (int)seg_idx.size();
     // distance-only integer lane pairs: two pairs of equal n per lane (sed_lane.hip: i32x2). Stable
     // sort by n, pair neighbours of equal n; a pair without a partner shares its lane with itself.
     b->nlane_x2 = 0;
@@ -886,10 +915,12 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // rewritten before that copy has completed: pin_busy), instead of one pageable copy per array and a memset.
     const size_t s_pd = sizeof(sed_pair_desc) * std::max(1, npairs), s_tasks = sizeof(int2) * std::max<size_t>(1, tasks.size()),
                  s_chain = 4 * (chain_pairs.size() + chain_off.size() + 4), s_lane = 4 * std::max<size_t>(1, lane_idx.size()),
-                 s_x2 = 4 * std::max<size_t>(1, x2.size()), s_res = sizeof(sed_result) * std::max(1, npairs);
+                 s_x2 = 4 * std::max<size_t>(1, x2.size()), s_res = sizeof(sed_result) * std::max(1, npairs),
+                 s_seg = 4 * std::max<size_t>(1, seg_idx.size());
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t o_pd = 0, o_sa = o_pd + al(s_pd), o_sb = o_sa + al(sa), o_tasks = o_sb + al(sb), o_chain = o_tasks + al(s_tasks),
-           o_lane = o_chain + al(s_chain), o_x2 = o_lane + al(s_lane), o_res = o_x2 + al(s_x2), o_ops = o_res + al(s_res),
+           o_lane = o_chain + al(s_chain), o_x2 = o_lane + al(s_lane), o_seg = o_x2 + al(s_x2), o_res = o_seg + al(s_seg),
+           o_ops = o_res + al(s_res),
            total = o_ops + al(4 * std::max<uint64_t>(1, opw));  // (results and scripts adjacent: one download)
     b->small = b->nbuf == 1 && total <= SED_SMALL_BATCH_BYTES;
     bool okalloc = b->d_bnd.reserve(4 * std::max<uint64_t>(1, bndw)) && b->d_tbmap.reserve(4 * std::max<uint64_t>(1, mapw));
@@ -898,7 +929,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     } else {
         okalloc = okalloc && b->d_ops.reserve(4 * std::max<uint64_t>(1, opw)) && b->d_pd.reserve(s_pd) && b->d_seqa.reserve(sa) && b->d_seqb.reserve(sb) &&
                   b->d_tasks.reserve(s_tasks) && b->d_lane.reserve(s_lane) && b->d_chain.reserve(s_chain) &&
-                  b->d_x2.reserve(s_x2);
+                  b->d_x2.reserve(s_x2) && b->d_seg.reserve(s_seg);
         for (int i = 0; i < b->nbuf && okalloc; ++i) okalloc = b->d_res[i].reserve(s_res);
     }
     for (int i = 0; i < b->nbuf && okalloc; ++i) okalloc = !want_tb || b->d_tb[i].reserve(4 * std::max<uint64_t>(1, tbw));
@@ -917,6 +948,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         if (!chain_off.empty()) memcpy(h + o_chain + 4 * chain_pairs.size(), chain_off.data(), 4 * chain_off.size());
         if (!lane_idx.empty()) memcpy(h + o_lane, lane_idx.data(), 4 * lane_idx.size());
         if (!x2.empty()) memcpy(h + o_x2, x2.data(), 4 * x2.size());
+        if (!seg_idx.empty()) memcpy(h + o_seg, seg_idx.data(), 4 * seg_idx.size());
         memset(h + o_res, 0, s_res);
         if ((e = hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
             return c->hipfail(e, "upload");
@@ -928,6 +960,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         b->p_chain = d + o_chain;
         b->p_lane = d + o_lane;
         b->p_x2 = d + o_x2;
+        b->p_seg = d + o_seg;
         b->p_res[0] = d + o_res;
         b->p_ops = d + o_ops;
         b->o_ops_small = o_ops - o_res;
@@ -940,6 +973,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         b->p_chain = b->d_chain.p;
         b->p_lane = b->d_lane.p;
         b->p_x2 = b->d_x2.p;
+        b->p_seg = b->d_seg.p;
         for (int i = 0; i < 3; ++i) b->p_res[i] = b->d_res[i].p;
         if ((e = hipMemcpyAsync(b->p_pd, b->pd.data(), sizeof(sed_pair_desc) * npairs, hipMemcpyHostToDevice,
                                 c->stream)) != hipSuccess)
@@ -964,6 +998,9 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         if (!x2.empty() &&
             (e = hipMemcpyAsync(b->p_x2, x2.data(), 4 * x2.size(), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
             return c->hipfail(e, "upload packed-wave list");
+        if (!seg_idx.empty() && (e = hipMemcpyAsync(b->p_seg, seg_idx.data(), 4 * seg_idx.size(), hipMemcpyHostToDevice,
+                                                    c->stream)) != hipSuccess)
+            return c->hipfail(e, "upload segment list");
         for (int i = 0; i < b->nbuf; ++i)
             if ((e = hipMemsetAsync(b->p_res[i], 0, s_res, c->stream)) != hipSuccess) return c->hipfail(e, "zero results");
         if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hipfail(e, "upload sync");
@@ -1204,7 +1241,8 @@ int run_batch(sed_batch *b) {
     // with lg[2] / lg[3]).  An event record is a marker packet on the queue: with records around the kernels,
     // consecutive config-2 DP kernels were ~18 us apart, and for the ~25 us lane kernel (config 5) every
     // avoided packet is measurable.  A phase that launches nothing records its events directly.
-    const int ndp = (b->nwave_x2 > 0) + (b->nwave > 0) + (b->nlane > 0);
+    const int nw64 = b->nwave - b->nseg;  // wave pairs of the one-wave-per-pair kernels
+    const int ndp = (b->nwave_x2 > 0) + (nw64 > 0) + (b->nseg > 0) + (b->nlane > 0);
     int idp = 0;
     auto dp_events = [&]() {
         L.ev0 = idp == 0 ? lg[0] : nullptr;
@@ -1227,7 +1265,7 @@ int run_batch(sed_batch *b) {
         if ((e = sed_launch_i32x2(L, (const int32_t *)b->p_x2, b->nwave_x2, ip)) != hipSuccess)
             return c->hipfail(e, "packed DP kernel launch");
     }
-    if (b->nwave > 0) {
+    if (nw64 > 0) {
         dp_events();
         if (b->mode == SED_MODE_I32 && b->nchains) {
             L.chain_pairs = (const int32_t *)b->p_chain;
@@ -1249,6 +1287,12 @@ int run_batch(sed_batch *b) {
         else
             e = sed_launch_f64(L, (const double *)c->gtab.p, b->fp, b->mode == SED_MODE_F64_TYPED);
         if (e != hipSuccess) return c->hipfail(e, "DP kernel launch");
+    }
+    if (b->nseg > 0) {  // fp64 pairs in 16-lane segments, four per wave
+        dp_events();
+        if ((e = sed_launch_f64_seg(L, (const double *)c->gtab.p, b->fp, b->mode == SED_MODE_F64_TYPED,
+                                    (const int32_t *)b->p_seg, b->nseg)) != hipSuccess)
+            return c->hipfail(e, "segment DP kernel launch");
     }
     if (b->nlane > 0) {
         dp_events();
@@ -1297,8 +1341,16 @@ int run_batch(sed_batch *b) {
                 e = sed_launch_traceback_stripes(L, (uint32_t *)b->p_ops, (uint32_t *)b->d_tbmap.p, b->tbpar_items,
                                                  b->tbpar_kmax);
             } else {
-                e = b->ck ? sed_launch_traceback_ck(L, (uint32_t *)b->p_ops, ip)
-                          : sed_launch_traceback(L, (uint32_t *)b->p_ops);
+                const hipEvent_t tb_end = L.ev1;
+                if (b->nseg > 0) L.ev1 = nullptr;  // the segment pairs' traceback below ends the phase
+                e = nw64 <= 0 ? hipSuccess
+                    : b->ck   ? sed_launch_traceback_ck(L, (uint32_t *)b->p_ops, ip)
+                              : sed_launch_traceback(L, (uint32_t *)b->p_ops);
+                if (e == hipSuccess && b->nseg > 0) {
+                    L.ev0 = nw64 <= 0 ? L.ev0 : nullptr;
+                    L.ev1 = tb_end;
+                    e = sed_launch_traceback_seg(L, (uint32_t *)b->p_ops, (const int32_t *)b->p_seg, b->nseg);
+                }
             }
             if (e != hipSuccess) return c->hipfail(e, "traceback kernel launch");
         }
@@ -1445,6 +1497,10 @@ int sed_set_option(sed_ctx *c, int key, int value) {
         c->opt_bitpar = value;
         return SED_OK;
     }
+    if (key == SED_OPT_SEG && value >= 0 && value <= 2) {
+        c->opt_seg = value;
+        return SED_OK;
+    }
     if (key == SED_OPT_SCALED && (value == 0 || value == 2)) {
         c->opt_scaled = value;
         return SED_OK;
@@ -1588,6 +1644,8 @@ int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave)
 int sed_batch_bitpar_pairs(const sed_batch *b) {
     return b ? (b->lane_bitpar ? b->nlane : b->nbitpar_f64) : SED_E_ARG;
 }
+
+int sed_batch_segment_pairs(const sed_batch *b) { return b ? b->nseg : SED_E_ARG; }
 
 int sed_batch_scaled_pairs(const sed_batch *b) {
     return b ? (b->scaled ? b->nlane - b->nbitpar_f64 : 0) : SED_E_ARG;

@@ -41,6 +41,7 @@ SED_OPT_DEBUG_CORRUPT = 9
 SED_OPT_DOT = 10
 SED_OPT_BITPAR = 11
 SED_OPT_SCALED = 12
+SED_OPT_SEG = 13
 MODE_NAMES = {1: "i32", 2: "f64", 3: "f64-typed"}
 
 _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
@@ -71,6 +72,7 @@ SIGNATURES = [
     ("sed_batch_packed_pairs", C.c_int, [C.c_void_p]),
     ("sed_batch_bitpar_pairs", C.c_int, [C.c_void_p]),
     ("sed_batch_scaled_pairs", C.c_int, [C.c_void_p]),
+    ("sed_batch_segment_pairs", C.c_int, [C.c_void_p]),
     ("sed_batch_traceback_mode", C.c_int, [C.c_void_p]),
     ("sed_batch_chain_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("sed_batch_run", C.c_int, [C.c_void_p]),
@@ -357,6 +359,11 @@ class Batch:
     def scaled_pairs(self):
         """fp64 lane pairs computed as an exact integer DP of costs scaled by 2^k (dyadic tables, SED_OPT_SCALED)."""
         return self._lib.sed_batch_scaled_pairs(self.ptr)
+
+    @property
+    def segment_pairs(self):
+        """fp64 wave pairs computed in 16-lane segments, four per wave (SED_OPT_SEG)."""
+        return self._lib.sed_batch_segment_pairs(self.ptr)
 
     def run(self):
         self.ctx._check(self._lib.sed_batch_run(self.ptr), "sed_batch_run")

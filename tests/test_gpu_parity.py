@@ -691,3 +691,36 @@ def test_checkpoint_route_every_R_stripe_and_chain(gpu, tables, R, chain):
         for k in (sedgpu.SED_OPT_TB, sedgpu.SED_OPT_ROWS_PER_LANE, sedgpu.SED_OPT_CHAIN, sedgpu.SED_OPT_LANE,
                   sedgpu.SED_OPT_SPLIT):
             gpu.set_option(k, 0)
+
+
+@pytest.mark.parametrize("table_name", ["costs.json", "int_literals", "frac_indel"])
+def test_fp64_segments_vs_oracle(gpu, tables, table_name):
+    """fp64 batches of > 256 wave pairs run the pairs their cost model favours in 16-lane segments, four per wave
+    (sed_wf_f64_kernel SW = 16: row DPP moves, 16-step chunks, a 15-step ramp) with the per-cell-code traceback of
+    that layout: the timing.py sweep's short IUPAC pairs (timing.py:45-57).  Ragged pairs of 1..300 (one or more
+    16 R-row stripes, columns past a chunk), scripts and distance-only, the typed fp64 kernel (int literals) and
+    fractional indels: every pair vs the oracle, and identical to SED_OPT_SEG = 2 (no segments) and = 1 (every wave
+    pair in segments)."""
+    table = tables[False] if table_name == "costs.json" else load_golden("g8_cost_tables.json")["tables"][table_name]
+    pairs = _random_pairs(8800 + len(table_name), 420, IUPAC, 1, 300, related=True)
+    pairs += _random_pairs(8900 + len(table_name), 60, IUPAC, 33, 700)
+    pairs += [("", "ACG"), ("GUA", ""), ("", ""), ("A", "C")]  # empty sides stay on the one-wave-per-pair kernel
+    plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
+    gpu.set_costs(plan)
+    for script in (True, False):
+        b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs],
+                                                 [plan.encode(y) for _, y in pairs]), script)
+        try:
+            assert b.mode in ("f64", "f64-typed") and b.lane_pairs == 0
+            nseg = b.segment_pairs
+            assert 0 < nseg <= len(pairs) - 3, nseg
+        finally:
+            b.close()
+        got = gpu_run(gpu, table, pairs, script=script)
+        _oracle_check(table, pairs, got)
+        for opt in (2, 1):
+            gpu.set_option(sedgpu.SED_OPT_SEG, opt)
+            try:
+                assert gpu_run(gpu, table, pairs, script=script) == got, (table_name, script, opt)
+            finally:
+                gpu.set_option(sedgpu.SED_OPT_SEG, 0)
