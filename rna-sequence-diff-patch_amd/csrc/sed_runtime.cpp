@@ -527,9 +527,13 @@ int choose_R(int mode, int max_n, int forced) {
 // lane: the batch routes short pairs to the fp64 lane kernel (fill_batch: use_lane), which never runs the wave
 // kernel, so they are left out of the model.
 // seg: pairs may run in 16-lane segments, four per wave (sed_kernels.hip: sed_wf_f64_kernel SW = 16): stripes of 16 R
-// rows and a 15-step ramp, at a quarter of a wave: stripes16(R) * (m + 15) * (R + 0.6) / 4.
+// rows and a 15-step ramp, at a quarter of a wave: stripes16(R) * (m + 15) * (R + 0.6) / 4, times a penalty for the
+// segments' per-lane loop control and stripe changes, fitted to the two fp64 workloads (profiles/r04/seg/ab_seg.jsonl):
+// timing (R = 4) ran 3.34 against 4.48 ms where the bare model says 0.71 of it (penalty 1.05), iupac (1024^2, R = 8)
+// 5.41 against 4.87 ms where it says 0.96 (penalty 1.16).
 double f64_cost(int n, int m, int R, int SW) {
-    return (double)((n + SW * R - 1) / (SW * R)) * (m + SW - 1) * (R + 0.6) * SW / 64.0;
+    const double pen = SW == 16 ? (R >= 8 ? 1.16 : 1.05) : 1.0;
+    return (double)((n + SW * R - 1) / (SW * R)) * (m + SW - 1) * (R + 0.6) * SW / 64.0 * pen;
 }
 bool f64_seg_better(int n, int m, int R) { return f64_cost(n, m, R, 16) < f64_cost(n, m, R, 64); }
 int choose_R_f64(const int32_t *len_a, const int32_t *len_b, int npairs, bool lane, bool seg) {
