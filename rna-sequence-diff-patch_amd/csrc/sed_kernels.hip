@@ -2047,6 +2047,11 @@ template <int R> constexpr int ck_band_start(int sig) {
     return 0;
 }
 
+// a word at a 32-bit byte offset from a uniform base: the scalar-base (saddr) load form, no 64-bit lane address
+__device__ __forceinline__ uint32_t ld_byte_off(const uint32_t *__restrict__ base, const uint32_t off) {
+    return *(const uint32_t *)((const char *)base + off);
+}
+
 // LDS ordering inside the traceback: a workgroup barrier for the one-wave traceback kernel; WAVE: a wave-local
 // wait, for a traceback run by a wave of a larger workgroup (LDS accesses of one wave execute in order; the
 // clobber keeps the compiler from moving them across).  Fusing the traceback into the CK forward kernel this way
@@ -2095,6 +2100,7 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
         const uint32_t *rcp = ccp + sed_ck_col_words(R, nstripes, nchunks);
         const uint32_t *pa = seqa + d.a_off, *pb = seqb + d.b_off;
         const int band = lane >> LR;
+        const uint32_t cko0 = ((uint32_t)(lane & (R - 1)) * 64u + (uint32_t)band) * 4u, cko1 = (uint32_t)(R * 64 + band) * 4u;
         const int sig0 = lane - band + G - 1;  // first real sweep step of this lane (<= 63)
         // code 3 (outside the window) for the steps before sig0, OR-ed into words 0..3 once they are complete
         uint32_t hm[4];
@@ -2121,11 +2127,15 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
             // are clamped to valid words and the border cases are selects afterwards.
             const int ir = min(rowbase + lane, n - 1);  // 0-based str1 index of this lane's row (clamped)
             const uint32_t wa = pa[ir >> 4];
+            // (uniform 64-bit bases + 32-bit lane offsets: the loads take the scalar-base form and the address
+            // arithmetic stays on the scalar unit)
             uint32_t ck0 = 0, ck1 = 0;
             if (c >= 1) {  // (uniform)
-                const uint32_t *cp = ccp + sed_ck_col_word(R, k, nchunks, c - 1, lane & (R - 1), G * Q + band);
-                ck0 = cp[0];
-                ck1 = cp[(R - (lane & (R - 1))) * 64];
+                const uint32_t *cp = ccp + sed_ck_col_word(R, k, nchunks, c - 1, 0, G * Q);
+                uint32_t o0 = cko0, o1 = cko1;
+                asm volatile("" : "+v"(o0), "+v"(o1));  // (else the zero-extended offsets are hoisted as 64-bit pairs)
+                ck0 = ld_byte_off(cp, o0);
+                ck1 = ld_byte_off(cp, o1);
             }
             // the row above the tile at column J0 - G + x (x = lane, lane + 64, lane + 128 < 132): row checkpoints of
             // forward lane G*Q - 1 (or lane 63 of the stripe above); steps clamped: past SG the columns are beyond m and
@@ -2134,11 +2144,15 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
             const bool above = Q >= 1 || k >= 1;  // (uniform) else row 0: the border
             const int kr = Q >= 1 ? k : k - 1, tr = Q >= 1 ? G * Q - 1 : 63, s0r = Q >= 1 ? 64 * c - G - 1 : 64 * c + 63 - G;
             uint32_t rk[3] = {0, 0, 0}, wb[3];
+            const uint32_t *rbase = rcp + sed_ck_row_word(R, max(kr, 0), ngroups, 0, tr);  // (uniform; read when above)
 #pragma unroll
             for (int h = 0; h < 3; ++h) {
                 const int x = lane + 64 * h;
                 if (h < 2 || x < 132) {
-                    if (above) rk[h] = rcp[sed_ck_row_word(R, kr, ngroups, min(max(s0r + x, 0), SG - 1), tr)];
+                    if (above) {
+                        const uint32_t s = (uint32_t)min(max(s0r + x, 0), SG - 1);
+                        rk[h] = ld_byte_off(rbase, ((s >> (6 - LR)) * (uint32_t)SED_CK_RW + (s & (uint32_t)(G - 1))) * 4u);
+                    }
                     const int ci = min(max(J0 - (G - 1) + x - 1, 0), m - 1);
                     wb[h] = pb[ci >> 4];
                 }
