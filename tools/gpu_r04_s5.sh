@@ -5,6 +5,10 @@ set -e
 O=gpurun_out/${1:-r04s5}
 mkdir -p $O
 export TMPDIR=/tmp
+# the traceback's scalar-base loads first: every checkpoint route (R = 4, 8, 16; stripe and chain; dot keys; parts;
+# the headline route)
+timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_routes.py -m gpu -k "checkpoint or headline or dot_keys" > $O/tests_ck.log 2>&1
+tail -3 $O/tests_ck.log
 timeout -k 10 200 python3 tools/c4_timeline.py 20 > $O/timeline_default.txt 2>&1
 SED_CK_SCHED=1 timeout -k 10 200 python3 tools/c4_timeline.py 20 > $O/timeline_sched.txt 2>&1
 cat $O/timeline_default.txt $O/timeline_sched.txt
