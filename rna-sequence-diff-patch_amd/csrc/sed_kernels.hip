@@ -449,6 +449,9 @@ template <int R> struct I32Waves { static constexpr int value = R >= 32 ? 4 : (R
 #ifndef SED_CK_WAVES
 #define SED_CK_WAVES 5
 #endif
+#ifndef SED_CK_GUNROLL
+#define SED_CK_GUNROLL 2  // groups per iteration of the CK chunk loop
+#endif
 #ifdef SED_I32_WAVES_PER_EU
 #define SED_I32_WAVES(R) SED_I32_WAVES_PER_EU
 #else
@@ -689,7 +692,7 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                 }
             };
             if (CK && c != c_cap) {
-#pragma unroll 2
+#pragma unroll SED_CK_GUNROLL
                 for (int g = 0; g < 64 / G; ++g) {
                     const int s0 = 64 * c + g * G;  // (s0 & 63 folds to g * G)
                     i32_group<R, TB, LEN, false, CK, DOT>(V, cv, top_prev, bottom, selv, lch, lsel + g * G, outc, W, s0, lane,

@@ -10,6 +10,6 @@ for r in $(seq 1 $N); do
   for V in "$@"; do
     if [ "$V" = "-" ]; then EV=""; else EV="$V"; fi
     env $EV timeout -k 10 200 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --traffic none ${AB_ARGS} > $O/ab.json 2>> $O/ab.log
-    python3 -c "import json; d=json.load(open('$O/ab.json')); print(json.dumps({'env':'$V','round':$r,'value':d['value'],'dp_ms':d['roofline']['kernel_ms'],'valid':d.get('script_valid_rate'),'exact':d.get('script_exact_rate'),'tb_ms':d.get('traceback_ms'),'step_ms':d['ms_per_step']}))" >> $O/ab.jsonl
+    python3 -c "import json; d=json.load(open('$O/ab.json')); print(json.dumps({'env':'$V','round':$r,'value':d['value'],'dp_ms':d['roofline'].get('kernel_ms_per_step', d['roofline'].get('kernel_ms')),'valid':d.get('script_valid_rate'),'exact':d.get('script_exact_rate'),'tb_ms':d.get('traceback_ms'),'step_ms':d['ms_per_step']}))" >> $O/ab.jsonl
   done
 done

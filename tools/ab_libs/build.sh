@@ -1,7 +1,8 @@
 #!/bin/bash
-# libsed.so variants with the CK forward kernel's waves-per-SIMD target (SED_CK_WAVES) at 4, 5 and 6
+# libsed.so variants for interleaved A/Bs (tools/ab2.sh): the CK forward kernel's groups per chunk-loop iteration
+# (SED_CK_GUNROLL, default 2) at 4 and 8
 set -e
 cd "$(dirname "$0")/../../rna-sequence-diff-patch_amd/csrc"
-for w in 4 5 6; do
-  make -s OBJ=sed_kernels_w$w.o OUT=../../tools/ab_libs/libsed_w$w.so EXTRA="-DSED_CK_WAVES=$w" ../../tools/ab_libs/libsed_w$w.so
+for u in 4 8; do
+  make -s OBJ=sed_kernels_u$u.o OUT=../../tools/ab_libs/libsed_u$u.so EXTRA="-DSED_CK_GUNROLL=$u" ../../tools/ab_libs/libsed_u$u.so
 done

@@ -9,6 +9,9 @@ export TMPDIR=/tmp
 # the headline route)
 timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_routes.py -m gpu -k "checkpoint or headline or dot_keys" > $O/tests_ck.log 2>&1
 tail -3 $O/tests_ck.log
+# CK chunk loop: 2 (default), 4 or 8 groups per iteration, interleaved
+timeout -k 10 400 bash tools/ab2.sh ${1:-r04s5}/unroll 2 rna-sequence-diff-patch_amd/libsed.so tools/ab_libs/libsed_u4.so tools/ab_libs/libsed_u8.so
+cat $O/unroll/ab.jsonl
 timeout -k 10 200 python3 tools/c4_timeline.py 20 > $O/timeline_default.txt 2>&1
 SED_CK_SCHED=1 timeout -k 10 200 python3 tools/c4_timeline.py 20 > $O/timeline_sched.txt 2>&1
 cat $O/timeline_default.txt $O/timeline_sched.txt
