@@ -162,11 +162,6 @@ struct sed_batch {
     int nparts = 1;
     hipStream_t part_stream[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_start = nullptr;
-    // SED_CK_SCHED=1 (A/B): every part's forward on the context's stream, back to back, and part i's traceback on
-    // part_stream[i] after it; fwd_done / tb_done order a part's traceback after its forward and the next run's
-    // forward of that part after its traceback
-    bool sched = false;
-    hipEvent_t fwd_done[3] = {nullptr, nullptr, nullptr}, tb_done[3] = {nullptr, nullptr, nullptr};
     // per event-log entry: the {dp start, dp end, tb start, tb end} events of parts 1..3 (created on first use)
     std::vector<std::array<hipEvent_t, 12>> plog;
     // per buffer: the event-log entry of the last run that used it (handles copied from `log`)
@@ -203,10 +198,6 @@ struct sed_batch {
         for (hipStream_t &ps : part_stream)
             if (ps) (void)hipStreamDestroy(ps);
         if (ev_start) (void)hipEventDestroy(ev_start);
-        for (int i = 0; i < 3; ++i) {
-            if (fwd_done[i]) (void)hipEventDestroy(fwd_done[i]);
-            if (tb_done[i]) (void)hipEventDestroy(tb_done[i]);
-        }
         for (auto &a : plog)
             for (hipEvent_t e : a)
                 if (e) (void)hipEventDestroy(e);
@@ -1119,59 +1110,12 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     b->nparts = 1;
     if (b->ck && b->nchains == 0 && b->nbuf == 1 && b->nwave_x2 == 0)
         b->nparts = std::max(1, std::min(want, b->nwave / 1024));
-    static const int sched_env = [] { const char *e = getenv("SED_CK_SCHED"); return e ? atoi(e) : 0; }();
-    b->sched = sched_env == 1 && b->nparts > 1 && b->nparts <= 3 && b->nlane == 0;
-    for (int i = 0; i + (b->sched ? 0 : 1) < b->nparts; ++i)
+    for (int i = 0; i + 1 < b->nparts; ++i)
         if (!b->part_stream[i] && (e = hipStreamCreateWithFlags(&b->part_stream[i], hipStreamNonBlocking)) != hipSuccess)
             return c->hipfail(e, "part stream");
-    for (int i = 0; b->sched && i < b->nparts; ++i)
-        if ((!b->fwd_done[i] && (e = hipEventCreateWithFlags(&b->fwd_done[i], hipEventDisableTiming)) != hipSuccess) ||
-            (!b->tb_done[i] && (e = hipEventCreateWithFlags(&b->tb_done[i], hipEventDisableTiming)) != hipSuccess))
-            return c->hipfail(e, "event create");
     if (b->nparts > 1 && !b->ev_start && (e = hipEventCreateWithFlags(&b->ev_start, hipEventDisableTiming)) != hipSuccess)
         return c->hipfail(e, "event create");
     if (b->nparts > 1 && (e = grow_log(b, 0)) != hipSuccess) return c->hipfail(e, "event create");  // the parts' entries
-    return SED_OK;
-}
-
-// SED_CK_SCHED=1: the parts' forwards back to back on the context's stream, part i's traceback on part_stream[i] after
-// its forward; the next run's forward of part i waits for that traceback (it rewrites the part's checkpoints).  No
-// lane pairs (fill_batch keeps such batches on the default schedule) and no debug corruption.
-int run_batch_sched(sed_batch *b, const std::array<hipEvent_t, 4> &lg, sed_launch L, const sed_i32_params &ip,
-                    bool len) {
-    sed_ctx *c = b->ctx;
-    hipError_t e;
-    const int P = b->nparts;
-    auto first = [&](int i) { return (int)((int64_t)b->npairs * i / P); };
-    std::array<hipEvent_t, 12> pl{};
-    if (lg[0]) {
-        const size_t li = b->nlog - 1;
-        if (b->plog.size() <= li) return c->fail(SED_E_STATE, "parts event log not grown");
-        pl = b->plog[li];
-    }
-    for (int i = 0; i < P; ++i) {
-        sed_launch Li = L;
-        Li.pd = L.pd + first(i);
-        Li.res = L.res + first(i);
-        Li.npairs = first(i + 1) - first(i);
-        Li.stream = c->stream;
-        Li.ev0 = i == 0 ? lg[0] : pl[4 * (i - 1)];
-        Li.ev1 = i == 0 ? lg[1] : pl[4 * (i - 1) + 1];
-        if ((e = hipStreamWaitEvent(c->stream, b->tb_done[i], 0)) != hipSuccess) return c->hipfail(e, "stream wait");
-        if ((e = sed_launch_i32(Li, ip, len)) != hipSuccess) return c->hipfail(e, "DP kernel launch");
-        if ((e = hipEventRecord(b->fwd_done[i], c->stream)) != hipSuccess) return c->hipfail(e, "event record");
-        const hipStream_t ts = b->part_stream[i];
-        if ((e = hipStreamWaitEvent(ts, b->fwd_done[i], 0)) != hipSuccess) return c->hipfail(e, "stream wait");
-        Li.stream = ts;
-        Li.ev0 = i == 0 ? lg[2] : pl[4 * (i - 1) + 2];
-        Li.ev1 = i == 0 ? lg[3] : pl[4 * (i - 1) + 3];
-        if ((e = sed_launch_traceback_ck(Li, (uint32_t *)b->p_ops, ip)) != hipSuccess)
-            return c->hipfail(e, "traceback kernel launch");
-        if ((e = hipEventRecord(b->tb_done[i], ts)) != hipSuccess) return c->hipfail(e, "event record");
-    }
-    b->evk[0] = lg;
-    ++b->runs;
-    b->ran = true;
     return SED_OK;
 }
 
@@ -1192,7 +1136,6 @@ int run_batch_parts(sed_batch *b, const std::array<hipEvent_t, 4> &lg, sed_launc
     const int P = b->nparts;
     auto stream = [&](int i) { return i == 0 ? c->stream : b->part_stream[i - 1]; };
     auto first = [&](int i) { return (int)((int64_t)b->npairs * i / P); };
-    if (b->sched) return run_batch_sched(b, lg, L, ip, len);
     // the other streams start after everything queued before this run (uploads, the previous run's part 0)
     if ((e = hipEventRecord(b->ev_start, c->stream)) != hipSuccess) return c->hipfail(e, "stream fork");
     for (int i = 1; i < P; ++i)

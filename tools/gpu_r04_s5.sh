@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4: c4 schedule A/B (SED_CK_SCHED=1: forwards back to back on one stream vs the default staggered parts) with
+# Round 4: c4 schedule A/B (SED_CK_SCHED=1, since removed: forwards back to back on one stream vs the default staggered parts) with
 # the parts timeline, and the fp64 segment cost model's picks (timing, iupac, timing at R = 8)
 set -e
 O=gpurun_out/${1:-r04s5}
