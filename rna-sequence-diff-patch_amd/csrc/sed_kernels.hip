@@ -1243,6 +1243,12 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
 // optional int-typing bit T (TYPED).  Cost table in LDS:
 //   tab[a*K + b] = {cost value, is-int flag}
 // ---------------------------------------------------------------------------
+// Path-length keys of the fp64 kernel in U-space: LK = SED_F64_LB - 4U (U = updates on the canonical path to the
+// cell, so L = i + j - U) with the op in the low 2 bits of a candidate.  At a cell every candidate's L is the cell's
+// i + j - U, so comparing B - 4U orders candidates exactly as L does, and the borders are all B: the insert
+// candidate is LK_left (op 0), the delete candidate LK_up + 1, the update candidate LK_diag - 4 + 2.  (L << 2 keys
+// took an add per candidate, +4, +5, +6: 21.25 against 20.25 VALU per cell on the R = 8 group loop's unmasked path.)
+#define SED_F64_LB 0x80000000u
 struct f64_cell_in {
     double d;
     uint32_t lk;
@@ -1254,20 +1260,18 @@ __device__ __forceinline__ void f64_step(double (&D)[R], uint32_t (&LK)[R], uint
                                          const uint32_t (&rowbase)[R], const double2 *__restrict__ tab,
                                          double &dtop_prev, uint32_t &ltop_prev, uint32_t &ttop_prev,
                                          double &dbot, uint32_t &lbot, uint32_t &tbot, uint32_t &bsel,
-                                         double &dch, uint32_t &lch, uint32_t &tch, uint32_t &sch, double &doutc,
-                                         uint32_t &loutc, uint32_t &toutc, uint32_t (&W)[4], const int u,
+                                         const double dtin, const uint32_t ltin, const uint32_t ttin,
+                                         const uint32_t stin, uint32_t (&W)[4], const int u,
                                          const double cins, const double cdel, const uint32_t tins,
                                          const uint32_t tdel, const bool active, const sed_full_out &fo,
                                          const int i0, const int j) {
-    const double dtop = seg_shr1_f64<SW>(dch, dbot);
-    const uint32_t ltop = seg_shr1<SW>(lch, lbot);
+    // the segment's first lane takes this step's top-row cell and column symbol (dtin .. stin, broadcast LDS reads of
+    // the chunk), the others the lane above's bottom cell and previous symbol
+    const double dtop = seg_shr1_f64<SW>(dtin, dbot);
+    const uint32_t ltop = seg_shr1<SW>(ltin, lbot);
     uint32_t ttop = 0;
-    if constexpr (TYPED) ttop = seg_shr1<SW>(tch, tbot);
-    bsel = seg_shr1<SW>(sch, bsel);
-    dch = seg_rol1_f64<SW>(dch);
-    lch = seg_rol1<SW>(lch);
-    if constexpr (TYPED) tch = seg_rol1<SW>(tch);
-    sch = seg_rol1<SW>(sch);
+    if constexpr (TYPED) ttop = seg_shr1<SW>(ttin, tbot);
+    bsel = seg_shr1<SW>(stin, bsel);
     double dup = dtop, ddiag = dtop_prev;
     uint32_t lup = ltop, ldiag = ltop_prev, tup = ttop, tdiag = ttop_prev;
 #pragma unroll
@@ -1279,9 +1283,9 @@ __device__ __forceinline__ void f64_step(double (&D)[R], uint32_t (&LK)[R], uint
         const double cc = ddiag + e.x;
         const double mn = fmin(ca, fmin(cb, cc));
         const bool ea = (ca == mn), eb = (cb == mn), ec = (cc == mn);
-        const uint32_t ka = ea ? LK[r] + 4u : 0xFFFFFFFFu;
-        const uint32_t kb = eb ? lup + 5u : 0xFFFFFFFFu;
-        const uint32_t kc = ec ? ldiag + 6u : 0xFFFFFFFFu;
+        const uint32_t ka = ea ? LK[r] : 0xFFFFFFFFu;  // (U-space keys: the insert candidate needs no add)
+        const uint32_t kb = eb ? lup + 1u : 0xFFFFFFFFu;
+        const uint32_t kc = ec ? ldiag - 2u : 0xFFFFFFFFu;
         const uint32_t km = umin3_op(ka, kb, kc);
         const uint32_t ln = km & ~3u;
         uint32_t tn = 0;
@@ -1329,10 +1333,16 @@ __device__ __forceinline__ void f64_step(double (&D)[R], uint32_t (&LK)[R], uint
     dbot = D[R - 1];
     lbot = LK[R - 1];
     if constexpr (TYPED) tbot = T[R - 1];
-    doutc = seg_shl1_f64<SW>(dbot, doutc);
-    loutc = seg_shl1<SW>(lbot, loutc);
-    if constexpr (TYPED) toutc = seg_shl1<SW>(tbot, toutc);
 }
+
+// Per wave: the current chunk's top row (cell values, L keys, typing) and str2 symbols, which the segment's first lane
+// reads one per step, and the segment's last lane's bottom cells of the chunk, which it writes one per step (the
+// next stripe's top row, stored to global memory at the chunk's end).  These replace DPP rotations of the chunk
+// values and a DPP collection of the bottom cells: 8-11 VALU per step.
+struct f64_chunk_lds {
+    double d[64], od[64];
+    uint32_t l[64], t[64], s[64], ol[64], ot[64];
+};
 
 // SW = 64: one wave per pair (pairs with d.seg set are skipped: they run in segments).  SW = 16 (short pairs of
 // large batches): each DPP row of 16 lanes runs its own pair (items idx[0 .. nidx), four per wave, the
@@ -1352,6 +1362,7 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
     constexpr int G = Grp<R>::G;
     static_assert(SW % G == 0, "a group of G steps never crosses a chunk");
     __shared__ double2 tab[SED_MAX_K * SED_MAX_K];
+    __shared__ f64_chunk_lds chx[4];
     const int K = prm.K;
     for (int e = threadIdx.x; e < K * K; e += blockDim.x)
         tab[e] = make_double2(gtab[2 * e], gtab[2 * e + 1]);
@@ -1415,14 +1426,14 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
             const uint32_t a = (ri < n) ? pa[ri] : 0u;
             rowbase[r] = a * (uint32_t)K;
             D[r] = (double)(ri + 1) * prm.del;
-            LK[r] = (uint32_t)(ri + 1) << 2;
+            LK[r] = SED_F64_LB;
             T[r] = tdel;
         }
         double dtop_prev = (double)row0 * prm.del;
-        uint32_t ltop_prev = (uint32_t)row0 << 2;
+        uint32_t ltop_prev = SED_F64_LB;
         uint32_t ttop_prev = (row0 == 0) ? 1u : tdel;
-        double dbot = 0.0, doutc = 0.0;
-        uint32_t lbot = 0, tbot = 0, bsel = 0, loutc = 0, toutc = 0;
+        double dbot = 0.0;
+        uint32_t lbot = 0, tbot = 0, bsel = 0;
         uint32_t W[4] = {0, 0, 0, 0};
 
         auto load_d = [&](int c) -> double {
@@ -1432,7 +1443,7 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
         };
         auto load_l = [&](int c) -> uint32_t {
             const int j = SW * c + lane + 1;
-            if (k == 0) return (uint32_t)j << 2;
+            if (k == 0) return SED_F64_LB;
             return load_sc1(bndL + j + SW);
         };
         auto load_t = [&](int c) -> uint32_t {
@@ -1445,6 +1456,9 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
         };
         double dch = load_d(0);
         uint32_t lch = load_l(0), tch = TYPED ? load_t(0) : 0u, sch = load_sel(0);
+        f64_chunk_lds &cx = chx[threadIdx.x >> 6];
+        const int sb = (threadIdx.x & 63) - lane;  // the segment's first slot
+        const bool lastlane = lane == SW - 1;
         uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * (SW * 4u);
         const bool last = (k == nstripes - 1);
         int s = 0;
@@ -1457,32 +1471,45 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
                 if (TYPED) tnx = load_t(c + 1);
                 snx = load_sel(c + 1);
             }
+            // this chunk's top row and symbols (after the previous chunk's last reads: a wave's LDS accesses run in
+            // order)
+            cx.d[sb + lane] = dch;
+            cx.l[sb + lane] = lch;
+            if (TYPED) cx.t[sb + lane] = tch;
+            cx.s[sb + lane] = sch;
             // (A separate loop for chunks of unmasked steps, as in the integer kernels, measured slower: iupac DP
             // 4.89 against 4.81 ms, timing 4.60 against 4.47 ms; profiles/r03/f64_plain_dropped.)
             for (int g = 0; g < SW / G && s < SG; ++g, s += G) {
                 const bool full = (s >= SW - 1) && (s + G - 1 < m);
+                const int cu0 = sb + g * G;
 #pragma unroll
                 for (int u = 0; u < G; ++u) {
                     const int j = s + u - lane + 1;
                     const bool active = (j >= 1) && (j <= m);
+                    const double dtin = cx.d[cu0 + u];
+                    const uint32_t ltin = cx.l[cu0 + u], ttin = TYPED ? cx.t[cu0 + u] : 0u, stin = cx.s[cu0 + u];
                     if (full)
                         f64_step<R, TB, TYPED, false, FULL, SW>(D, LK, T, rowbase, tab, dtop_prev, ltop_prev, ttop_prev,
-                                                                dbot, lbot, tbot, bsel, dch, lch, tch, sch, doutc, loutc,
-                                                                toutc, W, u, prm.ins, prm.del, tins, tdel, active, fo,
-                                                                row0 + 1, j);
+                                                                dbot, lbot, tbot, bsel, dtin, ltin, ttin, stin, W, u,
+                                                                prm.ins, prm.del, tins, tdel, active, fo, row0 + 1, j);
                     else
                         f64_step<R, TB, TYPED, true, FULL, SW>(D, LK, T, rowbase, tab, dtop_prev, ltop_prev, ttop_prev,
-                                                               dbot, lbot, tbot, bsel, dch, lch, tch, sch, doutc, loutc,
-                                                               toutc, W, u, prm.ins, prm.del, tins, tdel, active, fo,
-                                                               row0 + 1, j);
+                                                               dbot, lbot, tbot, bsel, dtin, ltin, ttin, stin, W, u,
+                                                               prm.ins, prm.del, tins, tdel, active, fo, row0 + 1, j);
+                    if (!last && lastlane) {  // the next stripe's top row
+                        cx.od[cu0 + u] = dbot;
+                        cx.ol[cu0 + u] = lbot;
+                        if (TYPED) cx.ot[cu0 + u] = tbot;
+                    }
                 }
                 if constexpr (TB) store_tb(tbk + ((uint64_t)(s / G) * SW + lane) * 4u, W);
             }
-            // lane i holds the segment's last lane's bottom cell of step s - SW + i, i.e. column s - 2 SW + 2 + i
-            if (!last) {
-                bndD[s - SW + 2 + lane] = (uint64_t)__double_as_longlong(doutc);
-                bndL[s - SW + 2 + lane] = loutc;
-                if (TYPED) bndT[s - SW + 2 + lane] = toutc;
+            // slot i holds the segment's last lane's bottom cell of the chunk's step SW c + i, i.e. column
+            // SW (c - 1) + 2 + i at index SW c + 2 + i (a short last chunk: only its steps' slots)
+            if (!last && lane < s - SW * c) {
+                bndD[SW * c + 2 + lane] = (uint64_t)__double_as_longlong(cx.od[sb + lane]);
+                bndL[SW * c + 2 + lane] = cx.ol[sb + lane];
+                if (TYPED) bndT[SW * c + 2 + lane] = cx.ot[sb + lane];
             }
             dch = dnx;
             lch = lnx;
@@ -1503,7 +1530,7 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
                     tv = (r == rf) ? T[r] : tv;
                 }
                 res[pair].dist = dv;
-                res[pair].len = (int32_t)(lv >> 2);
+                res[pair].len = n + m - (int32_t)((SED_F64_LB - lv) >> 2);
                 res[pair].is_int = TYPED ? (uint8_t)tv : (uint8_t)(dv == 0.0);
                 res[pair].err = 0;
             }

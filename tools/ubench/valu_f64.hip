@@ -1,0 +1,81 @@
+// Microbenchmark: wave64 issue cost of the fp64 DP cell's instructions on gfx950 (v_add_f64, v_min_f64,
+// v_cmp_eq_f64, v_cmp_eq_u64) against the 32-bit ops around them (v_cndmask_b32, v_add_u32, v_min3_u32, a DPP move),
+// 8 independent instructions per body, 8 and 4 waves per SIMD.  Output: cycles per wave instruction per SIMD.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#define ITERS 1024
+#define A8(M) M("%0") M("%1") M("%2") M("%3") M("%4") M("%5") M("%6") M("%7")
+#define ADDF(x) "v_add_f64 " x ", " x ", %8\n"
+#define MINF(x) "v_min_f64 " x ", " x ", %8\n"
+#define CMPF(x) "v_cmp_eq_f64 vcc, " x ", %8\n"
+#define CMPU(x) "v_cmp_eq_u64 vcc, " x ", %8\n"
+#define ADDU(x) "v_add_u32 " x ", " x ", %8\n"
+#define CND(x) "v_cndmask_b32 " x ", " x ", %8, vcc\n"
+#define MIN3(x) "v_min3_u32 " x ", " x ", %8, %9\n"
+#define DPP(x) "v_mov_b32_dpp " x ", %8 row_shr:1 row_mask:0xf bank_mask:0xf\n"
+// the fp64 cell's core: 3 adds, 2 mins, 3 compares (a cell per 8 instructions)
+#define CELL "v_add_f64 %0, %0, %8\n v_add_f64 %1, %1, %9\n v_add_f64 %2, %2, %8\n v_min_f64 %3, %1, %2\n" \
+             "v_min_f64 %3, %0, %3\n v_cmp_eq_f64 vcc, %0, %3\n v_cmp_eq_f64 s[0:1], %1, %3\n v_cmp_eq_f64 s[2:3], %2, %3\n"
+template <int V> __device__ __forceinline__ void body(double (&a)[8], uint32_t (&u)[8], double c1, double c2, uint32_t k1,
+                                                      uint32_t k2) {
+#define DREGS "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7])
+#define UREGS "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7])
+    if constexpr (V == 0) asm volatile(A8(ADDF) : DREGS : "v"(c1), "v"(c2));
+    if constexpr (V == 1) asm volatile(A8(MINF) : DREGS : "v"(c1), "v"(c2));
+    if constexpr (V == 2) asm volatile(A8(CMPF) : DREGS : "v"(c1), "v"(c2) : "vcc");
+    if constexpr (V == 3) asm volatile(A8(CMPU) : DREGS : "v"(c1), "v"(c2) : "vcc");
+    if constexpr (V == 4) asm volatile(A8(ADDU) : UREGS : "v"(k1), "v"(k2));
+    if constexpr (V == 5) asm volatile(A8(CND) : UREGS : "v"(k1), "v"(k2) : "vcc");
+    if constexpr (V == 6) asm volatile(A8(MIN3) : UREGS : "v"(k1), "v"(k2));
+    if constexpr (V == 7) asm volatile(A8(DPP) : UREGS : "v"(k1), "v"(k2));
+    if constexpr (V == 8) asm volatile(CELL : DREGS : "v"(c1), "v"(c2) : "vcc", "s0", "s1", "s2", "s3");
+}
+static const char *NAMES[] = {"v_add_f64", "v_min_f64", "v_cmp_eq_f64", "v_cmp_eq_u64", "v_add_u32", "v_cndmask_b32",
+                              "v_min3_u32", "v_mov_b32_dpp", "fp64 cell core (3 add, 2 min, 3 cmp)"};
+template <int V> __global__ __launch_bounds__(256) void k(uint32_t *out, uint32_t seed) {
+    double a[8];
+    uint32_t u[8];
+    for (int i = 0; i < 8; ++i) {
+        a[i] = (double)(seed + threadIdx.x + i);
+        u[i] = seed + threadIdx.x + i;
+    }
+    const double c1 = 0.25 * seed, c2 = 0.5 + seed;
+    const uint32_t k1 = seed * 3 + threadIdx.x, k2 = seed ^ threadIdx.x;
+    for (int it = 0; it < ITERS; ++it) body<V>(a, u, c1, c2, k1, k2);
+    double x = 0;
+    uint32_t y = 0;
+    for (int i = 0; i < 8; ++i) {
+        x += a[i];
+        y ^= u[i];
+    }
+    if (x == 1.2345 || y == 0x12345678u) out[0] = 1;
+}
+typedef void (*kfn)(uint32_t *, uint32_t);
+template <int... I> struct L { static constexpr kfn f[] = {k<I>...}; };
+int main() {
+    uint32_t *d;
+    (void)hipMalloc(&d, 4);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    using LL = L<0, 1, 2, 3, 4, 5, 6, 7, 8>;
+    const int nops = 9;
+    for (int wps : {8, 4}) {
+        const int blocks = 256 * wps;
+        for (int op = 0; op < nops; ++op) {
+            hipLaunchKernelGGL(LL::f[op], dim3(blocks), dim3(256), 0, 0, d, 1u);
+            (void)hipDeviceSynchronize();
+            (void)hipEventRecord(e0);
+            for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(LL::f[op], dim3(blocks), dim3(256), 0, 0, d, 1u);
+            (void)hipEventRecord(e1);
+            (void)hipEventSynchronize(e1);
+            float ms;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            const double winstr = 5.0 * blocks * 4.0 * ITERS * 8;
+            const double cyc = (ms * 1e6) * 2.4 / (winstr / 1024.0);
+            printf("waves/SIMD %d  %-40s %.2f cycles/instr\n", wps, NAMES[op], cyc);
+        }
+    }
+    return 0;
+}
