@@ -14,6 +14,9 @@
 #define CND(x) "v_cndmask_b32 " x ", " x ", %8, vcc\n"
 #define MIN3(x) "v_min3_u32 " x ", " x ", %8, %9\n"
 #define DPP(x) "v_mov_b32_dpp " x ", %8 row_shr:1 row_mask:0xf bank_mask:0xf\n"
+#define CNDS(x) "v_cndmask_b32 " x ", " x ", %8, s[4:5]\n"
+// a compare into VCC and the select that reads it, as in the fp64 cell (the pairs are independent)
+#define CMPCND(x) "v_cmp_eq_u32 vcc, " x ", %9\n v_cndmask_b32 " x ", -1, " x ", vcc\n"
 // the fp64 cell's core: 3 adds, 2 mins, 3 compares (a cell per 8 instructions)
 #define CELL "v_add_f64 %0, %0, %8\n v_add_f64 %1, %1, %9\n v_add_f64 %2, %2, %8\n v_min_f64 %3, %1, %2\n" \
              "v_min_f64 %3, %0, %3\n v_cmp_eq_f64 vcc, %0, %3\n v_cmp_eq_f64 s[0:1], %1, %3\n v_cmp_eq_f64 s[2:3], %2, %3\n"
@@ -30,9 +33,14 @@ template <int V> __device__ __forceinline__ void body(double (&a)[8], uint32_t (
     if constexpr (V == 6) asm volatile(A8(MIN3) : UREGS : "v"(k1), "v"(k2));
     if constexpr (V == 7) asm volatile(A8(DPP) : UREGS : "v"(k1), "v"(k2));
     if constexpr (V == 8) asm volatile(CELL : DREGS : "v"(c1), "v"(c2) : "vcc", "s0", "s1", "s2", "s3");
+    if constexpr (V == 9) asm volatile("s_mov_b64 s[4:5], -1\n" A8(CNDS) : UREGS : "v"(k1), "v"(k2) : "s4", "s5");
+    if constexpr (V == 10) asm volatile("s_mov_b64 vcc, -1\n" A8(CND) : UREGS : "v"(k1), "v"(k2) : "vcc");
+    if constexpr (V == 11) asm volatile(CMPCND("%0") CMPCND("%1") CMPCND("%2") CMPCND("%3") : UREGS : "v"(k1), "v"(k2) : "vcc");
 }
 static const char *NAMES[] = {"v_add_f64", "v_min_f64", "v_cmp_eq_f64", "v_cmp_eq_u64", "v_add_u32", "v_cndmask_b32",
-                              "v_min3_u32", "v_mov_b32_dpp", "fp64 cell core (3 add, 2 min, 3 cmp)"};
+                              "v_min3_u32", "v_mov_b32_dpp", "fp64 cell core (3 add, 2 min, 3 cmp)",
+                              "v_cndmask_b32 (SGPR-pair mask)", "v_cndmask_b32 (vcc set by s_mov)",
+                              "v_cmp_eq_u32 vcc + v_cndmask_b32 (pairs)"};
 template <int V> __global__ __launch_bounds__(256) void k(uint32_t *out, uint32_t seed) {
     double a[8];
     uint32_t u[8];
@@ -59,8 +67,8 @@ int main() {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    using LL = L<0, 1, 2, 3, 4, 5, 6, 7, 8>;
-    const int nops = 9;
+    using LL = L<0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11>;
+    const int nops = 12;
     for (int wps : {8, 4}) {
         const int blocks = 256 * wps;
         for (int op = 0; op < nops; ++op) {
