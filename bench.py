@@ -509,6 +509,8 @@ def main():
                     help="unit-cost distance-only lane pairs on the DP lane kernels instead of bit-parallel (A/B)")
     ap.add_argument("--seg", type=int, default=0,
                     help="SED_OPT_SEG: fp64 pairs in 16-lane segments: 0 auto, 1 every eligible pair, 2 never (A/B)")
+    ap.add_argument("--no-split-ck", action="store_true",
+                    help="SPLIT script batches (config 2) keep the ladder-key forward with per-cell codes (SED_OPT_SPLITCK 2; A/B)")
     ap.add_argument("--no-scaled", action="store_true",
                     help="fp64 lane pairs on the fp64 DP instead of the scaled-integer DP of dyadic costs (A/B)")
     ap.add_argument("--timing-every", type=int, default=-1,
@@ -592,6 +594,8 @@ def main():
         ctx.set_option(sedgpu.SED_OPT_BITPAR, 2)
     if args.no_scaled:
         ctx.set_option(sedgpu.SED_OPT_SCALED, 2)
+    if args.no_split_ck:
+        ctx.set_option(sedgpu.SED_OPT_SPLITCK, 2)
     if args.seg:
         ctx.set_option(sedgpu.SED_OPT_SEG, args.seg)
     if args.chain:
@@ -742,7 +746,7 @@ def main():
         # distance keys (3 ops/cell); the traceback's recompute runs after it on the same SIMDs and is not in
         # this model (kernel_ms is the DP).  Per-cell codes on ladder dot keys (CHAIN, config 3): v_dot4, v_min3,
         # v_and_or, v_alignbit on the d = -1 rows, plus 2 adds on the ladder's jump rows (2 of 8 at R = 8).
-        if want_script and batch.traceback_mode == 2:
+        if want_script and batch.traceback_mode in (2, 4):
             ops_cell = CELL_OPS["dot" if batch.dot_keys else "nolen"]
         elif want_script:
             ops_cell = lad_ops(R) if batch.ladder_dot_keys else CELL_OPS["script"]
@@ -750,7 +754,7 @@ def main():
             ops_cell = BITPAR_OPS_PER_ROW * float(np.sum(packed.len_a[:P])) / max(cells, 1.0)
         else:
             ops_cell = CELL_OPS["nolen_x2" if npk == P else "nolen"]
-    dot_cell = batch.mode == "i32" and want_script and batch.traceback_mode == 2 and batch.dot_keys
+    dot_cell = batch.mode == "i32" and want_script and batch.traceback_mode in (2, 4) and batch.dot_keys
     cyc = VALU_CYCLES_DOT if dot_cell else VALU_CYCLES_PER_OP
     valu_peak = SIMDS * CLOCK * 64 / (cyc * ops_cell) if ops_cell else None
     rate = cells / (dp_busy * 1e-3)
@@ -760,11 +764,14 @@ def main():
     else:
         wave_k = "sed_wf_i32_chain_kernel" if batch.chains else "sed_wf_i32_kernel"
         parts = ((["sed_wf_i32x2_kernel"] if wave_x2 else []) + ([wave_k] if nl + wave_x2 < P else []) +
+                 (["sed_ck_codes_kernel"] if want_script and batch.traceback_mode == 4 else []) +
                  ([("sed_lane_bitpar_kernel" if nbp else "sed_lane_i32x2_kernel" if lane_x2 else
                     "sed_lane_i32_kernel")] if nl else []))
     tb_kernels = []
     if want_script and nl < P:
         tb_kernels = {2: ["sed_traceback_ck_kernel"], 3: ["sed_tb_stripemap_kernel", "sed_tb_stripeemit_kernel"],
+                      4: ["sed_tb_stripemap_kernel", "sed_tb_stripeemit_kernel", "sed_traceback_kernel",
+                          "sed_traceback_window_kernel"],
                       1: ["sed_traceback_kernel", "sed_traceback_window_kernel"]}.get(batch.traceback_mode, [])
     kname = "+".join(parts)
     traffic, traffic_src, issue, issue_src = None, None, None, None
@@ -792,7 +799,8 @@ def main():
                    "scaled_pairs": batch.scaled_pairs, "segment_pairs": batch.segment_pairs,
                    "chains": batch.chains, "dot_keys": batch.dot_keys, "ladder_dot_keys": batch.ladder_dot_keys,
                    "traceback": {0: None, 1: "per-cell codes", 2: "checkpoints + recompute",
-                                 3: "per-cell codes, stripe-parallel walk"}[batch.traceback_mode],
+                                 3: "per-cell codes, stripe-parallel walk",
+                                 4: "checkpoints, every tile's codes recomputed, stripe-parallel walk"}[batch.traceback_mode],
                    "parallelism": "dp%d" % world, "env": env},
         # the kernels issue VALU on most cycles and move a fraction of the HBM peak: "bound" names the VALU; the
         # HBM figures are the roofline the north star asks for (SURVEY.md 8(d) bytes), "valu" the binding one

@@ -93,6 +93,10 @@ enum {
 #define SED_OPT_SEG 13          /* fp64 batches of > 256 wave pairs: pairs whose cost model favours it run in 16-lane
                                    segments, four per wave (stripes of 16 R rows, a 15-step ramp instead of 63: the
                                    timing.py sweep's short pairs): 0 auto, 1 every such pair, 2 never */
+#define SED_OPT_SPLITCK 14      /* SPLIT script batches (<= 256 long pairs: config 2, GUI calls): the forward runs distance
+                                   or dot keys with checkpoints and every 64 x 64 tile's codes are then recomputed at once
+                                   for the stripe-parallel traceback (sed_batch_traceback_mode 4): 0 auto (on), 2 never
+                                   (per-cell codes from the ladder-key forward) */
 #define SED_OPT_DEBUG_CORRUPT 9 /* testing only: p + 1 overwrites one checkpoint word of pair p before its traceback,
                                    which must then fail with SED_E_DEVICE naming the pair; 0 off */
 
@@ -163,7 +167,9 @@ int sed_dot_factor(const double *sub, double ins, double del, int maxmin, int la
 int sed_batch_dot_keys(const sed_batch *b);           /* bit 0: the checkpoint forward kernel runs dot keys, bit 1: the
                                                          CHAIN kernel runs ladder dot keys (SED_OPT_DOT) */
 int sed_batch_traceback_mode(const sed_batch *b);     /* 0 no script, 1 per-cell codes, 2 checkpoints (SED_OPT_TB),
-                                                         3 per-cell codes walked stripe-parallel (<= 64 pairs, R = 4) */
+                                                         3 per-cell codes walked stripe-parallel (<= 64 pairs, R = 4),
+                                                         4 SPLIT checkpoints recomputed into per-cell codes
+                                                         (SED_OPT_SPLITCK), walked as 3 or 1 */
 /* CHAIN diagnostics of the last run (waits for it): pairs handed out by the dynamic-CHAIN device counter, and
  * the most pairs one wave computed back to back (0 when CHAIN mode is off). */
 int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave);

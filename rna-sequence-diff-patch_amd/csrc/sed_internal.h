@@ -182,4 +182,7 @@ __host__ __device__ inline uint64_t sed_ck_row_word(int R, int k, int ngroups, i
 }
 // CK batches (L.ck): the traceback that recomputes tiles from the forward kernel's checkpoints
 hipError_t sed_launch_traceback_ck(const sed_launch &L, uint32_t *ops, const sed_i32_params &prm);
+// SPLIT batches with checkpoints: every tile's op codes from the checkpoints, into the per-cell code layout (one wave
+// per tile of each pair: grid max_tiles x npairs)
+hipError_t sed_launch_ck_codes(const sed_launch &L, int max_tiles, const sed_i32_params &prm);
 hipError_t sed_launch_selftest(uint32_t *d_out, hipStream_t stream);

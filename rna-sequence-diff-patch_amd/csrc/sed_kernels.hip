@@ -415,7 +415,7 @@ __device__ __forceinline__ uint32_t i32_sel(uint32_t b) { return 0x0D000100u | (
 // The stripe kernel's group: lane 0's top values from the chunk's LDS slots (ltop, broadcast reads),
 // each lane's str2 selectors from the wave's LDS selector ring at its own column (lsel: this group's
 // first step for this lane, doubled ring so the G reads never wrap).
-template <int R, bool TB, bool LEN, bool CAP, bool CK = false, bool DOT = false>
+template <int R, bool TB, bool LEN, bool CAP, bool CK = false, bool DOT = false, bool COLLECT = !CK>
 __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                           uint32_t &bottom, uint32_t &selv, const uint32_t *__restrict__ ltop,
                                           const uint32_t *__restrict__ lsel, uint32_t &outc, uint32_t (&W)[4],
@@ -429,7 +429,7 @@ __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         const int s = s0 + u;
-        i32_step<R, TB, LEN, !CK, true, false, DOT>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u);
+        i32_step<R, TB, LEN, COLLECT, true, false, DOT>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u);
         if constexpr (CK) rcv[u] = V[R - 1];  // the band's bottom row, step s (row checkpoints)
         if constexpr (CAP) {
             const bool hit = (s == cap_step) && (lane == cap_lane);
@@ -542,7 +542,8 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                   sed_i32_params prm) {
     constexpr int ROWS = 64 * R;
     constexpr int G = Grp<R>::G;
-    static_assert(!CK || (R <= 16 && !SPLIT && !TB && !LEN), "checkpoints: R <= 16, distance keys, one wave per pair");
+    static_assert(!CK || (R <= 16 && !TB && !LEN), "checkpoints: R <= 16, distance keys");
+    static_assert(!(CK && SPLIT) || R == 4, "SPLIT checkpoints (sed_ck_codes_kernel): R = 4");
     static_assert(!DOT || CK, "dot keys: checkpoint batches only");
     const int lane = threadIdx.x & 63;
     int pair, kfirst = 0;
@@ -659,8 +660,10 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * 256u;
         // CK: column checkpoints of stripe k at ccb[(chunk * (R+1) + v) * 64 + lane], row checkpoints at
         // rcb[group * 64 + (lane / G) * G + step % G] (sed_ck_*_word, the layout sed_traceback_ck_kernel reads)
-        uint32_t *ccb = tb + d.tb_off + sed_ck_col_word(R, k, nchunks, 0, 0, 0);
-        uint32_t *rcb = tb + d.tb_off + sed_ck_col_words(R, nstripes, nchunks) + (uint64_t)k * (uint64_t)(SG / G) * SED_CK_RW;
+        // (SPLIT: the checkpoints follow the pair's per-cell code region, which sed_ck_codes_kernel fills from them)
+        const uint64_t ckoff = (SPLIT && CK) ? (uint64_t)nstripes * (uint64_t)(SG / G) * 256u : 0u;
+        uint32_t *ccb = tb + d.tb_off + ckoff + sed_ck_col_word(R, k, nchunks, 0, 0, 0);
+        uint32_t *rcb = tb + d.tb_off + ckoff + sed_ck_col_words(R, nstripes, nchunks) + (uint64_t)k * (uint64_t)(SG / G) * SED_CK_RW;
         uint32_t rcv[G];
         const bool last = (k == nstripes - 1);
         const int cap_step = last ? m - 1 + cap_lane : -1;
@@ -688,10 +691,10 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                     constexpr int GH = SED_CK_TILE / R;  // forward lanes per traceback tile
                     if ((lane & (GH - 1)) == GH - 1)
                         store_words<G>(rcb + (uint64_t)(s0 / G) * SED_CK_RW + (uint32_t)(lane / GH) * G, rcv);
-                    if (lane == 63 && !last) store_words<G>(bnd + d.bnd_off + (uint32_t)s0, rcv);  // next stripe's top row
+                    if (!SPLIT && lane == 63 && !last) store_words<G>(bnd + d.bnd_off + (uint32_t)s0, rcv);  // next stripe's top row
                 }
             };
-            if (CK && c != c_cap) {
+            if (CK && !SPLIT && c != c_cap) {
 #pragma unroll SED_CK_GUNROLL
                 for (int g = 0; g < 64 / G; ++g) {
                     const int s0 = 64 * c + g * G;  // (s0 & 63 folds to g * G)
@@ -718,11 +721,11 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                     }
                     const bool capg = cap_step >= s && cap_step < s + G;
                     if (capg)
-                        i32_group<R, TB, LEN, true, CK, DOT>(V, cv, top_prev, bottom, selv, ltop, lsel, outc, W, s, lane,
-                                                        cap_step, cap_lane, cap_row, cap, rcv);
+                        i32_group<R, TB, LEN, true, CK, DOT, !CK || SPLIT>(V, cv, top_prev, bottom, selv, ltop, lsel, outc, W,
+                                                                          s, lane, cap_step, cap_lane, cap_row, cap, rcv);
                     else
-                        i32_group<R, TB, LEN, false, CK, DOT>(V, cv, top_prev, bottom, selv, ltop, lsel, outc, W, s, lane,
-                                                         cap_step, cap_lane, cap_row, cap, rcv);
+                        i32_group<R, TB, LEN, false, CK, DOT, !CK || SPLIT>(V, cv, top_prev, bottom, selv, ltop, lsel, outc, W,
+                                                                           s, lane, cap_step, cap_lane, cap_row, cap, rcv);
                     stores(s);
                     if constexpr (SPLIT) {
                         // lanes 64-G+u hold lane 63's bottom cell of step s+u, column s+u-62 (word col + 64)
@@ -2095,6 +2098,187 @@ template <bool WAVE> __device__ __forceinline__ void ck_sync() {
 // topb[x] (132 words): the row above the tile at lane 0's column of step x, plus 1 (lane 0's delete candidate);
 // selb[64 + x] (196 words): str2 selector of lane 0's column at step x; lane r reads selb[64 + sigma - r] itself
 // (its column at step sigma), so no selector travels through the DPP chain.  q0: the sink's L.
+// Per-pair constants of the checkpoint tiles.  ckoff: word offset of the checkpoints past d.tb_off (SPLIT batches keep
+// them after the pair's per-cell code region, sed_ck_codes_kernel).
+struct CkPairCtx {
+    int n, m, SG, nchunks, ngroups, band;
+    const uint32_t *ccp, *rcp, *pa, *pb;
+    uint32_t cko0, cko1, hm[4];
+};
+template <int R>
+__device__ __forceinline__ CkPairCtx ck_pair_ctx(const sed_pair_desc &d, const int lane, const uint32_t *__restrict__ seqa,
+                                                 const uint32_t *__restrict__ seqb, const uint32_t *__restrict__ ck,
+                                                 const uint64_t ckoff) {
+    constexpr int ROWS = 64 * R, G = Grp<R>::G;
+    constexpr int LR = R == 4 ? 2 : R == 8 ? 3 : 4;
+    CkPairCtx px;
+    px.n = d.n;
+    px.m = d.m;
+    const int nstripes = (d.n + ROWS - 1) / ROWS;
+    px.SG = (d.m + 63 + G - 1) / G * G;
+    px.nchunks = (px.SG + 63) >> 6;
+    px.ngroups = px.SG / G;
+    px.ccp = ck + d.tb_off + ckoff;
+    px.rcp = px.ccp + sed_ck_col_words(R, nstripes, px.nchunks);
+    px.pa = seqa + d.a_off;
+    px.pb = seqb + d.b_off;
+    px.band = lane >> LR;
+    px.cko0 = ((uint32_t)(lane & (R - 1)) * 64u + (uint32_t)px.band) * 4u;
+    px.cko1 = (uint32_t)(R * 64 + px.band) * 4u;
+    const int sig0 = lane - px.band + G - 1;  // first real sweep step of this lane (<= 63)
+    // code 3 (outside the window) for the steps before sig0, OR-ed into words 0..3 once they are complete
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int h = min(max(sig0 - 16 * w, 0), 16);
+        px.hm[w] = h >= 16 ? ~0u : (1u << (2 * h)) - 1u;
+    }
+    return px;
+}
+
+// One tile visit: tile (stripe k, band group Q, chunk c) recomputed from its checkpoints up to sweep step sig_end (FULL:
+// all 128 steps), the codes in W (lane r's code of step sigma in W[sigma >> 4], bits 2 (sigma & 15)); returns the lanes'
+// keys after the last step (the entry keys).
+template <int R, bool WAVE, bool FULL>
+__device__ __forceinline__ uint32_t ck_tile_sweep(const CkPairCtx &px, const int lane, const sed_i32_params &prm,
+                                                  uint32_t *__restrict__ topb, uint32_t *__restrict__ selb, const int k,
+                                                  const int Q, const int c, const int sig_end, uint32_t &one,
+                                                  uint32_t (&W)[8], uint32_t &vinit) {
+    constexpr int ROWS = 64 * R, G = Grp<R>::G;  // a tile: G forward lanes (bands) of R rows
+    constexpr int LR = R == 4 ? 2 : R == 8 ? 3 : 4;
+    constexpr bool VHOLD = CkVHold<R>::value;
+    const int n = px.n, m = px.m, SG = px.SG, nchunks = px.nchunks, ngroups = px.ngroups, band = px.band;
+    const int J0 = 64 * c - G * Q + 1, rowbase = k * ROWS + 64 * Q;
+    // ---- boundaries (distance keys -> traceback keys) ----
+    // Every load of the tile is issued before the first use (one memory round trip per tile visit): addresses
+    // are clamped to valid words and the border cases are selects afterwards.
+    const int ir = min(rowbase + lane, n - 1);  // 0-based str1 index of this lane's row (clamped)
+    const uint32_t wa = px.pa[ir >> 4];
+    // (uniform 64-bit bases + 32-bit lane offsets: the loads take the scalar-base form and the address
+    // arithmetic stays on the scalar unit)
+    uint32_t ck0 = 0, ck1 = 0;
+    if (c >= 1) {  // (uniform)
+        const uint32_t *cp = px.ccp + sed_ck_col_word(R, k, nchunks, c - 1, 0, G * Q);
+        uint32_t o0 = px.cko0, o1 = px.cko1;
+        asm volatile("" : "+v"(o0), "+v"(o1));  // (else the zero-extended offsets are hoisted as 64-bit pairs)
+        ck0 = ld_byte_off(cp, o0);
+        ck1 = ld_byte_off(cp, o1);
+    }
+    // the row above the tile at column J0 - G + x (x = lane, lane + 64, lane + 128 < 132): row checkpoints of
+    // forward lane G*Q - 1 (or lane 63 of the stripe above); steps clamped: past SG the columns are beyond m and
+    // never read by the walk; columns < 1 are the column-0 border (a CHAIN wave's lanes still hold the
+    // previous pair there)
+    const bool above = Q >= 1 || k >= 1;  // (uniform) else row 0: the border
+    const int kr = Q >= 1 ? k : k - 1, tr = Q >= 1 ? G * Q - 1 : 63, s0r = Q >= 1 ? 64 * c - G - 1 : 64 * c + 63 - G;
+    uint32_t rk[3] = {0, 0, 0}, wb[3];
+    const uint32_t *rbase = px.rcp + sed_ck_row_word(R, max(kr, 0), ngroups, 0, tr);  // (uniform; read when above)
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+        const int x = lane + 64 * h;
+        if (h < 2 || x < 132) {
+            if (above) {
+                const uint32_t s = (uint32_t)min(max(s0r + x, 0), SG - 1);
+                rk[h] = ld_byte_off(rbase, ((s >> (6 - LR)) * (uint32_t)SED_CK_RW + (s & (uint32_t)(G - 1))) * 4u);
+            }
+            const int ci = min(max(J0 - (G - 1) + x - 1, 0), m - 1);
+            wb[h] = px.pb[ci >> 4];
+        }
+    }
+    const uint32_t a = (wa >> ((ir & 15) * 2)) & 3u;
+    const uint32_t clo = (a & 1u) ? prm.costrow[1] : prm.costrow[0];
+    const uint32_t chi = (a & 1u) ? prm.costrow[3] : prm.costrow[2];
+    const uint32_t cv = (a & 2u) ? chi : clo;
+    uint32_t V = SED_KB, tp = SED_KB;  // c = 0: the column-0 borders
+    if (c >= 1) {
+        V = ck_to_tb(ck0, prm);
+        tp = ck_to_tb(ck1, prm);
+        if (VHOLD && J0 - band - 1 > m) V = 0u;  // (forward garbage past m: key 0 holds under the recurrence)
+    }
+    tp += 1u;  // diagonals carry the +1 of the delete candidate they were taken from
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+        const int x = lane + 64 * h;
+        if (h < 2 || x < 132) {
+            const uint32_t v = (above && J0 - G + x >= 1) ? ck_to_tb(rk[h], prm) : SED_KB;
+            topb[x] = v + 1u;
+            const int col = J0 - (G - 1) + x;  // column of lane 0 at step x
+            const int ci = min(max(col - 1, 0), m - 1);
+            const uint32_t sv = col < 1 ? SED_SEL_SENT : i32_sel((wb[h] >> ((ci & 15) * 2)) & 3u);
+            if constexpr (VHOLD) {  // band b's copy: the sentinel left of its window (x < G - 1 - b)
+#pragma unroll
+                for (int b = 0; b < G; ++b) selb[b * SED_CK_SELB + 64 + x] = x < G - 1 - b ? SED_SEL_SENT : sv;
+            } else {
+                selb[64 + x] = sv;
+            }
+        }
+    }
+    ck_sync<WAVE>();
+    // ---- sweep: lane r at step sigma computes (row rowbase + r + 1, column J0 - (G-1) + sigma - r) ----
+    // Whole 16-step words (a branch per step would keep the LDS reads from running ahead), except the
+    // word holding the entry step, which stops at it: the lanes' keys are then the entry keys.  The cell above and the diagonal
+    // carry the delete candidate's +1 (one v_add_u32_dpp: lane r - 1's key + 1, or topb for lane 0), so
+    // the update constant is one less.  Lanes still left of their window (sigma < sig0: lanes
+    // ck_active_lanes(sigma) .. 63, a compile-time count) keep their checkpoint through one v_cndmask on a
+    // scalar mask; their codes become 3 through hm.  Steps 0 .. G-2 hold every lane and are skipped.
+    W[0] = 0u;  // steps 0 .. G-2 are skipped: their bits are OR-ed to 3 from a defined word
+    if constexpr (VHOLD) {  // a band's first row: V - V_above + 1 until the band starts
+        // (through the asm DPP add: with the builtin, the compiler folded V - dpp(V) into one
+        // v_subrev_u32_dpp ... bound_ctrl:1, which returned V_above - V on the device)
+        uint32_t zero = 0u;
+        asm volatile("" : "+v"(zero));
+        const uint32_t vabove = dpp_shr1_add(0u, V, zero);
+        one = ((lane & (R - 1)) == 0 && lane > 0) ? V - vabove + 1u : 1u;
+    }
+#ifdef SED_TB_DEBUG
+    vinit = V;
+#endif
+    uint32_t tprev = dpp_shr1_add(topb[G - 1], V, one);  // diagonal of step G-1 (+1)
+    const uint32_t *selp = selb + (VHOLD ? band * SED_CK_SELB : 0) + 64 - lane;  // lane r's selector at step sigma
+    const int w_end = FULL ? 7 : sig_end >> 4;  // FULL: every word, whole
+    auto step = [&](const int sig, uint32_t &wv, const uint32_t topin, const uint32_t selv) {
+        if (sig < G - 1) return;  // every lane holds
+        const int bs = ck_band_start<R>(sig);  // folds to a constant in the unrolled sweep
+        if (VHOLD && bs > 0) one = lane == R * bs ? 1u : one;  // the band starts: its first row's real delete
+        const uint32_t topv = dpp_shr1_add(topin, V, one);
+        // (selv: steps before the lane's first column read don't-care)
+        uint32_t diag = tprev;
+        if (bs > 0) diag = lane == R * bs ? tp : diag;
+        const uint32_t mm = umin3(V, topv, diag + __builtin_amdgcn_perm(cv, 0xFFFFFFFDu, selv));
+        const uint32_t vn = mm & ~3u;
+        if constexpr (VHOLD) {
+            V = vn;
+        } else {
+            const int act = ck_active_lanes<R>(sig);  // lanes 0 .. act-1 are inside their window
+            V = act >= 64 ? vn : ck_hold(vn, V, act);
+        }
+        wv = __builtin_amdgcn_alignbit(mm, wv, 2);
+        tprev = topv;
+    };
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        if (w > w_end) break;  // the path never needs later steps
+        if (!FULL && w == w_end) {  // up to the entry step exactly: the lanes then hold the entry keys
+            // the word's LDS inputs first, so the per-step exits do not serialise an LDS round trip per step
+            uint32_t tw[16], sw[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                tw[u] = topb[16 * w + u + 1];
+                sw[u] = selp[16 * w + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                if (16 * w + u > sig_end) break;
+                step(16 * w + u, W[w], tw[u], sw[u]);
+            }
+            W[w] >>= 2u * (15u - ((uint32_t)sig_end & 15u));  // step u's code to bits 2u, 2u+1
+        } else {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) step(16 * w + u, W[w], topb[16 * w + u + 1], selp[16 * w + u]);
+        }
+        if (w < 4) W[w] |= px.hm[w];
+    }
+    return V;
+}
+
 template <int R, bool WAVE>
 __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const int pair, const uint32_t q0,
                                                   const int lane, const uint32_t *__restrict__ seqa,
@@ -2103,9 +2287,7 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
                                                   const sed_i32_params &prm, uint32_t *__restrict__ topb,
                                                   uint32_t *__restrict__ selb) {
     constexpr int ROWS = 64 * R, G = Grp<R>::G;  // a tile: G forward lanes (bands) of R rows
-    constexpr int LR = R == 4 ? 2 : R == 8 ? 3 : 4;
-    constexpr bool VHOLD = CkVHold<R>::value;
-    static_assert((1 << LR) == R, "R in {4, 8, 16}");
+    static_assert(R == 4 || R == 8 || R == 16, "R in {4, 8, 16}");
     const int n = d.n, m = d.m;
 #ifdef SED_TB_DEBUG
     int visit = 0;  // debug dumps: 136 words per tile visit (entry keys, initial keys, coordinates)
@@ -2124,21 +2306,7 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
     const uint32_t Kd = (prm.del << 16) + 4u, Ki = (prm.ins << 16) + 4u;
     int i = n, j = m;
     if (i > 0 && j > 0) {
-        const int nstripes = (n + ROWS - 1) / ROWS;
-        const int SG = (m + 63 + G - 1) / G * G, nchunks = (SG + 63) >> 6, ngroups = SG / G;
-        const uint32_t *ccp = ck + d.tb_off;
-        const uint32_t *rcp = ccp + sed_ck_col_words(R, nstripes, nchunks);
-        const uint32_t *pa = seqa + d.a_off, *pb = seqb + d.b_off;
-        const int band = lane >> LR;
-        const uint32_t cko0 = ((uint32_t)(lane & (R - 1)) * 64u + (uint32_t)band) * 4u, cko1 = (uint32_t)(R * 64 + band) * 4u;
-        const int sig0 = lane - band + G - 1;  // first real sweep step of this lane (<= 63)
-        // code 3 (outside the window) for the steps before sig0, OR-ed into words 0..3 once they are complete
-        uint32_t hm[4];
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const int h = min(max(sig0 - 16 * w, 0), 16);
-            hm[w] = h >= 16 ? ~0u : (1u << (2 * h)) - 1u;
-        }
+        const CkPairCtx px = ck_pair_ctx<R>(d, lane, seqa, seqb, ck, 0);
         uint32_t one = 1u;  // the delete candidate's +1, a VGPR operand of v_add_u32_dpp
         asm volatile("" : "+v"(one));
         int guard = 2 * (n + m) + 8;       // tiles visited; every visit makes progress
@@ -2152,145 +2320,9 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
             const int J0 = 64 * c - G * Q + 1, rowbase = k * ROWS + 64 * Q;
             const int re = i - rowbase - 1;             // the entry cell's tile row
             const int sig_end = (j - J0 + G - 1) + re;  // the entry cell's sweep step (<= 126)
-            // ---- boundaries (distance keys -> traceback keys) ----
-            // Every load of the tile is issued before the first use (one memory round trip per tile visit): addresses
-            // are clamped to valid words and the border cases are selects afterwards.
-            const int ir = min(rowbase + lane, n - 1);  // 0-based str1 index of this lane's row (clamped)
-            const uint32_t wa = pa[ir >> 4];
-            // (uniform 64-bit bases + 32-bit lane offsets: the loads take the scalar-base form and the address
-            // arithmetic stays on the scalar unit)
-            uint32_t ck0 = 0, ck1 = 0;
-            if (c >= 1) {  // (uniform)
-                const uint32_t *cp = ccp + sed_ck_col_word(R, k, nchunks, c - 1, 0, G * Q);
-                uint32_t o0 = cko0, o1 = cko1;
-                asm volatile("" : "+v"(o0), "+v"(o1));  // (else the zero-extended offsets are hoisted as 64-bit pairs)
-                ck0 = ld_byte_off(cp, o0);
-                ck1 = ld_byte_off(cp, o1);
-            }
-            // the row above the tile at column J0 - G + x (x = lane, lane + 64, lane + 128 < 132): row checkpoints of
-            // forward lane G*Q - 1 (or lane 63 of the stripe above); steps clamped: past SG the columns are beyond m and
-            // never read by the walk; columns < 1 are the column-0 border (a CHAIN wave's lanes still hold the
-            // previous pair there)
-            const bool above = Q >= 1 || k >= 1;  // (uniform) else row 0: the border
-            const int kr = Q >= 1 ? k : k - 1, tr = Q >= 1 ? G * Q - 1 : 63, s0r = Q >= 1 ? 64 * c - G - 1 : 64 * c + 63 - G;
-            uint32_t rk[3] = {0, 0, 0}, wb[3];
-            const uint32_t *rbase = rcp + sed_ck_row_word(R, max(kr, 0), ngroups, 0, tr);  // (uniform; read when above)
-#pragma unroll
-            for (int h = 0; h < 3; ++h) {
-                const int x = lane + 64 * h;
-                if (h < 2 || x < 132) {
-                    if (above) {
-                        const uint32_t s = (uint32_t)min(max(s0r + x, 0), SG - 1);
-                        rk[h] = ld_byte_off(rbase, ((s >> (6 - LR)) * (uint32_t)SED_CK_RW + (s & (uint32_t)(G - 1))) * 4u);
-                    }
-                    const int ci = min(max(J0 - (G - 1) + x - 1, 0), m - 1);
-                    wb[h] = pb[ci >> 4];
-                }
-            }
-            const uint32_t a = (wa >> ((ir & 15) * 2)) & 3u;
-            const uint32_t clo = (a & 1u) ? prm.costrow[1] : prm.costrow[0];
-            const uint32_t chi = (a & 1u) ? prm.costrow[3] : prm.costrow[2];
-            const uint32_t cv = (a & 2u) ? chi : clo;
-            uint32_t V = SED_KB, tp = SED_KB;  // c = 0: the column-0 borders
-            if (c >= 1) {
-                V = ck_to_tb(ck0, prm);
-                tp = ck_to_tb(ck1, prm);
-                if (VHOLD && J0 - band - 1 > m) V = 0u;  // (forward garbage past m: key 0 holds under the recurrence)
-            }
-            tp += 1u;  // diagonals carry the +1 of the delete candidate they were taken from
-#pragma unroll
-            for (int h = 0; h < 3; ++h) {
-                const int x = lane + 64 * h;
-                if (h < 2 || x < 132) {
-                    const uint32_t v = (above && J0 - G + x >= 1) ? ck_to_tb(rk[h], prm) : SED_KB;
-                    topb[x] = v + 1u;
-                    const int col = J0 - (G - 1) + x;  // column of lane 0 at step x
-                    const int ci = min(max(col - 1, 0), m - 1);
-                    const uint32_t sv = col < 1 ? SED_SEL_SENT : i32_sel((wb[h] >> ((ci & 15) * 2)) & 3u);
-                    if constexpr (VHOLD) {  // band b's copy: the sentinel left of its window (x < G - 1 - b)
-#pragma unroll
-                        for (int b = 0; b < G; ++b) selb[b * SED_CK_SELB + 64 + x] = x < G - 1 - b ? SED_SEL_SENT : sv;
-                    } else {
-                        selb[64 + x] = sv;
-                    }
-                }
-            }
-            ck_sync<WAVE>();
-            // ---- sweep: lane r at step sigma computes (row rowbase + r + 1, column J0 - (G-1) + sigma - r) ----
-            // Whole 16-step words (a branch per step would keep the LDS reads from running ahead), except the
-            // word holding the entry step, which stops at it: the lanes' keys are then the entry keys.  The cell above and the diagonal
-            // carry the delete candidate's +1 (one v_add_u32_dpp: lane r - 1's key + 1, or topb for lane 0), so
-            // the update constant is one less.  Lanes still left of their window (sigma < sig0: lanes
-            // ck_active_lanes(sigma) .. 63, a compile-time count) keep their checkpoint through one v_cndmask on a
-            // scalar mask; their codes become 3 through hm.  Steps 0 .. G-2 hold every lane and are skipped.
-            uint32_t W[8];
-            W[0] = 0u;  // steps 0 .. G-2 are skipped: their bits are OR-ed to 3 from a defined word
-            if constexpr (VHOLD) {  // a band's first row: V - V_above + 1 until the band starts
-                // (through the asm DPP add: with the builtin, the compiler folded V - dpp(V) into one
-                // v_subrev_u32_dpp ... bound_ctrl:1, which returned V_above - V on the device)
-                uint32_t zero = 0u;
-                asm volatile("" : "+v"(zero));
-                const uint32_t vabove = dpp_shr1_add(0u, V, zero);
-                one = ((lane & (R - 1)) == 0 && lane > 0) ? V - vabove + 1u : 1u;
-            }
-#ifdef SED_TB_DEBUG
-            const uint32_t vinit = V;
-#endif
-            uint32_t tprev = dpp_shr1_add(topb[G - 1], V, one);  // diagonal of step G-1 (+1)
-            uint32_t ent = 0;
-            const uint32_t *selp = selb + (VHOLD ? band * SED_CK_SELB : 0) + 64 - lane;  // lane r's selector at step sigma
-            const int w_end = sig_end >> 4;
-            auto step = [&](const int sig, uint32_t &wv, const uint32_t topin, const uint32_t selv) {
-                if (sig < G - 1) return;  // every lane holds
-                const int bs = ck_band_start<R>(sig);  // folds to a constant in the unrolled sweep
-                if (VHOLD && bs > 0) one = lane == R * bs ? 1u : one;  // the band starts: its first row's real delete
-                const uint32_t topv = dpp_shr1_add(topin, V, one);
-                // (selv: steps before the lane's first column read don't-care)
-                uint32_t diag = tprev;
-                if (bs > 0) diag = lane == R * bs ? tp : diag;
-                const uint32_t mm = umin3(V, topv, diag + __builtin_amdgcn_perm(cv, 0xFFFFFFFDu, selv));
-                const uint32_t vn = mm & ~3u;
-                if constexpr (VHOLD) {
-                    V = vn;
-                } else {
-                    const int act = ck_active_lanes<R>(sig);  // lanes 0 .. act-1 are inside their window
-                    V = act >= 64 ? vn : ck_hold(vn, V, act);
-                }
-                wv = __builtin_amdgcn_alignbit(mm, wv, 2);
-                tprev = topv;
-#ifdef SED_TB_DEBUG_VISIT
-                if (visit == SED_TB_DEBUG_VISIT) {  // every step's keys of one visit, after the visit dumps
-                    uint32_t *ds = out + ((n + m + 15) >> 4) + 64 + 136 * 32 + 3 * 64 * sig;
-                    ds[lane] = V;
-                    ds[64 + lane] = topv;
-                    ds[128 + lane] = mm;
-                }
-#endif
-            };
-#pragma unroll
-            for (int w = 0; w < 8; ++w) {
-                if (w > w_end) break;  // the path never needs later steps
-                if (w == w_end) {  // up to the entry step exactly: the lanes then hold the entry keys
-                    // the word's LDS inputs first, so the per-step exits do not serialise an LDS round trip per step
-                    uint32_t tw[16], sw[16];
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) {
-                        tw[u] = topb[16 * w + u + 1];
-                        sw[u] = selp[16 * w + u];
-                    }
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) {
-                        if (16 * w + u > sig_end) break;
-                        step(16 * w + u, W[w], tw[u], sw[u]);
-                    }
-                    W[w] >>= 2u * (15u - ((uint32_t)sig_end & 15u));  // step u's code to bits 2u, 2u+1
-                } else {
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) step(16 * w + u, W[w], topb[16 * w + u + 1], selp[16 * w + u]);
-                }
-                if (w < 4) W[w] |= hm[w];
-            }
-            ent = V;
+            uint32_t W[8], vinit = 0;
+            const uint32_t ent = ck_tile_sweep<R, WAVE, false>(px, lane, prm, topb, selb, k, Q, c, sig_end, one, W, vinit);
+            (void)vinit;
 #ifdef SED_TB_DEBUG
             if (visit < 32) {  // debug builds only (pair 0; its script words, 64 spare, then 136 words per visit v)
                 uint32_t *dv = out + ((n + m + 15) >> 4) + 64 + 136 * visit;
@@ -2365,6 +2397,74 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
     ck_traceback_pair<R, false>(d, pair, q0, lane, seqa, seqb, ck, res, ops, prm, topb, selb);
 }
 
+// SPLIT batches with checkpoints (config 2, GUI pairs; sed_runtime.cpp: split_ck).  The SPLIT forward kernel runs the
+// distance (or dot) keys, 2-3 VALU per cell instead of the ladder keys' 5.2, and stores checkpoints after the pair's
+// per-cell code region; this kernel then recomputes every 64 x 64 tile from them at once (one wave per tile, the
+// traceback's whole-tile sweep) and writes the tile's canonical op codes in the per-cell code layout of the TB kernels
+// (store_tb: per stripe and G-step group, 4 words per forward lane, code (step u, row rr) at bits 2 (u R + rr)), which
+// the stripe-parallel traceback walks (as plain ops: the ladder keys' per-row code offsets are not applied, L.tb_ladder).
+// Every tile is written, those below row n too, so the walks only ever read codes of a DP.  R = 4 (G = 16): tile lane r = 4 b + rr is forward lane G Q + b's row rr; its
+// codes of the chunk's forward steps 64 c .. 64 c + 63 sit at sweep steps G - 1 + 3 b + rr onwards.
+__device__ __forceinline__ uint32_t ck_codes_transpose(uint32_t y) {
+    // 4 x 4 transpose of 2-bit elements, byte = row: (row rr, element u) -> (row u, element rr)
+    uint32_t t = ((y >> 6) ^ y) & 0x00CC00CCu;
+    y ^= t ^ (t << 6);
+    t = ((y >> 12) ^ y) & 0x0000F0F0u;
+    return y ^ t ^ (t << 12);
+}
+template <int R>
+__global__ __launch_bounds__(64) void sed_ck_codes_kernel(const sed_pair_desc *__restrict__ pd,
+                                                          const uint32_t *__restrict__ seqa,
+                                                          const uint32_t *__restrict__ seqb, uint32_t *__restrict__ tb,
+                                                          sed_i32_params prm) {
+    static_assert(R == 4, "the code layout transposition is written for R = 4");
+    constexpr int ROWS = 64 * R, G = Grp<R>::G;
+    const int lane = threadIdx.x;
+    const sed_pair_desc d = pd[blockIdx.y];
+    if (d.lane || d.n == 0 || d.m == 0) return;
+    const int n = d.n, m = d.m;
+    const int nstripes = (n + ROWS - 1) / ROWS, SG = (m + 63 + G - 1) / G * G, nchunks = (SG + 63) >> 6;
+    const int tile = (int)blockIdx.x;  // (k R + Q) nchunks + c
+    if (tile >= nstripes * R * nchunks) return;
+    const int c = tile % nchunks, kq = tile / nchunks, Q = kq % R, k = kq / R;
+    const uint64_t codew = (uint64_t)nstripes * (uint64_t)(SG / G) * 256u;  // the pair's per-cell code words
+    __shared__ uint32_t topb[132], selb[SED_CK_SELB], wl[64 * 9], win[64 * 5];
+    const CkPairCtx px = ck_pair_ctx<R>(d, lane, seqa, seqb, tb, codew);
+    uint32_t one = 1u;
+    asm volatile("" : "+v"(one));
+    uint32_t W[8], vinit = 0;
+    (void)ck_tile_sweep<R, false, true>(px, lane, prm, topb, selb, k, Q, c, 127, one, W, vinit);
+    // this lane's window: 64 codes from sweep step s0 (bit 2 s0 of W[0..7])
+    const int b = lane >> 2, rr = lane & 3;
+    const uint32_t s0 = (uint32_t)(G - 1 + (R - 1) * b + rr);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) wl[lane * 9 + w] = W[w];
+    __syncthreads();
+    uint32_t x[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) x[i] = wl[lane * 9 + (int)(s0 >> 4) + i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) win[lane * 5 + i] = __builtin_amdgcn_alignbit(x[i + 1], x[i], (2u * s0) & 31u);
+    __syncthreads();
+    // lane = 4 b' + g writes forward lane G Q + b''s group 4 c + g: rows 4 b' .. 4 b' + 3, window word g
+    const int bo = lane >> 2, g = lane & 3;
+    const int gg = 4 * c + g;
+    if (gg >= SG / G) return;  // past the stripe's last group
+    uint32_t y[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) y[q] = win[(4 * bo + q) * 5 + g];
+    uint32_t o[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {  // word w: steps 4w .. 4w+3 of the group, byte w of each row's window word
+        const uint32_t sel = (uint32_t)w * 0x0101u + 0x0400u;  // bytes w of y[0], w of y[1]
+        const uint32_t y01 = __builtin_amdgcn_perm(y[1], y[0], sel | 0x0C0C0000u);
+        const uint32_t y23 = __builtin_amdgcn_perm(y[3], y[2], sel | 0x0C0C0000u);
+        o[w] = ck_codes_transpose(__builtin_amdgcn_perm(y23, y01, 0x05040100u));
+    }
+    uint32_t *gp = tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * 256u + (uint64_t)gg * 256u + (uint32_t)(G * Q + bo) * 4u;
+    *reinterpret_cast<uint4 *>(gp) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 // ---------------------------------------------------------------------------
 // Self-test of the cross-lane primitives the kernels rely on.
 // ---------------------------------------------------------------------------
@@ -2396,9 +2496,12 @@ __global__ void sed_selftest_kernel(uint32_t *out) {
 template <int R, bool TB, bool LEN = true, bool CK = false, bool DOT = false>
 static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
     if (L.ntasks > 0) {  // SPLIT: one workgroup per (pair, stripe): the compute wave and its feeder
-        SED_LAUNCH((sed_wf_i32_kernel<R, TB, true, LEN>), dim3(L.ntasks), dim3(128), 0, L, L.pd, L.npairs,
-                           L.tasks, (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res,
-                           prm);
+        if constexpr (CK && R != 4) {  // (SPLIT checkpoints: R = 4 only)
+            return hipErrorInvalidValue;
+        } else {
+            SED_LAUNCH((sed_wf_i32_kernel<R, TB, true, LEN, CK, DOT>), dim3(L.ntasks), dim3(128), 0, L, L.pd, L.npairs,
+                       L.tasks, (const uint32_t *)L.seqa, (const uint32_t *)L.seqb, L.tb, L.bnd, L.res, prm);
+        }
     } else {
         const int grid = (L.npairs + 3) / 4;
         // SED_OCC_LDS (tuning/A-B only): dynamic LDS bytes per workgroup, which caps the resident waves
@@ -2459,7 +2562,10 @@ hipError_t sed_launch_i32x2(const sed_launch &L, const int32_t *list, int nwaves
 hipError_t sed_launch_i32(const sed_launch &L, const sed_i32_params &prm, bool len) {
     const bool tb = L.tb != nullptr;
     if (tb && L.ck) {  // distance keys + checkpoints
-        if (L.ntasks > 0) return hipErrorInvalidValue;
+        if (L.ntasks > 0) {  // SPLIT: R = 4 (sed_ck_codes_kernel)
+            if (L.R != 4) return hipErrorInvalidValue;
+            return prm.dot ? launch_i32_R<4, false, false, true, true>(L, prm) : launch_i32_R<4, false, false, true>(L, prm);
+        }
         if (prm.dot) {  // dot keys (the host found a byte factorisation of the update addends)
             switch (L.R) {
             case 4: return launch_i32_R<4, false, false, true, true>(L, prm);
@@ -2543,6 +2649,13 @@ hipError_t sed_launch_traceback_seg(const sed_launch &L, uint32_t *ops, const in
     case 8: SED_LAUNCH((sed_traceback_kernel<8, 16>), dim3(grid), dim3(64), 0, L, L.pd, nidx, L.tb, L.res, ops, 0ull, idx); break;
     default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+hipError_t sed_launch_ck_codes(const sed_launch &L, int max_tiles, const sed_i32_params &prm) {
+    if (L.R != 4 || max_tiles <= 0 || L.npairs <= 0) return hipErrorInvalidValue;
+    SED_LAUNCH(sed_ck_codes_kernel<4>, dim3(max_tiles, L.npairs), dim3(64), 0, L, L.pd, (const uint32_t *)L.seqa,
+               (const uint32_t *)L.seqb, L.tb, prm);
     return hipGetLastError();
 }
 

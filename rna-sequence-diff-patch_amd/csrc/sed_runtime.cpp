@@ -67,6 +67,7 @@ struct sed_ctx {
     int opt_scaled = 0;         // SED_OPT_SCALED: 0 auto (fp64 lane pairs under dyadic costs), 2 never
     int opt_seg = 0;            // SED_OPT_SEG: 0 auto (fp64 pairs the cost model prefers in 16-lane segments), 1 every
                                 // eligible pair, 2 never
+    int opt_splitck = 0;        // SED_OPT_SPLITCK: 0 auto (on), 2 never (SPLIT script batches keep the per-cell-code forward)
     int opt_dot = 0;            // SED_OPT_DOT: 0 auto, 2 never (checkpoint batches keep the perm-based distance keys)    // SED_OPT_CHAIN_WAVES: cap on the persistent waves of dynamic CHAIN mode
     int opt_debug_corrupt = 0;  // SED_OPT_DEBUG_CORRUPT: pair + 1 whose sink-tile checkpoint is overwritten
     DevBuf selftest;
@@ -134,6 +135,11 @@ struct sed_batch {
     int time_every = 1;
     bool tbpar = false;        // stripe-parallel traceback (few long pairs, per-cell codes; sed_tb_stripe*_kernel)
     int tbpar_items = 0, tbpar_kmax = 0;
+    // SPLIT script batches at R = 4 (config 2, GUI pairs): the forward runs distance / dot keys and stores checkpoints
+    // after each pair's per-cell code region; sed_ck_codes_kernel (ck_tiles waves per pair) recomputes every tile's
+    // codes into that region, which the stripe-parallel traceback walks
+    bool split_ck = false;
+    int ck_tiles = 0;
     bool split = false;
     bool ck = false;           // traceback from checkpoints + recompute (sed_kernels.hip: CK) instead of codes
     bool dot = false;          // CK forward kernel on dot keys (dot_keys below)
@@ -677,6 +683,10 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     static const int tbpar_env = [] { const char *e = getenv("SED_TBPAR"); return e ? atoi(e) : -1; }();
     b->tbpar = want_tb && !b->ck && R == 4 && (tbpar_env < 0 ? npairs <= 64 : tbpar_env > 0);
     b->tbpar_items = b->tbpar_kmax = 0;
+    // SPLIT script batches: checkpoints + a tile-parallel recompute of the codes (dot or distance keys in the forward:
+    // 2-3 VALU per cell against the ladder keys' 5.2 on the latency-bound stripe chain)
+    b->split_ck = want_tb && split && R == 4 && c->opt_splitck != 2;
+    b->ck_tiles = 0;
 
     // ---- layout ----
     b->pd.assign(npairs, sed_pair_desc{});
@@ -723,9 +733,11 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
             const uint64_t SG = (mm + SW - 1 + G - 1) / G * G;
             const uint64_t nchunks = (SG + SW - 1) / SW;
             if (want_tb) {  // CK: per stripe nchunks x (R+1) x 64 column checkpoints + (SG/G) x 64 row checkpoints
-                const uint64_t w = b->ck ? nstripes * (nchunks * (R + 1) * 64 + (SG / G) * SED_CK_RW) : nstripes * (SG / G) * SW * 4;
+                const uint64_t wck = nstripes * (nchunks * (R + 1) * 64 + (SG / G) * SED_CK_RW);
+                const uint64_t w = b->ck ? wck : nstripes * (SG / G) * SW * 4 + (b->split_ck ? wck : 0);
                 tbw += w;
                 ck_bytes += 4.0 * (double)w;
+                if (b->split_ck) b->ck_tiles = std::max<int>(b->ck_tiles, (int)(nstripes * R * nchunks));
             }
             // SPLIT: 64-bit {epoch tag, value} words per column and stripe (the tagged hand-off, sed_kernels.hip)
             if (nstripes > 1) bndw += (nchunks + 2) * SW * (packed ? (split ? 2 : 1) : 4) * (split ? nstripes : 1);
@@ -1031,7 +1043,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         ip.kdel = (ip.del << 16) + 5u;
         // dot keys: checkpoint batches of the stripe kernel (CHAIN batches share the traceback's key format)
         b->dot = false;
-        if (b->ck && b->nchains == 0 && c->K == 4 && c->opt_dot != 2) {
+        if ((b->ck || b->split_ck) && b->nchains == 0 && c->K == 4 && c->opt_dot != 2) {
             int64_t kap[4][4], maxmin = 0;
             for (int a = 0; a < 4; ++a)
                 for (int bb = 0; bb < 4; ++bb) kap[a][bb] = (int64_t)ip.ins + ip.del - (int64_t)c->sub[a * 4 + bb];
@@ -1229,7 +1241,7 @@ int run_batch(sed_batch *b) {
     L.res = (sed_result *)b->p_res[k];
     L.R = b->R;
     L.stream = ds;
-    L.tb_ladder = b->mode == SED_MODE_I32;
+    L.tb_ladder = b->mode == SED_MODE_I32 && !b->split_ck;  // (split_ck codes are the plain ops)
     L.ck = b->ck;
     L.tasks = b->split ? (const int2 *)b->p_tasks : nullptr;
     L.ntasks = b->split ? b->ntasks : 0;
@@ -1286,6 +1298,16 @@ int run_batch(sed_batch *b) {
             }
             e = sed_launch_i32_chain(L, ip, len);
             if (e == hipSuccess && b->chain_dyn) ++b->chain_launches[k];
+        } else if (b->mode == SED_MODE_I32 && b->split_ck) {  // forward with checkpoints, then every tile's codes
+            sed_launch Lf = L;
+            Lf.ck = true;
+            Lf.ev1 = nullptr;
+            e = sed_launch_i32(Lf, ip, len);
+            if (e == hipSuccess) {
+                sed_launch Lc = L;
+                Lc.ev0 = nullptr;
+                e = sed_launch_ck_codes(Lc, b->ck_tiles, ip);
+            }
         } else if (b->mode == SED_MODE_I32)
             e = sed_launch_i32(L, ip, len);
         else
@@ -1505,6 +1527,10 @@ int sed_set_option(sed_ctx *c, int key, int value) {
         c->opt_seg = value;
         return SED_OK;
     }
+    if (key == SED_OPT_SPLITCK && (value == 0 || value == 2)) {
+        c->opt_splitck = value;
+        return SED_OK;
+    }
     if (key == SED_OPT_SCALED && (value == 0 || value == 2)) {
         c->opt_scaled = value;
         return SED_OK;
@@ -1588,7 +1614,7 @@ int sed_batch_lane_pairs(const sed_batch *b) { return b ? b->nlane : SED_E_ARG; 
 int sed_batch_chains(const sed_batch *b) { return b ? b->nchains : SED_E_ARG; }
 int sed_batch_traceback_mode(const sed_batch *b) {
     if (!b || !(b->flags & SED_WANT_SCRIPT)) return 0;
-    return b->ck ? 2 : (b->tbpar ? 3 : 1);
+    return b->ck ? 2 : b->split_ck ? 4 : (b->tbpar ? 3 : 1);
 }
 
 int sed_dot_factor(const double *sub, double ins, double del, int maxmin, int ladder_maxsum, uint32_t *out) {

@@ -42,6 +42,7 @@ SED_OPT_DOT = 10
 SED_OPT_BITPAR = 11
 SED_OPT_SCALED = 12
 SED_OPT_SEG = 13
+SED_OPT_SPLITCK = 14
 MODE_NAMES = {1: "i32", 2: "f64", 3: "f64-typed"}
 
 _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
@@ -336,7 +337,8 @@ class Batch:
 
     @property
     def traceback_mode(self):
-        """0 distance only, 1 per-cell traceback codes, 2 checkpoints + recompute (SED_OPT_TB)."""
+        """0 distance only, 1 per-cell traceback codes, 2 checkpoints + recompute (SED_OPT_TB), 3 per-cell codes walked
+        stripe-parallel, 4 SPLIT checkpoints recomputed into per-cell codes (SED_OPT_SPLITCK)."""
         return self._lib.sed_batch_traceback_mode(self.ptr)
 
     def chain_stats(self):

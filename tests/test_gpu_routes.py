@@ -417,7 +417,8 @@ def test_stripe_parallel_traceback(gpu, tables, R, split):
     try:
         b, (d, ii, ln, ops) = _batch_run(gpu, packed, True, runs=2)
         try:
-            assert b.traceback_mode == (3 if R == 4 else 1) and b.rows_per_lane == R  # stripe route at R = 4
+            # stripe walk at R = 4; SPLIT batches there take the checkpoint forward + tile-parallel code recompute
+            assert b.traceback_mode == ((4 if split != 2 else 3) if R == 4 else 1) and b.rows_per_lane == R
         finally:
             b.close()
         _check_all(plan, packed, d, ii, ln, ops, script=True)
@@ -531,3 +532,43 @@ def test_dot_keys_on_random_factorable_tables(gpu):
         finally:
             for k in list(opts) + [sedgpu.SED_OPT_DOT]:
                 gpu.set_option(k, 0)
+
+
+@pytest.mark.parametrize("user,dot", [(True, True), (False, True), (True, False)])
+def test_split_checkpoint_codes_route(gpu, tables, user, dot):
+    """SPLIT script batches (config 2, GUI pairs; SED_OPT_SPLITCK): the SPLIT forward on dot keys (or distance keys
+    with SED_OPT_DOT = 2) stores checkpoints, sed_ck_codes_kernel recomputes every 64 x 64 tile's codes into the
+    per-cell code layout, and the stripe-parallel walk reads them.  Ragged pairs of 1..12 stripes (lengths not
+    multiples of 64 or 256, single-stripe pairs, n >> m, m >> n, empty sides), two runs back to back; every op vs the
+    oracle and identical to the ladder-key forward (SED_OPT_SPLITCK = 2)."""
+    A, B = _ragged(5400 + user + 2 * dot, 10, 1, 12 * 256, 1, 3000)
+    rng = np.random.default_rng(5500 + user)
+    for n, m in ((0, 40), (60, 0), (257, 5), (300, 1), (256, 64), (255, 63), (3 * 256 + 1, 2 * 256 + 3), (40, 2900),
+                 (4096, 4096)):
+        A.append(rng.integers(0, 4, size=n).astype(np.uint8))
+        B.append(rng.integers(0, 4, size=m).astype(np.uint8))
+    plan = _plan(tables[user])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs(A, B)
+    outs = []
+    try:
+        if not dot:
+            gpu.set_option(sedgpu.SED_OPT_DOT, 2)
+        for opt in (0, 2):
+            gpu.set_option(sedgpu.SED_OPT_SPLITCK, opt)
+            b, out = _batch_run(gpu, packed, True, runs=2)
+            try:
+                assert b.rows_per_lane == 4
+                assert b.traceback_mode == (4 if opt == 0 else 3)
+                if opt == 0:
+                    assert b.dot_keys == dot
+            finally:
+                b.close()
+            outs.append(out)
+    finally:
+        gpu.set_option(sedgpu.SED_OPT_SPLITCK, 0)
+        gpu.set_option(sedgpu.SED_OPT_DOT, 0)
+    d, ii, ln, ops = outs[0]
+    _check_all(plan, packed, d, ii, ln, ops, script=True)
+    for x, y in zip(outs[0], outs[1]):
+        assert np.array_equal(x, y)
