@@ -675,6 +675,7 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         // unrolled chunks take the compiler > 15 min.)
         const int c_cap = last ? cap_step >> 6 : -1;
         int s = 0;
+        int ready = 0;  // SPLIT: steps the feeder has published as ready (last read)
         for (int c = 0; c < nchunks; ++c) {
             uint32_t tnx = 0, snx = 0;
             if (c + 1 < nchunks) {
@@ -708,7 +709,10 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                     const uint32_t *ltop = lch;
                     if constexpr (SPLIT) {
                         ltop = lch + (s & (SED_SPLIT_RING - 64));
-                        if (k > 0) {  // the feeder has this group's top values in the ring (LDS only: no vmcnt)
+                        // the feeder has this group's top values in the ring (LDS only: no vmcnt).  The ready count
+                        // is re-read only when the groups it covered are used up (the feeder publishes up to 64 steps
+                        // at a time), so most groups start without an LDS round trip.
+                        if (k > 0 && ready < s + G) {
                             uint32_t f = lds_flag_get(split_flag), spins = 0;
                             while (ok && (int)(f & ~SED_PROG_POISON) < s + G) {
                                 if (++spins > (1u << 24)) ok = false;
@@ -716,6 +720,7 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                                 f = lds_flag_get(split_flag);
                             }
                             if (f & SED_PROG_POISON) ok = false;
+                            ready = (int)(f & ~SED_PROG_POISON);
                             asm volatile("" ::: "memory");
                         }
                     }
