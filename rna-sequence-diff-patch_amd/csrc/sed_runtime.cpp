@@ -1851,8 +1851,9 @@ int sed_run_batch(sed_ctx *c, const uint8_t *codes_a, const int64_t *off_a, cons
     if (npairs < 0 || (npairs > 0 && (!off_a || !len_a || !off_b || !len_b)))
         return c->fail(SED_E_ARG, "bad batch arguments");
     // Host-buffer batches are cut into chunks whose traceback workspace (2 bits per cell plus the
-    // wavefront skew) stays under SED_TB_BUDGET_GB (default 48): a list of many long pairs then
-    // runs in several launches instead of failing with SED_E_OOM.
+    // wavefront skew, and the SPLIT route's checkpoints beside its codes: ~0.13 B per cell more) stays under
+    // SED_TB_BUDGET_GB (default 48): a list of many long pairs then runs in several launches instead of failing
+    // with SED_E_OOM.
     double budget = 48e9;
     if (const char *e = getenv("SED_TB_BUDGET_GB")) budget = std::max(1e6, atof(e) * 1e9);
     int32_t p0 = 0;
@@ -1861,7 +1862,7 @@ int sed_run_batch(sed_ctx *c, const uint8_t *codes_a, const int64_t *off_a, cons
         double bytes = 0;
         if (flags & SED_WANT_SCRIPT) {
             while (p1 < npairs) {
-                const double pb = 0.25 * (double)std::max(0, len_a[p1]) * (double)(std::max(0, len_b[p1]) + 127);
+                const double pb = 0.39 * (double)std::max(0, len_a[p1]) * (double)(std::max(0, len_b[p1]) + 127);
                 if (p1 > p0 && bytes + pb > budget) break;
                 bytes += pb;
                 ++p1;

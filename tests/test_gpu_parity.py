@@ -263,7 +263,7 @@ def test_chain_mode_is_used(gpu, tables):
 
 def test_script_batches_are_chunked_by_traceback_budget(gpu, tables, monkeypatch):
     """sed_run_batch cuts a script batch into several launches when its traceback workspace
-    exceeds SED_TB_BUDGET_GB; results are unchanged (here ~30 chunks of ~1 MB)."""
+    exceeds SED_TB_BUDGET_GB; results are unchanged (here ~45 chunks of ~1 MB)."""
     pairs = _random_pairs(909, 90, "ACGU", 0, 900, related=True)
     monkeypatch.setenv("SED_TB_BUDGET_GB", "0.001")
     got = gpu_run(gpu, tables[True], pairs)
