@@ -410,6 +410,8 @@ template <bool LEN, bool DOT = false> __device__ __forceinline__ uint32_t i32_se
 // perm selector of str2 symbol b: byte3 <- 0xFF, byte2 <- cost byte b, bytes 1:0 <- the constant
 __device__ __forceinline__ uint32_t i32_sel(uint32_t b) { return 0x0D000100u | ((4u + b) << 16); }
 
+template <bool B> struct BoolTag { static constexpr bool value = B; };
+
 // CAP: the group that produces the sink cell (captured on its lane); every extra variant is
 // another merge point where the register allocator may insert copies of the whole state.
 // The stripe kernel's group: lane 0's top values from the chunk's LDS slots (ltop, broadcast reads),
@@ -676,7 +678,11 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
         const int c_cap = last ? cap_step >> 6 : -1;
         int s = 0;
         int ready = 0;  // SPLIT: steps the feeder has published as ready (last read)
-        for (int c = 0; c < nchunks; ++c) {
+        // CK (not SPLIT): the chunks before the sink's run the unrolled group loop, the sink's chunk and any after it the
+        // rolled one, as two loops: one loop choosing per chunk merged the paths, and the register allocator moved the
+        // row state in and out of the unrolled loop's registers every chunk (24 VALU per 2112)
+        auto chunk = [&](auto fast_tag, const int c) {
+            constexpr bool FASTC = decltype(fast_tag)::value;
             uint32_t tnx = 0, snx = 0;
             if (c + 1 < nchunks) {
                 if (!SPLIT) tnx = load_top(c + 1);
@@ -695,7 +701,7 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                     if (!SPLIT && lane == 63 && !last) store_words<G>(bnd + d.bnd_off + (uint32_t)s0, rcv);  // next stripe's top row
                 }
             };
-            if (CK && !SPLIT && c != c_cap) {
+            if constexpr (FASTC) {
 #pragma unroll SED_CK_GUNROLL
                 for (int g = 0; g < 64 / G; ++g) {
                     const int s0 = 64 * c + g * G;  // (s0 & 63 folds to g * G)
@@ -757,7 +763,13 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
             if (!SPLIT) lch[lane] = tch;  // after the chunk's last LDS read (in order)
             const uint32_t slot = (uint32_t)(64 * (c + 1) + lane) & 127u;  // replaces column 64(c-1) + lane
             ring[slot] = ring[slot + 128] = sch;
+        };
+        int cfast = 0;
+        if constexpr (CK && !SPLIT) {
+            cfast = c_cap >= 0 ? c_cap : nchunks;
+            for (int c = 0; c < cfast; ++c) chunk(BoolTag<true>{}, c);
         }
+        for (int c = cfast; c < nchunks; ++c) chunk(BoolTag<false>{}, c);
         if (!last) __builtin_amdgcn_s_waitcnt(0);  // own bottom-row stores done before the next stripe reads them
     }
     if (klast == nstripes - 1 && lane == cap_lane) {
