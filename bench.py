@@ -217,25 +217,58 @@ def cpu_baseline_python(table, alphabet, A, B, qa, qb, want_script, cores, secon
                       "%.1f s" % (what, "distance + canonical edit script" if want_script else "distance", dt)}
 
 
+def strided_sample(P, count):
+    """About `count` pair indices spread over all P pairs: every ceil(P / count)-th pair from pair 0, plus the last
+    pair, so the sample spans every part (SED_CK_HALVES), every residency round of the waves and every rank's shard
+    end to end (not a prefix).  Returns (indices, stride)."""
+    count = int(max(1, min(P, count)))
+    stride = -(-P // count)
+    idx = np.arange(0, P, stride, dtype=np.int64)
+    if idx[-1] != P - 1:
+        idx = np.append(idx, P - 1)
+    return idx, int(stride)
+
+
+def oracle_subset(cs, packed, idx, want_ops, threads):
+    """The C oracle over the pairs `idx` of `packed` (descriptor arrays gathered, sequence buffers shared)."""
+    import oracle
+    sel = lambda a: np.ascontiguousarray(np.asarray(a)[idx])  # noqa: E731
+    return oracle.batch(cs, packed.codes_a, sel(packed.off_a), sel(packed.len_a), packed.codes_b, sel(packed.off_b),
+                        sel(packed.len_b), len(idx), want_ops=want_ops, nthreads=threads)
+
+
 def cpu_baseline(plan, packed, seconds, threads, want_ops):
-    """Oracle (C restatement, test infrastructure) on a bounded prefix of the same pairs."""
+    """Oracle (C restatement, test infrastructure) on a bounded, strided sample of the same pairs: about `seconds`
+    of work on `threads` threads, spread over the whole batch (strided_sample)."""
     import oracle
     cs = oracle.Costs.from_plan(plan)
     P = packed.npairs
     la, lb = packed.len_a[:P], packed.len_b[:P]
-    cum = np.cumsum(la.astype(np.float64) * lb)
-    probe = int(min(P, np.searchsorted(cum, 2e6) + 1))  # ~2M cells, single thread
+    cells_p = la.astype(np.float64) * lb
+    cum = np.cumsum(cells_p)
+    probe = int(min(P, np.searchsorted(cum, 2e6) + 1))  # ~2M cells, single thread (rate probe only)
     t0 = time.perf_counter()
     oracle.batch(cs, packed.codes_a, packed.off_a, la, packed.codes_b, packed.off_b, lb, probe, want_ops=want_ops)
     per_cell = (time.perf_counter() - t0) / max(1.0, float(cum[probe - 1]))
     budget = seconds * threads / max(per_cell, 1e-12)  # cells the sample may hold
-    count = int(min(P, max(threads, np.searchsorted(cum, budget))))
+    count = int(min(P, max(threads, budget / max(1.0, float(cells_p.mean())))))
+    idx, stride = strided_sample(P, count)
     t0 = time.perf_counter()
-    dist, is_int, ln, ops, ops_off = oracle.batch(cs, packed.codes_a, packed.off_a, la, packed.codes_b,
-                                                  packed.off_b, lb, count, want_ops=want_ops, nthreads=threads)
+    dist, is_int, ln, ops, ops_off = oracle_subset(cs, packed, idx, want_ops, threads)
     dt = time.perf_counter() - t0
-    return {"value": float(cum[count - 1]) / dt, "seconds": dt, "count": count, "dist": dist, "len": ln,
-            "ops": ops, "ops_off": ops_off}
+    return {"value": float(cells_p[idx].sum()) / dt, "seconds": dt, "count": len(idx), "idx": idx, "stride": stride,
+            "dist": dist, "len": ln, "ops": ops, "ops_off": ops_off}
+
+
+def sample_exact(idx, o_dist, o_len, o_ops, o_off, dist, ln, ops, ops_off, want_script):
+    """Per sampled pair: distance, length and (script mode) every op equal to the oracle's."""
+    exact = (o_dist == dist[idx]) & ((o_len == ln[idx]) | (ln[idx] == -1))
+    if want_script:
+        for k, p in enumerate(idx):
+            if exact[k]:
+                g = sedgpu.unpack_ops(ops, ops_off, int(p), int(ln[p]))
+                exact[k] = np.array_equal(g, o_ops[o_off[k]: o_off[k] + o_len[k]])
+    return exact
 
 
 def pmc_pass(counters, kernels, timeout=240):
@@ -431,25 +464,18 @@ def valid_scripts_ragged(plan, qa, qb, dist, ln, ops, ops_off, exact_int):
     return good
 
 
-def oracle_agree(plan, packed, count, dist, ln, ops, ops_off, want_script, threads):
-    """Pairs among the first `count` of `packed` whose distance, length and every op equal the C oracle's."""
+def oracle_agree(plan, packed, idx, dist, ln, ops, ops_off, want_script, threads):
+    """Pairs among `idx` of `packed` whose distance, length and every op equal the C oracle's."""
     import oracle
     cs = oracle.Costs.from_plan(plan)
-    od, _, oln, oops, ooff = oracle.batch(cs, packed.codes_a, packed.off_a, packed.len_a, packed.codes_b,
-                                          packed.off_b, packed.len_b, count, want_ops=want_script, nthreads=threads)
-    exact = (od == dist[:count]) & ((oln == ln[:count]) | (ln[:count] == -1))
-    if want_script:
-        for p in range(count):
-            if exact[p]:
-                g = sedgpu.unpack_ops(ops, ops_off, p, int(ln[p]))
-                exact[p] = np.array_equal(g, oops[ooff[p]: ooff[p] + oln[p]])
-    return int(exact.sum())
+    od, _, oln, oops, ooff = oracle_subset(cs, packed, idx, want_script, threads)
+    return int(sample_exact(idx, od, oln, oops, ooff, dist, ln, ops, ops_off, want_script).sum())
 
 
 def verify_gathered(args, plan, P, n, m, world, gdist, glen, gops, want_script, mode, threads, seconds):
     """Rank 0 after the gather: every rank's results, checked on rank 0 (N > 1).  The script property check over
-    ALL gathered pairs (inputs regenerated from the seeds), and an oracle comparison of each rank's leading pairs
-    within `seconds` of CPU time in total.  Returns the bench line's check fields."""
+    ALL gathered pairs (inputs regenerated from the seeds), and an oracle comparison of a strided sample of each
+    rank's pairs (first to last) within `seconds` of CPU time in total.  Returns the bench line's check fields."""
     exact_int = mode == "i32"
     valid = total = agree = sampled = 0
     base = wbase = 0
@@ -469,14 +495,13 @@ def verify_gathered(args, plan, P, n, m, world, gdist, glen, gops, want_script, 
             ops = None
         wbase += words
         total += Pr
-        # oracle sample: the rank's leading pairs, about seconds / world of single-thread-equivalent work
+        # oracle sample: a strided sample over the whole rank shard, about seconds / world of work
         la, lb = packed.len_a[:Pr].astype(np.float64), packed.len_b[:Pr].astype(np.float64)
-        cum = np.cumsum(la * lb)
         budget = 1.5e8 * threads * seconds / world  # cells; the C oracle runs ~1e8-2e8 cells/s per thread
-        cnt = int(min(Pr, max(1, np.searchsorted(cum, budget))))
-        agree += oracle_agree(plan, packed, cnt, d, ln, ops, packed.ops_off, want_script, threads)
-        sampled += cnt
-        per_rank.append(cnt)
+        idx, stride = strided_sample(Pr, budget / max(1.0, float((la * lb).mean())))
+        agree += oracle_agree(plan, packed, idx, d, ln, ops, packed.ops_off, want_script, threads)
+        sampled += len(idx)
+        per_rank.append({"pairs": len(idx), "stride": stride})
         base += Pr
     out = {"verified_on_rank0": {"pairs": total, "oracle_sample_per_rank": per_rank}}
     if want_script:
@@ -693,21 +718,18 @@ def main():
                                                               batch.mode == "i32") / P
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(plan, packed, args.cpu_seconds, threads, want_script)
-            c = cpu["count"]
-            exact = (cpu["dist"] == d_gpu[:c]) & ((cpu["len"] == ln_gpu[:c]) | (ln_gpu[:c] == -1))
-            if want_script:
-                for p in range(c):
-                    if exact[p]:
-                        g = sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln_gpu[p]))
-                        o = cpu["ops"][cpu["ops_off"][p]: cpu["ops_off"][p] + cpu["len"][p]]
-                        exact[p] = np.array_equal(g, o)
+            c, idx = cpu["count"], cpu["idx"]
+            exact = sample_exact(idx, cpu["dist"], cpu["len"], cpu["ops"], cpu["ops_off"], d_gpu, ln_gpu, ops,
+                                 packed.ops_off, want_script)
             check["script_exact_rate" if want_script else "dist_exact_rate"] = float(exact.mean())
-            check["exact_sample"] = int(c)
+            check["exact_sample"] = {"pairs": int(c), "stride": cpu["stride"], "first": int(idx[0]),
+                                     "last": int(idx[-1]), "of": int(P)}
             shape = "%dx%d" % (n, m) if n else "ragged"
             cpu_obj = {"value": cpu["value"], "unit": "cells/s", "cores": threads, "kind": "port",
-                       "sample": "first %d of the %d pairs (%s, %s, %s), C oracle sed_oracle.c, %.1f s"
-                                 % (c, P, shape, costs_file, "distance + script" if want_script else "distance",
-                                    cpu["seconds"]),
+                       "sample": "%d of the %d pairs, every %d-th from pair 0 plus the last (%s, %s, %s), C oracle "
+                                 "sed_oracle.c, %.1f s" % (c, P, cpu["stride"], shape, costs_file,
+                                                           "distance + script" if want_script else "distance",
+                                                           cpu["seconds"]),
                        "cpu_model": cpu_model()}
             if not args.no_python_baseline:
                 cpu_obj["python_node_graph"] = cpu_baseline_python(
@@ -804,7 +826,7 @@ def main():
                    "parallelism": "dp%d" % world, "env": env},
         # the kernels issue VALU on most cycles and move a fraction of the HBM peak: "bound" names the VALU; the
         # HBM figures are the roofline the north star asks for (SURVEY.md 8(d) bytes), "valu" the binding one
-        "roofline": {"bound": "valu", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"bound": "valu" if valu_peak is not None else "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "time_basis": ("DP kernels' busy time per step: union of every DP launch's HIP-event interval "
                                     "over the steps of %s / steps" % time_pass) if args.timing_every == 1 else time_pass,

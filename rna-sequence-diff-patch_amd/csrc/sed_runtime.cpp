@@ -681,7 +681,9 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // (a map of every stripe's exits, then one wave per stripe segment) instead of one ~n+m step chain;
     // SED_TBPAR=0/1 overrides (A/B)
     static const int tbpar_env = [] { const char *e = getenv("SED_TBPAR"); return e ? atoi(e) : -1; }();
-    b->tbpar = want_tb && !b->ck && R == 4 && (tbpar_env < 0 ? npairs <= 64 : tbpar_env > 0);
+    // (never with fp64 pairs in 16-lane segments: the stripe kernels read the 64-lane code layout only)
+    b->tbpar = want_tb && !b->ck && R == 4 && (tbpar_env < 0 ? npairs <= 64 : tbpar_env > 0) &&
+               !(seg_ok && mode != SED_MODE_I32);
     b->tbpar_items = b->tbpar_kmax = 0;
     // SPLIT script batches: checkpoints + a tile-parallel recompute of the codes (dot or distance keys in the forward:
     // 2-3 VALU per cell against the ladder keys' 5.2 on the latency-bound stripe chain)
@@ -761,6 +763,9 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         cells += (double)nn * mm;
         in_bytes += packed ? (nn + mm) / 4.0 : (double)(nn + mm);
     }
+    // a SPLIT script batch whose pairs all have an empty side has no tile to recompute: plain per-cell codes (the
+    // traceback walks only the border)
+    if (b->split_ck && b->ck_tiles == 0) b->split_ck = false;
     // algorithmic traceback bytes: the 2-bit choice of every cell, or (CK) the checkpoints written
     tb_bytes = b->ck ? ck_bytes : cells * 0.25;
     b->tb_words = tbw;

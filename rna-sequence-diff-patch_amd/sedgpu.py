@@ -166,6 +166,11 @@ class Context:
     def set_mode(self, mode):
         """0 auto, 1 integer, 2 fp64, 3 fp64 with int typing."""
         self.set_option(SED_OPT_MODE, mode)
+        self.invalidate_costs()
+
+    def invalidate_costs(self):
+        """Forget the cached cost plan: the next set_costs() uploads its table.  Call it after any direct
+        lib.sed_set_costs / mode change that bypasses set_costs()."""
         self._cost_key = None
         self._cost_plan = None
 
@@ -506,6 +511,9 @@ class EngineClient:
 
     def set_mode(self, mode):
         self.set_option(SED_OPT_MODE, mode)
+        self.invalidate_costs()
+
+    def invalidate_costs(self):
         self._cost_key = None
 
     def set_costs(self, plan):

@@ -81,7 +81,7 @@ def test_verify_gathered_checks_every_rank():
     out = bench.verify_gathered(args, plan, P, n, m, world, gd, gl, go, True, "i32", 2, 5.0)
     assert out["script_valid_rate"] == 1.0 and out["script_exact_rate"] == 1.0
     assert out["verified_on_rank0"]["pairs"] == P * world
-    assert out["verified_on_rank0"]["oracle_sample_per_rank"] == [P, P]
+    assert out["verified_on_rank0"]["oracle_sample_per_rank"] == [{"pairs": P, "stride": 1}] * 2
     # one op of rank 1's last pair flipped: insert <-> delete keeps the length but breaks the alignment
     bad = [x.copy() for x in opsl]
     k = int(np.argmax(bad[-1] == 2))
@@ -111,3 +111,37 @@ def test_interval_union():
     # two parts staggered over 3 steps: part 0 [0,7], [10,17], [20,27]; part 1 [3,10], [13,20], [23,30]
     spans = [(10 * k, 10 * k + 7) for k in range(3)] + [(10 * k + 3, 10 * k + 10) for k in range(3)]
     assert bench.interval_union(spans) == pytest.approx(30.0)
+
+
+def test_strided_sample_spans_the_shard():
+    """The exact-rate sample runs first to last pair (every part and residency round), not a prefix."""
+    idx, stride = bench.strided_sample(8192, 1100)
+    assert stride == 8 and idx[0] == 0 and idx[-1] == 8191
+    assert np.all(np.diff(idx) <= stride) and len(idx) == 1025
+    assert (idx >= 4096).sum() > 500  # part 1 of the two CK parts
+    idx, stride = bench.strided_sample(5, 100)
+    assert stride == 1 and list(idx) == [0, 1, 2, 3, 4]
+    idx, _ = bench.strided_sample(10, 3)  # stride 4: 0, 4, 8 + the last
+    assert list(idx) == [0, 4, 8, 9]
+
+
+def test_oracle_subset_matches_full_batch():
+    import json
+    import oracle
+    import sedcost
+    import sedgpu
+    from conftest import GOLDEN
+    table = json.load(open(os.path.join(GOLDEN, "user_costs.json")))
+    plan = sedcost.build_plan(table, ["ACGU"], ["ACGU"])
+    cs = oracle.Costs.from_plan(plan)
+    rng = np.random.default_rng(5)
+    qa = [rng.integers(0, 4, int(rng.integers(1, 60))).astype(np.uint8) for _ in range(40)]
+    qb = [rng.integers(0, 4, int(rng.integers(1, 60))).astype(np.uint8) for _ in range(40)]
+    packed = sedgpu.PackedPairs(qa, qb)
+    fd, _, fl, fo, foff = oracle.batch(cs, packed.codes_a, packed.off_a, packed.len_a, packed.codes_b, packed.off_b,
+                                       packed.len_b, 40, want_ops=True)
+    idx, _ = bench.strided_sample(40, 9)
+    sd, _, sl, so, soff = bench.oracle_subset(cs, packed, idx, True, 2)
+    for k, p in enumerate(idx):
+        assert sd[k] == fd[p] and sl[k] == fl[p]
+        assert np.array_equal(so[soff[k]:soff[k] + sl[k]], fo[foff[p]:foff[p] + fl[p]])

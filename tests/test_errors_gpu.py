@@ -59,7 +59,7 @@ def test_alphabet_limit_and_bad_options(gpu):
     sub = np.ones(K * K, np.float64)
     sub_int = np.zeros(K * K, np.uint8)
     assert lib.sed_set_costs(gpu.ptr, K, sub, sub_int, 1.0, 0, 1.0, 0) == 0
-    gpu._cost_key = None
+    gpu.invalidate_costs()
     with pytest.raises(sedgpu.SedError, match="exceeds"):
         gpu.run(_packed([1, 39], [2]), False)
     assert lib.sed_set_option(gpu.ptr, sedgpu.SED_OPT_ROWS_PER_LANE, 3) == -1

@@ -572,3 +572,77 @@ def test_split_checkpoint_codes_route(gpu, tables, user, dot):
     _check_all(plan, packed, d, ii, ln, ops, script=True)
     for x, y in zip(outs[0], outs[1]):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("user", [False, True])
+def test_split_checkpoint_window_walk(gpu, tables, user):
+    """SPLIT script batches of 65..256 pairs: the SPLIT checkpoint forward and the tile-parallel code recompute, then
+    the window walk (sed_traceback_window_kernel) over the plain op codes (tb_ladder off), since the stripe-parallel
+    walk takes <= 64 pairs only.  100 ragged pairs of 257..1500 (some with an empty side), every op vs the oracle and
+    identical to the ladder-key forward (SED_OPT_SPLITCK = 2)."""
+    A, B = _ragged(5600 + user, 96, 257, 1500, 1, 1500)
+    rng = np.random.default_rng(5610 + user)
+    for n, m in ((300, 0), (0, 700), (1024, 1), (257, 1500)):
+        A.append(rng.integers(0, 4, size=n).astype(np.uint8))
+        B.append(rng.integers(0, 4, size=m).astype(np.uint8))
+    plan = _plan(tables[user])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs(A, B)
+    outs = []
+    try:
+        for opt in (0, 2):
+            gpu.set_option(sedgpu.SED_OPT_SPLITCK, opt)
+            b, out = _batch_run(gpu, packed, True, runs=2)
+            try:
+                assert b.rows_per_lane == 4 and b.traceback_mode == (4 if opt == 0 else 1)
+            finally:
+                b.close()
+            outs.append(out)
+    finally:
+        gpu.set_option(sedgpu.SED_OPT_SPLITCK, 0)
+    _check_all(plan, packed, *outs[0], script=True)
+    _same(outs[1], outs[0], packed.ops_off)
+
+
+def test_split_script_batch_with_only_empty_sides(gpu, tables):
+    """A SPLIT script batch (n > 256) whose every pair has an empty side has no tile to recompute: it must run on
+    per-cell codes (the border walk), not fail the code-recompute launch.  wagnerFisher(s1, "") with len(s1) > 256
+    followed by the script is the GUI's way there (sed_run_pair), and a small batch of such pairs (all-delete and
+    all-insert scripts) the batch way; both vs the oracle."""
+    plan = _plan(tables[True])
+    gpu.set_costs(plan)
+    rng = np.random.default_rng(5700)
+    a = rng.integers(0, 4, size=300).astype(np.uint8)
+    d, ii, ln, ops = gpu.run_pair(a.tobytes(), b"", True)
+    packed1 = sedgpu.PackedPairs([a], [np.zeros(0, np.uint8)])
+    _check_all(plan, packed1, np.array([d]), np.array([ii]), np.array([ln], np.int32), ops)
+    A = [rng.integers(0, 4, size=n).astype(np.uint8) for n in (300, 0, 4096, 257)]
+    B = [rng.integers(0, 4, size=m).astype(np.uint8) for m in (0, 900, 0, 0)]
+    packed = sedgpu.PackedPairs(A, B)
+    b, out = _batch_run(gpu, packed, True, runs=2)
+    try:
+        assert b.traceback_mode in (1, 3)
+    finally:
+        b.close()
+    _check_all(plan, packed, *out, script=True)
+
+
+def test_checkpoint_two_residency_rounds_every_pair(gpu, tables):
+    """More checkpoint wave pairs than the forward kernel holds resident at once (5 waves per SIMD x 1024 SIMDs =
+    5120): 5600 ragged pairs of 1000..1500 (related and unrelated) under automatic options take R = 16, checkpoints +
+    recompute, dot keys and 2 parts on 2 streams, and the second residency round of each part runs.  Two runs back
+    to back; EVERY pair vs the multithreaded oracle op by op (StringEditDistance.py:133-334), not a sample."""
+    A, B = _ragged(5800, 5600, 1000, 1500, 1000, 1500)
+    la = np.array([len(x) for x in A], np.float64)
+    lb = np.array([len(x) for x in B], np.float64)
+    assert (la * lb).sum() >= 512 * (la + lb).sum()  # the automatic checkpoint rule (sed_runtime.cpp: b->ck)
+    plan = _plan(tables[True])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs(A, B)
+    b, (d, ii, ln, ops) = _batch_run(gpu, packed, True, runs=2)
+    try:
+        assert b.mode == "i32" and b.rows_per_lane == 16 and b.traceback_mode == 2
+        assert b.dp_launches == 2 and b.dot_keys and b.chains == 0 and b.lane_pairs == 0
+    finally:
+        b.close()
+    _check_all(plan, packed, d, ii, ln, ops)
