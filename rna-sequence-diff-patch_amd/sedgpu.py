@@ -7,16 +7,24 @@ wagnerFisher in the GUI process (gui.py:360), then IRMethods.create_search_threa
 forks a multiprocessing.Process per similarity method and again for wf_score
 (IRMethods.py:487-491, 511-514).  HIP cannot be used in a child forked after the
 parent initialised it.  context() therefore returns, in such a child, an
-EngineClient: on first use the child starts one engine worker (a fresh
-interpreter running this file, which owns its own HIP context) and sends every
-call to it over a pipe.  Processes that never inherited a HIP context use the
-GPU directly.  SED_ENGINE=worker keeps HIP out of the calling process always;
-SED_ENGINE=inproc forbids the worker (a forked child then raises SedError).
-An inherited Context is never touched by the child (not even by __del__).
+EngineClient that sends every call to an engine that owns a HIP context:
+  - by default the parent itself: every fork of a process that holds a Context
+    gets a socket pair, and a thread of the parent serves that child's requests
+    on a Context of its own (created on the child's first call, closed when the
+    child goes away).  A child pays no start-up beyond that sed_create, which is
+    what create_search_threads' two Process rounds need;
+  - otherwise (SED_FORK_ENGINE=worker, a grandchild, or a fork taken while no
+    Context existed) the child starts one engine worker, a fresh interpreter
+    running this file, and talks to it over a pipe pair.
+Processes that never inherited a HIP context use the GPU directly.
+SED_ENGINE=worker keeps HIP out of the calling process always; SED_ENGINE=inproc
+forbids both (a forked child then raises SedError).  An inherited Context is
+never touched by the child (not even by __del__).
 """
 import ctypes as C
 import os
 import pickle
+import socket
 import subprocess
 import sys
 import threading
@@ -450,15 +458,27 @@ class EngineClient:
     engine worker process: a fresh interpreter running this file, started on first use, that owns its
     own HIP context.  One request at a time over a pipe pair; the worker exits when the pipe closes."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, channel=None):
         self.device = device
         self._proc = None
         self._tx = self._rx = None
         self._cost_key = None
         self._pid = os.getpid()
+        self._channel = channel  # this process's socket to its parent's engine thread (None: start a worker)
+        self.served_by = None
 
     def _start(self):
         from multiprocessing.connection import Connection
+        if self._channel is not None:  # the parent serves this child (see the module docstring)
+            sock, self._channel = self._channel, None
+            self._tx = self._rx = Connection(sock.detach())
+            self.served_by = "parent"
+            self._tx.send_bytes(pickle.dumps(("open", self.device), protocol=pickle.HIGHEST_PROTOCOL))
+            status, val = pickle.loads(self._rx.recv_bytes())
+            if status != "ok":
+                raise SedError(val)
+            return
+        self.served_by = "worker"
         c2w_r, c2w_w = os.pipe()
         w2c_r, w2c_w = os.pipe()
         env = dict(os.environ)
@@ -476,7 +496,7 @@ class EngineClient:
     def _call(self, *req):
         if self._pid != os.getpid():  # a fork of a process with a client: start its own worker
             self.__init__(self.device)
-        if self._proc is None:
+        if self._tx is None:
             self._start()
         try:
             self._tx.send_bytes(pickle.dumps(req, protocol=pickle.HIGHEST_PROTOCOL))
@@ -488,17 +508,19 @@ class EngineClient:
         return val
 
     def close(self):
-        if self._proc is not None and self._pid == os.getpid():
-            for f in (self._tx, self._rx):
+        if self._tx is not None and self._pid == os.getpid():
+            for f in {id(self._tx): self._tx, id(self._rx): self._rx}.values():
                 try:
                     f.close()
                 except OSError:
                     pass
-            try:
-                self._proc.wait(timeout=10)
-            except subprocess.TimeoutExpired:
-                self._proc.kill()
+            if self._proc is not None:
+                try:
+                    self._proc.wait(timeout=10)
+                except subprocess.TimeoutExpired:
+                    self._proc.kill()
         self._proc = None
+        self._tx = self._rx = None
 
     def __del__(self):
         try:
@@ -547,10 +569,8 @@ class _PlanArgs:
         return (self.K, self.sub.tobytes(), self.sub_int.tobytes(), self.ins, self.ins_int, self.dele, self.del_int)
 
 
-def _engine_worker(device, rfd, wfd):
-    """Serve EngineClient requests until the client closes the pipe."""
-    from multiprocessing.connection import Connection
-    rx, tx = Connection(rfd, writable=False), Connection(wfd, readable=False)
+def _serve(rx, tx, device):
+    """Serve EngineClient requests on one Context until the client closes its end."""
     ctx = None
     while True:
         try:
@@ -558,10 +578,14 @@ def _engine_worker(device, rfd, wfd):
         except (EOFError, OSError):
             break
         try:
+            op, args = req[0], req[1:]
+            if op == "open":  # (a parent-served child names its device first)
+                device = args[0]
             if ctx is None:
                 ctx = Context(device)
-            op, args = req[0], req[1:]
-            if op == "set_costs":
+            if op == "open":
+                val = None
+            elif op == "set_costs":
                 ctx.set_costs(_PlanArgs(*args))
                 val = None
             elif op == "set_option":
@@ -580,9 +604,51 @@ def _engine_worker(device, rfd, wfd):
             out = ("ok", val)
         except Exception as ex:  # reported to the client as SedError
             out = ("err", "%s: %s" % (type(ex).__name__, ex))
-        tx.send_bytes(pickle.dumps(out, protocol=pickle.HIGHEST_PROTOCOL))
+        try:
+            tx.send_bytes(pickle.dumps(out, protocol=pickle.HIGHEST_PROTOCOL))
+        except OSError:
+            break
     if ctx is not None:
         ctx.close()
+
+
+def _engine_worker(device, rfd, wfd):
+    """The worker process's main loop."""
+    from multiprocessing.connection import Connection
+    _serve(Connection(rfd, writable=False), Connection(wfd, readable=False), device)
+
+
+def _serve_child(sock):
+    """Thread of a HIP process serving one forked child over its socket pair."""
+    from multiprocessing.connection import Connection
+    conn = Connection(sock.detach())
+    try:
+        _serve(conn, conn, 0)
+    finally:
+        conn.close()
+
+
+# fork hooks: a process holding a HIP Context gives each fork a socket pair to a serving thread of its own
+_fork_pair = None
+_child_channel = None  # (socket, pid) in a child forked from a HIP process
+
+
+def _before_fork():
+    global _fork_pair
+    _fork_pair = None
+    if _hip_pid == os.getpid() and os.environ.get("SED_FORK_ENGINE", "parent") == "parent":
+        try:
+            _fork_pair = socket.socketpair(socket.AF_UNIX, socket.SOCK_STREAM)
+        except OSError:
+            _fork_pair = None
+
+
+def _after_fork_in_parent():
+    global _fork_pair
+    pair, _fork_pair = _fork_pair, None
+    if pair is not None:
+        pair[1].close()
+        threading.Thread(target=_serve_child, args=(pair[0],), daemon=True, name="sed-engine-fork").start()
 
 
 _ctx = None
@@ -590,18 +656,24 @@ _ctx_pid = None
 
 
 def _reset_lock_in_child():
-    global _lock
+    global _lock, _fork_pair, _child_channel
     _lock = threading.Lock()  # a fork taken while another thread held it must not deadlock the child
+    pair, _fork_pair = _fork_pair, None
+    if pair is not None:
+        pair[0].close()
+        _child_channel = (pair[1], os.getpid())
+    else:
+        _child_channel = None
 
 
 if hasattr(os, "register_at_fork"):
-    os.register_at_fork(after_in_child=_reset_lock_in_child)
+    os.register_at_fork(before=_before_fork, after_in_parent=_after_fork_in_parent, after_in_child=_reset_lock_in_child)
 
 
 def context(device=None):
     """Process-wide default engine (device from SED_DEVICE / LOCAL_RANK, else 0): an in-process Context,
     or an EngineClient in a child forked after its parent initialised HIP (or with SED_ENGINE=worker)."""
-    global _ctx, _ctx_pid
+    global _ctx, _ctx_pid, _child_channel
     with _lock:
         pid = os.getpid()
         if _ctx is None or _ctx_pid != pid:
@@ -610,7 +682,9 @@ def context(device=None):
             mode = os.environ.get("SED_ENGINE", "auto")
             inherited = _hip_pid is not None and _hip_pid != pid
             if mode == "worker" or (inherited and mode != "inproc"):
-                _ctx = EngineClient(device)
+                ch = _child_channel[0] if (_child_channel and _child_channel[1] == pid and mode != "worker") else None
+                _child_channel = None  # (one client per channel)
+                _ctx = EngineClient(device, ch)
             else:
                 _ctx = Context(device)  # raises SedError in a fork of a HIP process (SED_ENGINE=inproc)
             _ctx_pid = pid

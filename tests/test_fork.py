@@ -1,9 +1,10 @@
 """CPU: the drop-in module under the reference's process model (IRMethods.create_search_threads forks a
 multiprocessing.Process per method after gui.py ran wagnerFisher in the parent, IRMethods.py:487-491,
 511-514).  A child forked after its parent initialised HIP must never call into the inherited context:
-sedgpu.context() gives it an engine worker process instead (SED_ENGINE=inproc: a clear SedError).  Here
-the parent's HIP initialisation is simulated (no GPU in this container), so the worker itself reports
-that no device exists -- as an error, within seconds, not a hang."""
+sedgpu.context() gives it an EngineClient served by a thread of the parent on a Context of its own (or, with
+SED_FORK_ENGINE=worker, by an engine worker process; SED_ENGINE=inproc: a clear SedError).  Here the parent's
+HIP initialisation is simulated (no GPU in this container), so the serving Context itself reports that no
+device exists -- as an error, within seconds, not a hang."""
 import multiprocessing as mp
 import os
 
@@ -20,10 +21,12 @@ class _NoCallLib:
         raise AssertionError("child called %s on the parent's HIP context" % name)
 
 
-def _child(q, engine):
+def _child(q, engine, fork_engine=None):
     try:
         if engine is not None:
             os.environ["SED_ENGINE"] = engine
+        if fork_engine is not None:
+            os.environ["SED_FORK_ENGINE"] = fork_engine
         inherited = sedgpu._ctx
         inherited.close()  # must not touch the parent's context
         assert inherited.ptr is None
@@ -32,11 +35,11 @@ def _child(q, engine):
         packed = sedgpu.PackedPairs([np.array([0, 1, 2], np.uint8)], [np.array([0, 2], np.uint8)])
         try:
             ctx.run(packed, False)
-            q.put((kind, "no error"))
+            q.put((kind, "no error", ctx.served_by))
         except sedgpu.SedError as ex:
-            q.put((kind, str(ex)))
+            q.put((kind, str(ex), ctx.served_by))
     except BaseException as ex:  # reported to the parent
-        q.put(("crash", repr(ex)))
+        q.put(("crash", repr(ex), None))
 
 
 def _fake_parent_context():
@@ -46,23 +49,30 @@ def _fake_parent_context():
     return c
 
 
-@pytest.mark.parametrize("engine", [None, "inproc"])
-def test_forked_child_never_uses_the_parents_hip_context(monkeypatch, engine):
+@pytest.mark.parametrize("engine,fork_engine", [(None, None), (None, "worker"), ("inproc", None)])
+def test_forked_child_never_uses_the_parents_hip_context(monkeypatch, engine, fork_engine):
+    """Default: the parent serves the child on a Context of its own (a thread per fork, over a socket pair);
+    SED_FORK_ENGINE=worker: the child starts an engine worker; SED_ENGINE=inproc: the child raises."""
     monkeypatch.setattr(sedgpu, "_hip_pid", os.getpid())
     monkeypatch.setattr(sedgpu, "_ctx", _fake_parent_context())
     monkeypatch.setattr(sedgpu, "_ctx_pid", os.getpid())
     monkeypatch.delenv("SED_ENGINE", raising=False)
+    monkeypatch.delenv("SED_FORK_ENGINE", raising=False)
+    if fork_engine:
+        monkeypatch.setenv("SED_FORK_ENGINE", fork_engine)  # (read by the parent's fork hook too)
     fork = mp.get_context("fork")
     q = fork.Queue()
-    p = fork.Process(target=_child, args=(q, engine))
+    p = fork.Process(target=_child, args=(q, engine, fork_engine))
     p.start()
-    kind, msg = q.get(timeout=120)
+    kind, msg, served = q.get(timeout=120)
     p.join(timeout=60)
     assert p.exitcode == 0
     if engine == "inproc":
         assert kind == "crash" and "fork" in msg  # context() refuses to build a Context in the fork
     else:
         assert kind == "EngineClient", msg
+        assert served == (fork_engine or "parent")
+        # no device here: the serving Context (the parent's thread, or the worker) reports it as SedError
         assert "sed_create(0) failed" in msg or "libsed.so not found" in msg, msg
     sedgpu._ctx.ptr = None  # the fake must not reach sed_destroy here either
 
