@@ -625,32 +625,42 @@ def load_es(path):
 # ---------------------------------------------------------------------------
 # batch extensions (not in the reference): one launch for many pairs
 # ---------------------------------------------------------------------------
-def distance_batch(strs1, strs2, userCosts=False):
-    """[dp[n][m].value for each (str1, str2)] — one GPU launch; same typing and KeyErrors."""
+def batch_plan(strs1, strs2, userCosts=False):
+    """The reference's KeyError for the first offending pair, if any (sedcost.check_batch), then the batch's plan."""
     table = _table(userCosts)
-    for a, b in zip(strs1, strs2):
-        sedcost.check_pair(table, a, b)
+    sedcost.check_batch(table, strs1, strs2)
+    return sedcost.build_plan(table, strs1, strs2)
+
+
+def _packed(plan, strs1, strs2):
+    ca, la = plan.encode_many(strs1)
+    cb, lb = plan.encode_many(strs2)
+    return sedgpu.PackedPairs.from_concat(ca, la, cb, lb)
+
+
+def distance_batch(strs1, strs2, userCosts=False, plan=None):
+    """[dp[n][m].value for each (str1, str2)] — one GPU launch; same typing and KeyErrors.  plan: batch_plan()'s
+    result for the same arguments (wfsearch builds it once for its cache key)."""
+    strs1, strs2 = list(strs1), list(strs2)
+    if plan is None:
+        plan = batch_plan(strs1, strs2, userCosts)
     if not strs1:
         return []
-    plan = sedcost.build_plan(table, strs1, strs2)
     ctx = sedgpu.context()
     ctx.set_costs(plan)
-    packed = sedgpu.PackedPairs([plan.encode(a) for a in strs1], [plan.encode(b) for b in strs2])
-    dist, is_int, _, _ = ctx.run(packed, False, no_len=True)
+    dist, is_int, _, _ = ctx.run(_packed(plan, strs1, strs2), False, no_len=True)
     return [int(d) if t else float(d) for d, t in zip(dist.tolist(), is_int.tolist())]
 
 
 def edit_script_batch(strs1, strs2, userCosts=False):
     """[(value, generate_es(create_paths(dp)[0], s1, s2))] for each pair — one GPU launch."""
-    table = _table(userCosts)
-    for a, b in zip(strs1, strs2):
-        sedcost.check_pair(table, a, b)
+    strs1, strs2 = list(strs1), list(strs2)
+    plan = batch_plan(strs1, strs2, userCosts)
     if not strs1:
         return []
-    plan = sedcost.build_plan(table, strs1, strs2)
     ctx = sedgpu.context()
     ctx.set_costs(plan)
-    packed = sedgpu.PackedPairs([plan.encode(a) for a in strs1], [plan.encode(b) for b in strs2])
+    packed = _packed(plan, strs1, strs2)
     dist, is_int, ln, ops = ctx.run(packed, True)
     out = []
     for p, (a, b) in enumerate(zip(strs1, strs2)):

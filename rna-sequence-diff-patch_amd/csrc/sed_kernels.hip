@@ -2414,6 +2414,291 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
     ck_traceback_pair<R, false>(d, pair, q0, lane, seqa, seqb, ck, res, ops, prm, topb, selb);
 }
 
+// ---------------------------------------------------------------------------
+// Checkpoint traceback replaying the forward lanes (sed_traceback_ckr_kernel, round 5; the default at R = 16).
+// A 64-row tile is G = 64/R forward lanes of R rows, and the forward kernel computed it in the 64 steps of one chunk,
+// each lane starting from its own column checkpoint (chunk c-1's end), lane 0 of the tile taking the row above from
+// the row checkpoints.  Replaying exactly that -- G lanes of R rows on the forward's systolic schedule, in ladder keys
+// with per-cell codes (i32_step's cell: v_perm, v_add, v_min3, v_and_or, v_alignbit, + the delete add on 3 of 16
+// rows) -- recomputes the whole tile in 64 steps, where the lane-per-row sweep of sed_traceback_ck_kernel needs up to
+// 127 (its staircase ramps over 64 lanes) at 6 VALU per cell.  A pair's G lanes are a G-th of a wave, so a wave
+// carries NP = 64/G = R pairs, each at its own tile, in lockstep (pair slot s = lanes s G .. s G + G - 1):
+//   1. every lane loads its tile's boundary (its R + 1 column-checkpoint words, a share of the slot's 64 top values
+//      and 63 + G str2 selectors, converted to ladder keys and staged in LDS);
+//   2. the sweep runs as many steps as the furthest entry cell of the wave needs, storing each lane's codes per
+//      G-step group in LDS ([lane][group] uint4: code of step u, row r at bits 2 ((u R + r) & 15) of word (u R + r) / 16);
+//   3. every slot's walker lane (band 0) walks its path through the codes from the entry cell until it leaves the
+//      tile (above it, left of its band's checkpoint column, or at column 0), emitting ops from the sink as before;
+//   4. the exit cell's L (decoded from the top row or the column checkpoint it leaves through) must equal the ops
+//      still to emit (SED_ERR_TB_CHECK: a corrupt checkpoint), and the slot's state goes to its other lanes.
+// The walk is vector code (one op per iteration for every walker at once; ~26 VALU and one LDS read per op).
+// ---------------------------------------------------------------------------
+// forward key (distance or dot) -> the ladder key of the same (D, L) with op 0 on rung c:
+// W = ((D - i del - j ins) << 16) - 8U + SED_KB3 + c, U = i + j - L (the updates on the path)
+__device__ __forceinline__ uint32_t ck_to_lad(uint32_t w, const sed_i32_params &prm, uint32_t c) {
+    if (prm.dot) {  // k = A X + U, D - i del - j ins = -X
+        const uint32_t k = w - SED_KB_DOT;
+        const uint32_t X = __umulhi(k, prm.dotM) >> (prm.dotS - 32u);
+        const uint32_t U = k - __umul24(prm.dotA, X);
+        return SED_KB3 + c - (X << 16) - 8u * U;
+    }
+    const uint32_t U = (SED_KB - w) & 0xFFFFu;  // w = ((D - i del - j ins) << 16) - U + SED_KB
+    return w - 7u * U + (SED_KB3 - SED_KB) + c;
+}
+
+// One forward step of a replayed lane (i32_step's ladder-key cell with codes): the cell above the lane's band comes
+// from the lane before it, except on a slot's band 0 (the leader), which takes topin (the tile's row above); at R = 4
+// a slot is one DPP row and row_shr:1 leaves the leader its `old` operand.
+template <int R>
+__device__ __forceinline__ void ckr_step(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
+                                         uint32_t &bottom, const uint32_t topin, const uint32_t selv,
+                                         const bool leader, uint32_t (&W)[4], const int u) {
+    using Lad = Ladder<R>;
+    constexpr int d0 = Lad::rung(1) - Lad::rung(0);
+    const uint32_t dg0 = top_prev + __builtin_amdgcn_perm(cv[0], (uint32_t)(d0 - 6), selv);
+    uint32_t topv;
+    if constexpr (R == 4) {
+        topv = seg_shr1<16>(topin, bottom);
+    } else {
+        topv = dpp_shr1(topin, bottom);
+        topv = leader ? topin : topv;
+    }
+    uint32_t up = topv, diag = top_prev;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t left = V[r];
+        const int c = Lad::rung(r + 1), d = c - Lad::rung(r);  // compile-time after unrolling
+        const uint32_t mm = umin3(left, d == -1 ? up : up + (uint32_t)(d + 1),
+                                  r == 0 ? dg0 : diag + __builtin_amdgcn_perm(cv[r], (uint32_t)(d - 6), selv));
+        const int k = u * R + r;
+        W[k >> 4] = __builtin_amdgcn_alignbit(mm, W[k >> 4], 2);
+        up = (mm & ~7u) | (uint32_t)c;
+        diag = left;
+        V[r] = up;
+    }
+    top_prev = topv;
+    bottom = V[R - 1];
+}
+
+// (a VGPR budget like the forward kernel's, 5 waves per SIMD: unbounded, the scheduler hoisted every step's v_perm of a
+// group ahead of the min chain, 183 VGPRs at R = 16, and this kernel runs beside the forward kernel's waves.  The LDS is
+// dynamic: with its static size the compiler saw an occupancy of 1-2 waves per SIMD and ignored the budget)
+#ifndef SED_CKR_WAVES
+#define SED_CKR_WAVES(R) ((R) == 16 ? 4 : 5)
+#endif
+template <int R> struct CkrLds {
+    static constexpr int G = 64 / R, NP = 64 / G, NG = 64 / G, SELN = 64 + G;
+    // words: codes [64 lanes][NG groups][4], top [NP][64], sel [NP][SELN], left [R][64], raw [NP][8], state [NP][4]
+    static constexpr int codes = 0, top = codes + 64 * NG * 4, sel = top + NP * 64, left = sel + NP * SELN,
+                         raw = left + R * 64, st = raw + NP * 8, words = st + NP * 4;
+};
+template <int R>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SED_CKR_WAVES(R)))) void sed_traceback_ckr_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
+                                                               const uint32_t *__restrict__ seqa,
+                                                               const uint32_t *__restrict__ seqb,
+                                                               const uint32_t *__restrict__ ck,
+                                                               sed_result *__restrict__ res,
+                                                               uint32_t *__restrict__ ops, sed_i32_params prm) {
+    static_assert(R == 4 || R == 8 || R == 16, "R in {4, 8, 16}");
+    constexpr int ROWS = 64 * R, G = Grp<R>::G, NP = 64 / G, NG = 64 / G;  // NP pairs per wave, NG groups per sweep
+    constexpr int LR = R == 4 ? 2 : R == 8 ? 3 : 4, LG = 6 - LR;
+    constexpr int SELN = 64 + G;  // selectors of a slot: column J0 - (G - 1) + x, x < 63 + G
+    constexpr uint64_t PAT = Ladder<R>::pat;
+    constexpr int P = Ladder<R>::P;
+    using LD = CkrLds<R>;
+    extern __shared__ uint4 ckr_lds[];  // CkrLds<R>::words * 4 bytes (sed_launch_traceback_ck)
+    uint32_t *lw = reinterpret_cast<uint32_t *>(ckr_lds);
+    uint4 *lcodes = ckr_lds;
+    auto ltop = reinterpret_cast<uint32_t (*)[64]>(lw + LD::top);
+    auto lsel = reinterpret_cast<uint32_t (*)[SELN]>(lw + LD::sel);
+    auto lleft = reinterpret_cast<uint32_t (*)[64]>(lw + LD::left);
+    auto lraw = reinterpret_cast<uint32_t (*)[8]>(lw + LD::raw);
+    int4 *lst = reinterpret_cast<int4 *>(lw + LD::st);
+    const int lane = threadIdx.x, slot = lane / G, b = lane % G;
+    const int pair = (int)blockIdx.x * NP + slot;
+    bool live = pair < npairs;
+    sed_pair_desc d{};
+    if (live) d = pd[pair];
+    live = live && !d.lane;
+    const int n = live ? d.n : 0, m = live ? d.m : 0;
+    int i = n, j = m, err = 0;
+    uint32_t q = live ? (uint32_t)res[pair].len : 0u;
+    const int nstripes = (n + ROWS - 1) / ROWS;
+    const int SG = (m + 63 + G - 1) / G * G, nchunks = (SG + 63) >> 6, ngroups = SG / G;
+    const uint32_t *ccp = ck + d.tb_off;
+    const uint32_t *rcp = ccp + sed_ck_col_words(R, nstripes, nchunks);
+    const uint32_t *pa = seqa + d.a_off, *pb = seqb + d.b_off;
+    uint32_t *out = ops + d.ops_off;
+    uint64_t acc = 0;  // (walker) the last 32 ops, the latest (position q) in bits 1:0
+    const uint32_t Kd = (prm.del << 16) + 8u, Ki = (prm.ins << 16) + 8u;
+    (void)Kd;
+    (void)Ki;
+    int guard = 2 * (n + m) + 8;
+    const bool walker = b == 0;
+    // key L of a cell (ladder key w of cell (ii, jj)) == q?
+    auto l_ok = [&](uint32_t w, int ii, int jj) {
+        return (uint32_t)i32_decode<R, true>(w, ii, jj, prm).y == q;
+    };
+    while (true) {
+        const bool act = live && err == 0 && i > 0 && j > 0;  // (uniform per slot)
+        if (!__any(act)) break;
+        // ---- the tile of the slot's cell (i, j) ----
+        int k = 0, Q = 0, c = 0, rowbase = 0, J0 = 0, sge = -1;
+        if (act) {
+            k = (i - 1) / ROWS;
+            const int t = ((i - 1) % ROWS) >> LR;
+            Q = t / G;
+            c = (j - 1 + t) >> 6;
+            rowbase = k * ROWS + 64 * Q;
+            J0 = 64 * c - G * Q + 1;
+            sge = j - J0 + ((i - rowbase - 1) >> LR);  // the entry cell's step in the chunk
+        }
+        int smax = 0;  // steps the sweep needs: the furthest entry of the wave
+#pragma unroll
+        for (int s = 0; s < NP; ++s) smax = max(smax, __builtin_amdgcn_readlane(sge, s * G) + 1);
+        const int ng = (smax + G - 1) / G;
+        // ---- boundary: cost rows, column checkpoints, top row and selectors (staged in LDS) ----
+        const int tl = G * Q + b;                        // this lane's forward lane
+        const int row0 = min(rowbase + R * b, max(n - 1, 0));  // 0-based str1 index of its first row (clamped)
+        const uint32_t wa = act ? pa[row0 >> 4] >> (2 * (row0 & 15)) : 0u;
+        uint32_t cv[R], V[R], top_prev, bottom;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t a = (wa >> (2 * r)) & 3u;
+            cv[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
+        }
+        if (act && c >= 1) {
+            const uint32_t *cp = ccp + sed_ck_col_word(R, k, nchunks, c - 1, 0, tl);
+            uint32_t w[R + 1];
+#pragma unroll
+            for (int r = 0; r <= R; ++r) w[r] = cp[r * 64];
+#pragma unroll
+            for (int r = 0; r < R; ++r) V[r] = ck_to_lad(w[r], prm, (uint32_t)Ladder<R>::rung(r + 1));
+            top_prev = ck_to_lad(w[R], prm, 0u);
+        } else {
+            i32_reset<R, true>(V, top_prev);
+        }
+        bottom = V[R - 1];
+#pragma unroll
+        for (int r = 0; r < R; ++r) lleft[r][lane] = V[r];
+        // the row above the tile at column J0 + x (x = b + G u): the row checkpoints of forward lane G Q - 1, or
+        // lane 63 of the stripe above, at the step that lane computed the column (clamped to the stripe: past
+        // SG the columns are beyond m and never walked); row 0 and columns <= 0 hold the border
+        // (lane b's steps s0 + G u share one address: group (s0 >> LG) + u, slot s0 & (G - 1), so the loads take immediate
+        // offsets; steps outside the stripe's [0, SG) are not loaded)
+        const bool above = Q >= 1 || k >= 1;
+        const int kr = Q >= 1 ? k : k - 1, tr = Q >= 1 ? G * Q - 1 : 63;
+        const int s0 = (Q >= 1 ? 64 * c - 1 : 64 * c + 63) + b;  // (>= -1)
+        const uint32_t *rb = rcp + sed_ck_row_word(R, max(kr, 0), ngroups, 0, tr) +
+                             (int64_t)(s0 >> LG) * SED_CK_RW + (s0 & (G - 1));
+        // str2's packed words of the slot's columns J0 - G .. J0 + 63: at most 6 (R = 16) .. 7 (R = 4) words from
+        // word wb0, two per lane, staged raw in LDS
+        const int wb0 = max(J0 - G, 0) >> 4;
+        const int bw = (max(m, 1) - 1) >> 4;
+#pragma unroll
+        for (int h = 0; h < 2 * 4 / G + 1; ++h) {
+            const int x = b + G * h;
+            if (x < 8) lraw[slot][x] = act ? pb[min(wb0 + x, bw)] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 64 / G; ++u) {
+            const int x = b + G * u;
+            uint32_t v = SED_KB3;
+            if (act && above && J0 + x >= 1 && s0 + G * u < SG) v = ck_to_lad(rb[u * SED_CK_RW], prm, 0u);
+            ltop[slot][x] = v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < SELN / G; ++u) {
+            const int x = b + G * u;
+            const int col = J0 - (G - 1) + x;
+            const int ci = min(max(col - 1, 0), max(m - 1, 0));
+            const uint32_t wb = lraw[slot][min((ci >> 4) - wb0, 7)];
+            lsel[slot][x] = col < 1 ? SED_SEL_SENT3 : i32_sel((wb >> ((ci & 15) * 2)) & 3u);
+        }
+        __syncthreads();
+        // ---- sweep: forward steps 64 c .. 64 c + G ng - 1 of the tile's G lanes ----
+        {
+            const uint32_t *tp = ltop[slot];
+            const uint32_t *sp = lsel[slot] + (G - 1 - b);  // this lane's column at step x: J0 - b + x
+            const bool leader = b == 0;
+            for (int g = 0; g < ng; ++g) {
+                uint32_t W[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int u = 0; u < G; ++u) ckr_step<R>(V, cv, top_prev, bottom, tp[G * g + u], sp[G * g + u], leader, W, u);
+                lcodes[lane * NG + g] = make_uint4(W[0], W[1], W[2], W[3]);
+            }
+        }
+        __syncthreads();
+        // ---- walk: each slot's walker from the entry cell until it leaves the tile ----
+        if (walker && act) {
+            const uint32_t *cw = reinterpret_cast<const uint32_t *>(lcodes) + (uint32_t)slot * (uint32_t)(G * NG * 4);
+            int rt = i - rowbase - 1, sg = sge;
+            const uint32_t qin = q;
+            while (true) {
+                const int lb = rt >> LR, rr = rt & (R - 1);
+                const int kk = (sg & (G - 1)) * R + rr;
+                const uint32_t word = cw[((lb * NG + (sg >> LG)) << 2) + (kk >> 4)];
+                const uint32_t code = (word >> (2 * (kk & 15))) & 3u;
+                const uint32_t op = (code - (uint32_t)((PAT >> (4 * ((rr + 1) & (P - 1)))) & 0xFu)) & 3u;
+                if (q == 0u || op == 3u) {  // (a code outside the ladder's range: a corrupt tile)
+                    err = q == 0u ? SED_ERR_TB_LENGTH : SED_ERR_TB_CHECK;
+                    break;
+                }
+                acc = (acc << 2) | op;
+                if ((--q & 15u) == 0u) out[q >> 4] = (uint32_t)acc;
+                if (op == 0u) {
+                    sg -= 1;
+                } else {
+                    sg -= (op == 2u ? 1 : 0) + (rr == 0 ? 1 : 0);
+                    rt -= 1;
+                }
+                if (rt < 0 || sg < 0 || J0 + sg - (rt >> LR) <= 0) break;
+            }
+            i = rowbase + rt + 1;
+            j = J0 + sg - (rt >> LR);
+            if (!err && q == qin) err = SED_ERR_TB_STALL;
+            if (!err && i >= 1 && j >= 1) {  // the exit cell's L must be the ops still to emit
+                if (rt < 0) {
+                    const int x = j - J0;
+                    if (x >= 0 && x < 64 && !l_ok(ltop[slot][x], i, j)) err = SED_ERR_TB_CHECK;
+                } else if (sg < 0) {
+                    const int lb = rt >> LR;
+                    if (j == J0 - lb - 1 && !l_ok(lleft[rt & (R - 1)][slot * G + lb], i, j)) err = SED_ERR_TB_CHECK;
+                }
+            }
+            if (--guard <= 0 && !err) err = SED_ERR_TB_GUARD;
+            lst[slot] = make_int4(i, j, (int)q, err);
+        }
+        __syncthreads();
+        if (act) {
+            const int4 s = lst[slot];
+            i = s.x;
+            j = s.y;
+            q = (uint32_t)s.z;
+            err = s.w;
+        }
+        __syncthreads();  // (lst and the LDS tiles are rewritten by the next visit)
+    }
+    if (walker && live) {
+        if (!err) {  // the border: inserts along row 0, deletes along column 0
+            while (j > 0 || i > 0) {
+                if (q == 0u) {
+                    err = SED_ERR_TB_LENGTH;
+                    break;
+                }
+                const uint32_t op = j > 0 ? 0u : 1u;
+                acc = (acc << 2) | op;
+                if ((--q & 15u) == 0u) out[q >> 4] = (uint32_t)acc;
+                if (op == 0u) --j;
+                else --i;
+            }
+            if (!err && q != 0u) err = SED_ERR_TB_LENGTH;
+        }
+        if (err) res[pair].err = (uint8_t)err;
+    }
+}
+
 // SPLIT batches with checkpoints (config 2, GUI pairs; sed_runtime.cpp: split_ck).  The SPLIT forward kernel runs the
 // distance (or dot) keys, 2-3 VALU per cell instead of the ladder keys' 5.2, and stores checkpoints after the pair's
 // per-cell code region; this kernel then recomputes every 64 x 64 tile from them at once (one wave per tile, the
@@ -2679,6 +2964,23 @@ hipError_t sed_launch_ck_codes(const sed_launch &L, int max_tiles, const sed_i32
 hipError_t sed_launch_traceback_ck(const sed_launch &L, uint32_t *ops, const sed_i32_params &prm) {
     const dim3 grid(L.npairs), block(64);
     const uint32_t *a = (const uint32_t *)L.seqa, *b = (const uint32_t *)L.seqb;
+    // SED_CK_REPLAY (A/B): 1 = the forward-lane replay (sed_traceback_ckr_kernel) at every R, 0 = the lane-per-row sweep
+    // (sed_traceback_ck_kernel) at every R; unset: the replay at R = 16
+    static const int replay_env = [] { const char *e = getenv("SED_CK_REPLAY"); return e ? atoi(e) : -1; }();
+    if (replay_env < 0 ? L.R == 16 : replay_env > 0) {
+        const dim3 gr((L.npairs + L.R - 1) / L.R);  // R pairs per wave
+        switch (L.R) {
+#define CASE(RR)                                                                                                  \
+    case RR:                                                                                                      \
+        SED_LAUNCH(sed_traceback_ckr_kernel<RR>, gr, block, CkrLds<RR>::words * 4, L, L.pd, L.npairs, a, b, L.tb, \
+                   L.res, ops, prm);                                                                              \
+        break;
+            CASE(4) CASE(8) CASE(16)
+#undef CASE
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     switch (L.R) {
     case 4: SED_LAUNCH(sed_traceback_ck_kernel<4>, grid, block, 0, L, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
     case 8: SED_LAUNCH(sed_traceback_ck_kernel<8>, grid, block, 0, L, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;

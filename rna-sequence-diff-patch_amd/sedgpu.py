@@ -141,6 +141,7 @@ class Context:
         lib = load()
         self._lib = lib
         self._pid = os.getpid()
+        self.device = device
         self.ptr = lib.sed_create(device)
         _hip_pid = self._pid
         if not self.ptr:
@@ -269,6 +270,27 @@ class PackedPairs:
         self.ops_off = np.zeros(max(self.npairs, 1) + 1, np.int64)
         if self.npairs:
             self.ops_off[1:self.npairs + 1] = np.cumsum(words[:self.npairs])
+
+    @classmethod
+    def from_concat(cls, codes_a, len_a, codes_b, len_b):
+        """Pairs from concatenated codes and per-pair lengths (CostPlan.encode_many)."""
+        self = cls.__new__(cls)
+        P = len(len_a)
+        self.npairs = P
+        self.len_a = np.asarray(len_a, np.int32) if P else np.zeros(1, np.int32)
+        self.len_b = np.asarray(len_b, np.int32) if P else np.zeros(1, np.int32)
+        self.off_a = np.zeros(max(P, 1), np.int64)
+        self.off_b = np.zeros(max(P, 1), np.int64)
+        if P:
+            self.off_a[1:] = np.cumsum(self.len_a[:-1])
+            self.off_b[1:] = np.cumsum(self.len_b[:-1])
+        self.codes_a = np.concatenate([np.asarray(codes_a, np.uint8), np.zeros(1, np.uint8)])
+        self.codes_b = np.concatenate([np.asarray(codes_b, np.uint8), np.zeros(1, np.uint8)])
+        words = (self.len_a.astype(np.int64) + self.len_b + 15) // 16
+        self.ops_off = np.zeros(max(P, 1) + 1, np.int64)
+        if P:
+            self.ops_off[1:P + 1] = np.cumsum(words[:P])
+        return self
 
     @classmethod
     def from_arrays(cls, A, B):
@@ -569,9 +591,16 @@ class _PlanArgs:
         return (self.K, self.sub.tobytes(), self.sub_int.tobytes(), self.ins, self.ins_int, self.dele, self.del_int)
 
 
-def _serve(rx, tx, device):
-    """Serve EngineClient requests on one Context until the client closes its end."""
+_serve_pool = []  # idle serving Contexts of this process (parent-served children): the next child reuses one
+_serve_pool_lock = threading.Lock()
+
+
+def _serve(rx, tx, device, pooled=False):
+    """Serve EngineClient requests on one Context until the client closes its end.  pooled: the Context comes from
+    and returns to _serve_pool (a parent serving its forked children: create_search_threads' second Process then
+    starts without a sed_create), with the options the client set put back to their defaults."""
     ctx = None
+    touched = set()
     while True:
         try:
             req = pickle.loads(rx.recv_bytes())
@@ -582,7 +611,15 @@ def _serve(rx, tx, device):
             if op == "open":  # (a parent-served child names its device first)
                 device = args[0]
             if ctx is None:
-                ctx = Context(device)
+                if pooled:
+                    with _serve_pool_lock:
+                        for x in _serve_pool:
+                            if x.device == device:
+                                _serve_pool.remove(x)
+                                ctx = x
+                                break
+                if ctx is None:
+                    ctx = Context(device)
             if op == "open":
                 val = None
             elif op == "set_costs":
@@ -590,6 +627,7 @@ def _serve(rx, tx, device):
                 val = None
             elif op == "set_option":
                 ctx.set_option(*args)
+                touched.add(args[0])
                 val = None
             elif op == "selftest":
                 val = ctx.selftest()
@@ -608,6 +646,18 @@ def _serve(rx, tx, device):
             tx.send_bytes(pickle.dumps(out, protocol=pickle.HIGHEST_PROTOCOL))
         except OSError:
             break
+    if ctx is not None and pooled:
+        try:
+            for key in touched:
+                ctx.set_option(key, 0)
+            if touched:
+                ctx.invalidate_costs()
+            with _serve_pool_lock:
+                if len(_serve_pool) < 2:
+                    _serve_pool.append(ctx)
+                    ctx = None
+        except SedError:
+            pass
     if ctx is not None:
         ctx.close()
 
@@ -623,7 +673,7 @@ def _serve_child(sock):
     from multiprocessing.connection import Connection
     conn = Connection(sock.detach())
     try:
-        _serve(conn, conn, 0)
+        _serve(conn, conn, 0, pooled=True)
     finally:
         conn.close()
 

@@ -17,7 +17,6 @@ similarities) are not on the engine's path and raise NotImplementedError.
 from collections import OrderedDict
 
 import StringEditDistance as SED
-import sedcost
 
 _CACHE = OrderedDict()
 _CACHE_SIZE = 8
@@ -35,15 +34,14 @@ def wf_scores(query, seqs, user_cost=False):
     seqs = list(seqs)
     if not seqs:
         return []
-    table = SED.user_costs if user_cost else SED.default_costs
-    for s in seqs:  # the reference raises on the first offending document, in order
-        sedcost.check_pair(table, query, s)
-    key = (query, tuple(seqs), sedcost.build_plan(table, [query], seqs).key())
+    queries = [query] * len(seqs)
+    plan = SED.batch_plan(queries, seqs, user_cost)  # the reference raises on the first offending document, in order
+    key = (query, tuple(seqs), plan.key())
     hit = _CACHE.get(key)
     if hit is not None:
         _CACHE.move_to_end(key)
         return list(hit)
-    vals = SED.distance_batch([query] * len(seqs), seqs, user_cost)
+    vals = SED.distance_batch(queries, seqs, user_cost, plan=plan)
     scores = [1 / (1 + v) for v in vals]
     _CACHE[key] = tuple(scores)
     while len(_CACHE) > _CACHE_SIZE:

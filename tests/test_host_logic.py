@@ -177,3 +177,59 @@ def test_plan_encoding_roundtrip(tables):
     k = plan.code
     assert plan.sub[k["a"], k["A"]] == 0 and plan.sub_int[k["a"], k["A"]] == 1
     assert plan.sub[k["Y"], k["W"]] == tables[False]["update"]["Y"]["W"]
+
+
+def _first_error(fn):
+    try:
+        fn()
+    except KeyError as ex:
+        return ("KeyError", ex.args)
+    return None
+
+
+def test_check_batch_like_sequential_checks(tables):
+    """sedcost.check_batch (distance_batch, wfsearch) raises exactly what check_pair over the pairs in order raises:
+    its fast path (every combination over the union alphabets resolves) must never hide an error, and the slow
+    path finds the first offending pair.  Random batches over valid symbols, lowercase (free on a case-insensitive
+    match, an error on a mismatch), unknown symbols and empty strings; both tables and tables missing keys."""
+    rng = np.random.default_rng(77)
+    pools = ["ACGU", "ACGUYRN", "ACGUa", "ACGUT", "ACGUacgu", "AGRGA"]
+    extra = [{"insert": 1.0, "delete": 1.0, "update": {"A": {"C": 1.0}, "C": {"A": 2.0}}},
+             {"delete": 1.0, "update": {}}, {"insert": 1.0, "update": {}}]
+    for trial in range(400):
+        table = (tables[False], tables[True], *extra)[trial % 5]
+        pool = pools[trial % len(pools)] if trial % 5 < 2 else "ACac"
+        P = int(rng.integers(1, 12))
+        s1 = ["".join(rng.choice(list(pool), size=int(rng.integers(0, 6)))) for _ in range(P)]
+        s2 = ["".join(rng.choice(list(pool), size=int(rng.integers(0, 6)))) for _ in range(P)]
+        if trial % 3 == 0:  # the one-vs-many shape of wfsearch
+            s1 = [s1[0]] * P
+
+        def seq():
+            for a, b in zip(s1, s2):
+                sedcost.check_pair(table, a, b)
+        want = _first_error(seq)
+        got = _first_error(lambda: sedcost.check_batch(table, s1, s2))
+        assert got == want, (trial, s1, s2, got, want)
+
+
+def test_batch_plan_and_packing_match_per_string(tables):
+    """build_plan over the joined strings, encode_many and PackedPairs.from_concat equal the per-string versions."""
+    import sedgpu
+    rng = np.random.default_rng(5)
+    s1 = ["".join(rng.choice(list("ACGUNY"), size=int(rng.integers(0, 40)))) for _ in range(50)]
+    s2 = ["".join(rng.choice(list("ACGUR"), size=int(rng.integers(0, 40)))) for _ in range(50)]
+    plan = sedcost.build_plan(tables[False], s1, s2)
+    seen = {}
+    for s in s1 + s2:
+        for c in s:
+            seen.setdefault(c, 0)
+    assert set(plan.alphabet) == set(seen)
+    assert plan.alphabet[:len(dict.fromkeys("".join(s1)))] == list(dict.fromkeys("".join(s1)))
+    ca, la = plan.encode_many(s1)
+    cb, lb = plan.encode_many(s2)
+    p1 = sedgpu.PackedPairs.from_concat(ca, la, cb, lb)
+    p0 = sedgpu.PackedPairs([plan.encode(a) for a in s1], [plan.encode(b) for b in s2])
+    for f in ("codes_a", "codes_b", "len_a", "len_b", "off_a", "off_b", "ops_off"):
+        assert np.array_equal(getattr(p1, f), getattr(p0, f)), f
+    assert p1.npairs == p0.npairs == 50
