@@ -2483,6 +2483,9 @@ __device__ __forceinline__ void ckr_step(uint32_t (&V)[R], const uint32_t (&cv)[
 // (a VGPR budget like the forward kernel's, 5 waves per SIMD: unbounded, the scheduler hoisted every step's v_perm of a
 // group ahead of the min chain, 183 VGPRs at R = 16, and this kernel runs beside the forward kernel's waves.  The LDS is
 // dynamic: with its static size the compiler saw an occupancy of 1-2 waves per SIMD and ignored the budget)
+#ifndef SED_CKR_PRIO
+#define SED_CKR_PRIO 0  // s_setprio of the replay waves (A/B: they run beside the other part's forward waves)
+#endif
 #ifndef SED_CKR_WAVES
 #define SED_CKR_WAVES(R) ((R) == 16 ? 4 : 5)
 #endif
@@ -2505,6 +2508,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SED_CKR_WAVE
     constexpr int SELN = 64 + G;  // selectors of a slot: column J0 - (G - 1) + x, x < 63 + G
     constexpr uint64_t PAT = Ladder<R>::pat;
     constexpr int P = Ladder<R>::P;
+#if SED_CKR_PRIO
+    __builtin_amdgcn_s_setprio(SED_CKR_PRIO);
+#endif
     using LD = CkrLds<R>;
     extern __shared__ uint4 ckr_lds[];  // CkrLds<R>::words * 4 bytes (sed_launch_traceback_ck)
     uint32_t *lw = reinterpret_cast<uint32_t *>(ckr_lds);
