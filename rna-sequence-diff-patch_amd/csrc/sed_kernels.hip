@@ -2705,6 +2705,265 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SED_CKR_WAVE
     }
 }
 
+// ---------------------------------------------------------------------------
+// Checkpoint traceback in quarter bands (sed_traceback_ckq_kernel; round 5, the default at R = 16).
+// The replay above recomputes a tile in 64 steps but needs G lanes per pair, so at R = 16 a wave carries 16 pairs and a
+// config-4 shard only 512 waves: half a wave per SIMD, latency-bound (4.5 ms alone against 2.1 ms for the lane-per-row
+// sweep, profiles/r05/s4).  Here each forward band (16 rows) is recomputed by 4 lanes of 4 rows, so a pair takes 16
+// lanes (one DPP row) and a wave 4 pairs: 2048 waves for the shard.  The 16 lanes of a pair form one staircase: lane
+// L = 4 b + s (band b, quarter s) computes column J0 + sigma - L at sweep step sigma, i.e. band b's window (columns
+// J0 - b .. J0 - b + 63, the forward's chunk) at steps 3 b + s .. 3 b + s + 63, and its rows from band b's column
+// checkpoint.  Until its window a lane holds its checkpoint: the first 12 steps run masked per lane (the code word of
+// a masked step is shifted as if it had run), which needs neither sentinel selectors nor a compensated delete, and
+// its row above at its first step is, by construction, the lane before it (still holding, or in its first column).
+// The cell is i32_step's ladder-key cell on the period-4 ladder (rows of a lane start on multiples of 4): v_perm,
+// v_add, v_min3, v_and_or, v_alignbit + the delete add on 1 row in 4 = 5.25 VALU; 76 steps for the whole tile (72 on
+// average for the furthest entry of the wave's 4 pairs, tools/sim_ckq.py) against up to 127 at 6 per cell.  The codes
+// stay in VGPRs (19 words per lane, 4 steps each) and each pair's path is walked on the scalar unit from its entry
+// cell (readlane per op), as in sed_traceback_ck_kernel; the exit cell's L is checked against the top row or the
+// column checkpoint it leaves through.
+// ---------------------------------------------------------------------------
+#define SED_CKQ_STEPS 76
+#define SED_CKQ_GROUPS 19
+#define SED_CKQ_NX 92  // selectors of a pair: column J0 - 15 + x (x < 91)
+#define SED_RUNG4(x) ((0x1230u >> (4u * ((uint32_t)(x) & 3u))) & 0xFu)  // Ladder<4>::rung
+
+__device__ __forceinline__ void ckq_step(uint32_t (&V)[4], const uint32_t (&cv)[4], uint32_t &top_prev,
+                                         uint32_t &bottom, const uint32_t topin, const uint32_t selv, uint32_t &cw) {
+    using Lad = Ladder<4>;
+    constexpr int d0 = Lad::rung(1) - Lad::rung(0);
+    const uint32_t dg0 = top_prev + __builtin_amdgcn_perm(cv[0], (uint32_t)(d0 - 6), selv);
+    const uint32_t topv = seg_shr1<16>(topin, bottom);  // (row_shr:1: lane 0 of the pair's DPP row keeps topin)
+    uint32_t up = topv, diag = top_prev;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t left = V[r];
+        const int c = Lad::rung(r + 1), d = c - Lad::rung(r);  // compile-time after unrolling
+        const uint32_t mm = umin3(left, d == -1 ? up : up + (uint32_t)(d + 1),
+                                  r == 0 ? dg0 : diag + __builtin_amdgcn_perm(cv[r], (uint32_t)(d - 6), selv));
+        cw = __builtin_amdgcn_alignbit(mm, cw, 2);  // step u, row r at bits 8 u + 2 r of the group's word
+        up = (mm & ~7u) | (uint32_t)c;
+        diag = left;
+        V[r] = up;
+    }
+    top_prev = topv;
+    bottom = V[3];
+}
+
+__global__ __launch_bounds__(64) void sed_traceback_ckq_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
+                                                               const uint32_t *__restrict__ seqa,
+                                                               const uint32_t *__restrict__ seqb,
+                                                               const uint32_t *__restrict__ ck,
+                                                               sed_result *__restrict__ res,
+                                                               uint32_t *__restrict__ ops, sed_i32_params prm) {
+    constexpr int R = 16, ROWS = 64 * R, G = 4, NP = 4;
+    __shared__ uint32_t ltop[NP][SED_CKQ_STEPS], lsel[NP][SED_CKQ_NX], lraw[NP][8];
+    const int lane = threadIdx.x, slot = lane >> 4, L = lane & 15, b = L >> 2, s = L & 3;
+    const int sigL = L - b;  // the lane's first step in its band's window (3 b + s)
+    const int pair = (int)blockIdx.x * NP + slot;
+    bool live = pair < npairs;
+    sed_pair_desc d{};
+    if (live) d = pd[pair];
+    live = live && !d.lane;
+    const int n = live ? d.n : 0, m = live ? d.m : 0;
+    int i = n, j = m, err = 0;
+    uint32_t q = live ? (uint32_t)res[pair].len : 0u, acc = 0u;  // acc: the last 16 ops, the latest in bits 1:0
+    int guard = 2 * (n + m) + 8;
+    const int nstripes = (n + ROWS - 1) / ROWS;
+    const int SG = (m + 63 + G - 1) / G * G, nchunks = (SG + 63) >> 6, ngroups = SG / G;
+    const uint32_t *ccp = ck + d.tb_off;
+    const uint32_t *rcp = ccp + sed_ck_col_words(R, nstripes, nchunks);
+    const uint32_t *pa = seqa + d.a_off, *pb = seqb + d.b_off;
+    uint32_t *out = ops + d.ops_off;
+    while (true) {
+        const bool act = live && err == 0 && i > 0 && j > 0;  // (uniform per pair)
+        if (!__any(act)) break;
+        // ---- the tile of the pair's cell (i, j) ----
+        int k = 0, Q = 0, c = 0, rowbase = 0, J0 = 0, sge = -1;
+        if (act) {
+            k = (i - 1) / ROWS;
+            const int t = ((i - 1) % ROWS) >> 4;
+            Q = t >> 2;
+            c = (j - 1 + t) >> 6;
+            rowbase = k * ROWS + 64 * Q;
+            J0 = 64 * c - G * Q + 1;
+            sge = j - J0 + ((i - rowbase - 1) >> 2);  // the entry cell's step: column J0 + sigma - L
+        }
+        int smax = 0;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) smax = max(smax, __builtin_amdgcn_readlane(sge, 16 * p) + 1);
+        const int ng = (smax + 3) >> 2;
+        // ---- boundary: cost rows, column checkpoint, top row and selectors (LDS) ----
+        const int tl = G * Q + b;
+        const int row0 = min(rowbase + 4 * L, max(n - 1, 0));  // 0-based str1 index of the lane's first row (clamped)
+        const uint32_t wa = act ? pa[row0 >> 4] >> (2 * (row0 & 15)) : 0u;
+        uint32_t cv[4], V[4], VI[4], top_prev, bottom;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t a = (wa >> (2 * r)) & 3u;
+            cv[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
+        }
+        if (act && c >= 1) {
+            // rows 4 s .. 4 s + 3 of band b at its checkpoint column J0 - b - 1, and the row above the lane's first row
+            // there: band row 4 s - 1, or the band's top_prev (word R) for s = 0
+            const uint32_t *cp = ccp + sed_ck_col_word(R, k, nchunks, c - 1, 4 * s, tl);
+            uint32_t w[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) w[r] = cp[r * 64];
+            const uint32_t wt = s ? cp[-64] : cp[R * 64];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) V[r] = ck_to_lad(w[r], prm, (uint32_t)Ladder<4>::rung(r + 1));
+            top_prev = ck_to_lad(wt, prm, 0u);
+        } else {
+            i32_reset<4, true>(V, top_prev);  // column-0 state (chunk 0: the forward's virtual columns)
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) VI[r] = V[r];
+        bottom = V[3];
+        // the row above the tile at column J0 + x (x = L + 16 u < 76), as in sed_traceback_ckr_kernel
+        const bool above = Q >= 1 || k >= 1;
+        const int kr = Q >= 1 ? k : k - 1, tr = Q >= 1 ? G * Q - 1 : 63;
+        const int s0 = (Q >= 1 ? 64 * c - 1 : 64 * c + 63) + L;
+        const uint32_t *rb = rcp + sed_ck_row_word(R, max(kr, 0), ngroups, 0, tr) +
+                             (int64_t)(s0 >> 2) * SED_CK_RW + (s0 & 3);
+        const int wb0 = max(J0 - 16, 0) >> 4;  // str2 words of the selectors' columns (at most 7)
+        if (L < 8) lraw[slot][L] = act ? pb[min(wb0 + L, (max(m, 1) - 1) >> 4)] : 0u;
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            const int x = L + 16 * u;
+            if (x < SED_CKQ_STEPS) {
+                uint32_t v = SED_KB3;
+                if (act && above && J0 + x >= 1 && s0 + 16 * u < SG) v = ck_to_lad(rb[u * 4 * SED_CK_RW], prm, 0u);
+                ltop[slot][x] = v;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+            const int x = L + 16 * u;
+            if (x < SED_CKQ_NX) {
+                const int col = J0 - 15 + x;
+                const int ci = min(max(col - 1, 0), max(m - 1, 0));
+                const uint32_t wb = lraw[slot][min(max((ci >> 4) - wb0, 0), 7)];
+                lsel[slot][x] = col < 1 ? SED_SEL_SENT3 : i32_sel((wb >> ((ci & 15) * 2)) & 3u);
+            }
+        }
+        __syncthreads();
+        // ---- sweep ----
+        uint32_t CW[SED_CKQ_GROUPS];
+        {
+            const uint32_t *tp = ltop[slot];
+            const uint32_t *sp = lsel[slot] + (15 - L);  // the lane's column at step x: J0 + x - L
+#pragma unroll
+            for (int g = 0; g < 3; ++g) {  // steps 0 .. 11: lanes before their window hold (masked)
+                uint32_t cw = 0u;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int sig = 4 * g + u;
+                    if (sig >= sigL) ckq_step(V, cv, top_prev, bottom, tp[sig], sp[sig], cw);
+                    else cw >>= 8;
+                }
+                CW[g] = cw;
+            }
+#pragma unroll
+            for (int g = 3; g < SED_CKQ_GROUPS; ++g) {
+                if (g >= ng) break;  // (uniform)
+                uint32_t cw = 0u;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) ckq_step(V, cv, top_prev, bottom, tp[4 * g + u], sp[4 * g + u], cw);
+                CW[g] = cw;
+            }
+        }
+        // ---- walk: each pair's path on the scalar unit, word by word (the step only decreases) ----
+#pragma unroll 1
+        for (int p = 0; p < NP; ++p) {
+            const int pl = 16 * p;
+            if (!__builtin_amdgcn_readlane(act ? 1 : 0, pl)) continue;
+            const int si0 = __builtin_amdgcn_readlane(i, pl), sj0 = __builtin_amdgcn_readlane(j, pl);
+            const int sJ0 = __builtin_amdgcn_readlane(J0, pl), srb = __builtin_amdgcn_readlane(rowbase, pl);
+            const uint32_t qin = (uint32_t)__builtin_amdgcn_readlane((int)q, pl);
+            uint32_t sq = qin, sacc = (uint32_t)__builtin_amdgcn_readlane((int)acc, pl);
+            uint32_t *sout = (uint32_t *)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uintptr_t)out, pl)) |
+                                          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uintptr_t)out >> 32), pl) << 32));
+            int rt = si0 - srb - 1, sg = sj0 - sJ0 + (rt >> 2), serr = 0;
+            bool inside = true;
+#pragma unroll
+            for (int w = SED_CKQ_GROUPS - 1; w >= 0; --w) {
+                while (inside && (sg >> 2) == w) {
+                    const uint32_t wv = (uint32_t)__builtin_amdgcn_readlane((int)CW[w], pl + (rt >> 2));
+                    const uint32_t code = (wv >> (8 * (sg & 3) + 2 * (rt & 3))) & 3u;
+                    const uint32_t op = (code - SED_RUNG4(rt + 1)) & 3u;
+                    if (sq == 0u || op == 3u) {  // (a code off the ladder: a corrupt tile)
+                        serr = sq == 0u ? SED_ERR_TB_LENGTH : SED_ERR_TB_CHECK;
+                        inside = false;
+                        break;
+                    }
+                    sacc = (sacc << 2) | op;
+                    if ((--sq & 15u) == 0u) sout[sq >> 4] = sacc;
+                    if (op == 0u) {
+                        sg -= 1;
+                    } else {
+                        sg -= (op == 2u ? 1 : 0) + ((rt & 3) == 0 ? 1 : 0);
+                        rt -= 1;
+                    }
+                    const int lw = rt >> 2;  // (arithmetic: -1 above the tile)
+                    if (rt < 0 || sg < lw - (lw >> 2) || sJ0 + sg - lw <= 0) inside = false;
+                }
+            }
+            const int si = srb + rt + 1, sj = sJ0 + sg - (rt >> 2);
+            if (!serr && sq == qin) serr = SED_ERR_TB_STALL;
+            if (!serr && si >= 1 && sj >= 1) {  // the exit cell's L must be the ops still to emit
+                uint32_t key = 0u;
+                bool chk = false;
+                if (rt < 0) {
+                    const int x = sj - sJ0;
+                    if (x >= 0 && x < SED_CKQ_STEPS) {
+                        key = ltop[p][x];
+                        chk = true;
+                    }
+                } else {
+                    const int lw = rt >> 2;
+                    if (sj == sJ0 - (lw >> 2) - 1) {
+                        const int rr = rt & 3;
+                        const uint32_t vr = rr == 0 ? VI[0] : rr == 1 ? VI[1] : rr == 2 ? VI[2] : VI[3];
+                        key = (uint32_t)__builtin_amdgcn_readlane((int)vr, pl + lw);
+                        chk = true;
+                    }
+                }
+                if (chk && (uint32_t)i32_decode<4, true>(key, si, sj, prm).y != sq) serr = SED_ERR_TB_CHECK;
+            }
+            const int sguard = __builtin_amdgcn_readlane(guard, pl) - 1;
+            if (!serr && sguard <= 0) serr = SED_ERR_TB_GUARD;
+            if (slot == p) {
+                i = si;
+                j = sj;
+                q = sq;
+                acc = sacc;
+                err = serr;
+                guard = sguard;
+            }
+        }
+        __syncthreads();  // (the LDS tiles are rewritten by the next visit)
+    }
+    if (L == 0 && live) {
+        if (!err) {  // the border: inserts along row 0, deletes along column 0
+            while (j > 0 || i > 0) {
+                if (q == 0u) {
+                    err = SED_ERR_TB_LENGTH;
+                    break;
+                }
+                const uint32_t op = j > 0 ? 0u : 1u;
+                acc = (acc << 2) | op;
+                if ((--q & 15u) == 0u) out[q >> 4] = acc;
+                if (op == 0u) --j;
+                else --i;
+            }
+            if (!err && q != 0u) err = SED_ERR_TB_LENGTH;
+        }
+        if (err) res[pair].err = (uint8_t)err;
+    }
+}
+
 // SPLIT batches with checkpoints (config 2, GUI pairs; sed_runtime.cpp: split_ck).  The SPLIT forward kernel runs the
 // distance (or dot) keys, 2-3 VALU per cell instead of the ladder keys' 5.2, and stores checkpoints after the pair's
 // per-cell code region; this kernel then recomputes every 64 x 64 tile from them at once (one wave per tile, the
@@ -2970,10 +3229,15 @@ hipError_t sed_launch_ck_codes(const sed_launch &L, int max_tiles, const sed_i32
 hipError_t sed_launch_traceback_ck(const sed_launch &L, uint32_t *ops, const sed_i32_params &prm) {
     const dim3 grid(L.npairs), block(64);
     const uint32_t *a = (const uint32_t *)L.seqa, *b = (const uint32_t *)L.seqb;
-    // SED_CK_REPLAY (A/B): 1 = the forward-lane replay (sed_traceback_ckr_kernel) at every R, 0 = the lane-per-row sweep
-    // (sed_traceback_ck_kernel) at every R; unset: the replay at R = 16
-    static const int replay_env = [] { const char *e = getenv("SED_CK_REPLAY"); return e ? atoi(e) : -1; }();
-    if (replay_env < 0 ? L.R == 16 : replay_env > 0) {
+    // SED_CK_REPLAY (A/B): 0 = the lane-per-row sweep (sed_traceback_ck_kernel) at every R, 1 = the forward-lane replay
+    // (sed_traceback_ckr_kernel) at every R, 2 = the quarter-band kernel (sed_traceback_ckq_kernel) at R = 16; unset: 2
+    static const int replay_env = [] { const char *e = getenv("SED_CK_REPLAY"); return e ? atoi(e) : 2; }();
+    if (replay_env == 2 && L.R == 16) {
+        SED_LAUNCH(sed_traceback_ckq_kernel, dim3((L.npairs + 3) / 4), block, 0, L, L.pd, L.npairs, a, b, L.tb, L.res,
+                   ops, prm);
+        return hipGetLastError();
+    }
+    if (replay_env == 1) {
         const dim3 gr((L.npairs + L.R - 1) / L.R);  // R pairs per wave
         switch (L.R) {
 #define CASE(RR)                                                                                                  \
