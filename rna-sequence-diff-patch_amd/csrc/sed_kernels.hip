@@ -2867,14 +2867,25 @@ __global__ __launch_bounds__(64) void sed_traceback_ckq_kernel(const sed_pair_de
             }
 #pragma unroll
             for (int g = 3; g < SED_CKQ_GROUPS; ++g) {
-                if (g >= ng) break;  // (uniform)
-                uint32_t cw = 0u;
+                if (g < ng) {  // (uniform; no break: the loop unrolls, so every code word sits in its own VGPR)
+                    uint32_t cw = 0u;
 #pragma unroll
-                for (int u = 0; u < 4; ++u) ckq_step(V, cv, top_prev, bottom, tp[4 * g + u], sp[4 * g + u], cw);
-                CW[g] = cw;
+                    for (int u = 0; u < 4; ++u) ckq_step(V, cv, top_prev, bottom, tp[4 * g + u], sp[4 * g + u], cw);
+                    CW[g] = cw;
+                }
             }
         }
-        // ---- walk: each pair's path on the scalar unit, word by word (the step only decreases) ----
+        // the codes as ops: field (step u, row r) of a word holds (rung(r + 1) + op) & 3 and rung(r + 1) = 3, 2, 1, 0 for
+        // r = 0 .. 3, so op = field + r + 1 (mod 4): one SWAR mod-4 add of 0x39393939 per word, off the scalar walk
+#pragma unroll
+        for (int g = 0; g < SED_CKQ_GROUPS; ++g)
+            CW[g] = ((CW[g] & 0x55555555u) + 0x11111111u) ^ ((CW[g] ^ 0x39393939u) & 0xAAAAAAAAu);
+        // ---- walk: each pair's path on the scalar unit, word by word ----
+        // State B = 8 sigma + 2 r (bit index of the cell's op in its lane's code stream: word B >> 5, bit B & 31) and the
+        // lane LP.  Every op moves B uniformly (insert 8, delete 2, update 10), also into the lane above: from row 0 at
+        // step sigma a delete reaches row 3 of lane L - 1 at sigma - 1, i.e. B - 2.  The lane changes on a delete or
+        // update from row 0, and the walk leaves the tile above lane 0 or below the lane's bound lim (its window starts
+        // at step 3 b + s; chunk 0: column 0).
 #pragma unroll 1
         for (int p = 0; p < NP; ++p) {
             const int pl = 16 * p;
@@ -2885,31 +2896,80 @@ __global__ __launch_bounds__(64) void sed_traceback_ckq_kernel(const sed_pair_de
             uint32_t sq = qin, sacc = (uint32_t)__builtin_amdgcn_readlane((int)acc, pl);
             uint32_t *sout = (uint32_t *)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uintptr_t)out, pl)) |
                                           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uintptr_t)out >> 32), pl) << 32));
-            int rt = si0 - srb - 1, sg = sj0 - sJ0 + (rt >> 2), serr = 0;
-            bool inside = true;
+            const int rt0 = si0 - srb - 1;
+            int LP = pl + (rt0 >> 2);
+            int B = 8 * (sj0 - sJ0 + (rt0 >> 2)) + 2 * (rt0 & 3);
+            auto lim_of = [&](const int Lw) { return 8 * max(Lw - (Lw >> 2), Lw - sJ0 + 1); };
+            int lim = lim_of(LP - pl);
+            bool above = false, stop = false;
 #pragma unroll
             for (int w = SED_CKQ_GROUPS - 1; w >= 0; --w) {
-                while (inside && (sg >> 2) == w) {
-                    const uint32_t wv = (uint32_t)__builtin_amdgcn_readlane((int)CW[w], pl + (rt >> 2));
-                    const uint32_t code = (wv >> (8 * (sg & 3) + 2 * (rt & 3))) & 3u;
-                    const uint32_t op = (code - SED_RUNG4(rt + 1)) & 3u;
-                    if (sq == 0u || op == 3u) {  // (a code off the ladder: a corrupt tile)
-                        serr = sq == 0u ? SED_ERR_TB_LENGTH : SED_ERR_TB_CHECK;
-                        inside = false;
-                        break;
-                    }
-                    sacc = (sacc << 2) | op;
-                    if ((--sq & 15u) == 0u) sout[sq >> 4] = sacc;
-                    if (op == 0u) {
-                        sg -= 1;
-                    } else {
-                        sg -= (op == 2u ? 1 : 0) + ((rt & 3) == 0 ? 1 : 0);
-                        rt -= 1;
-                    }
-                    const int lw = rt >> 2;  // (arithmetic: -1 above the tile)
-                    if (rt < 0 || sg < lw - (lw >> 2) || sJ0 + sg - lw <= 0) inside = false;
-                }
+                if (stop) continue;  // (no break: the loop unrolls, CW[w] is a fixed VGPR)
+                int lo = max(32 * w, lim);
+                // One op per iteration, written as scalar asm: the compiler turned the combined conditions into lane
+                // masks (~30 SALU per op).  Here: ~15 SALU + the v_readlane on the common path; the script word
+                // completed at q (a multiple of 16, below the visit's first q) is stored from the SGPRs; a delete or
+                // update from row 0 moves to the lane above (above the tile: ab = 1) and recomputes the bound.
+                uint32_t op, t, t2, ab = 0;
+                uint32_t vo, vd;
+                asm volatile(
+                    "Lwl%=:\n\t"
+                    "s_cmp_lt_i32 %[B], %[lo]\n\t"
+                    "s_cbranch_scc1 Lwx%=\n\t"
+                    "v_readlane_b32 %[t], %[cw], %[LP]\n\t"
+                    "s_lshr_b32 %[t], %[t], %[B]\n\t"
+                    "s_and_b32 %[op], %[t], 3\n\t"
+                    "s_lshl2_add_u32 %[acc], %[acc], %[op]\n\t"
+                    "s_add_u32 %[q], %[q], -1\n\t"
+                    "s_and_b32 %[t], %[q], 15\n\t"
+                    "s_cbranch_scc1 Lwn%=\n\t"
+                    "s_cmp_lt_u32 %[q], %[qin]\n\t"
+                    "s_cbranch_scc0 Lwn%=\n\t"
+                    "s_lshr_b32 %[t], %[q], 2\n\t"
+                    "s_and_b32 %[t], %[t], -4\n\t"
+                    "s_waitcnt expcnt(0)\n\t"
+                    "v_mov_b32 %[vo], %[t]\n\t"
+                    "v_mov_b32 %[vd], %[acc]\n\t"
+                    "global_store_dword %[vo], %[vd], %[out]\n"
+                    "Lwn%=:\n\t"
+                    "s_and_b32 %[t2], %[B], 6\n\t"
+                    "s_lshl_b32 %[t], %[op], 3\n\t"
+                    "s_lshr_b32 %[t], 0x800a0208, %[t]\n\t"
+                    "s_and_b32 %[t], %[t], 0xff\n\t"
+                    "s_sub_u32 %[B], %[B], %[t]\n\t"
+                    "s_cmp_lg_u32 %[t2], 0\n\t"
+                    "s_cbranch_scc1 Lwl%=\n\t"
+                    "s_cmp_eq_u32 %[op], 0\n\t"
+                    "s_cbranch_scc1 Lwl%=\n\t"
+                    "s_sub_u32 %[LP], %[LP], 1\n\t"
+                    "s_cmp_lt_i32 %[LP], %[pl]\n\t"
+                    "s_cbranch_scc1 Lwa%=\n\t"
+                    "s_sub_u32 %[t], %[LP], %[pl]\n\t"
+                    "s_lshr_b32 %[t2], %[t], 2\n\t"
+                    "s_sub_u32 %[t2], %[t], %[t2]\n\t"
+                    "s_sub_u32 %[t], %[t], %[J0m1]\n\t"
+                    "s_max_i32 %[t], %[t], %[t2]\n\t"
+                    "s_lshl_b32 %[lim], %[t], 3\n\t"
+                    "s_max_i32 %[lo], %[lim], %[w32]\n\t"
+                    "s_branch Lwl%=\n"
+                    "Lwa%=:\n\t"
+                    "s_mov_b32 %[ab], 1\n"
+                    "Lwx%=:"
+                    : [B] "+s"(B), [LP] "+s"(LP), [q] "+s"(sq), [acc] "+s"(sacc), [lo] "+s"(lo), [lim] "+s"(lim),
+                      [op] "=&s"(op), [t] "=&s"(t), [t2] "=&s"(t2), [ab] "+s"(ab), [vo] "=&v"(vo), [vd] "=&v"(vd)
+                    : [cw] "v"(CW[w]), [qin] "s"(qin), [pl] "s"(pl), [J0m1] "s"(sJ0 - 1), [w32] "s"(32 * w),
+                      [out] "s"(sout)
+                    : "scc", "memory");
+                (void)op;
+                (void)t;
+                (void)t2;
+                (void)vo;
+                (void)vd;
+                if (ab) above = true;
+                if (above || B < lim) stop = true;
             }
+            const int rt = above ? -1 : 4 * (LP - pl) + ((B >> 1) & 3), sg = B >> 3;
+            int serr = sq > qin ? SED_ERR_TB_LENGTH : 0;
             const int si = srb + rt + 1, sj = sJ0 + sg - (rt >> 2);
             if (!serr && sq == qin) serr = SED_ERR_TB_STALL;
             if (!serr && si >= 1 && sj >= 1) {  // the exit cell's L must be the ops still to emit
