@@ -2415,23 +2415,24 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
 }
 
 // ---------------------------------------------------------------------------
-// Checkpoint traceback replaying the forward lanes (sed_traceback_ckr_kernel, round 5; the default at R = 16).
-// A 64-row tile is G = 64/R forward lanes of R rows, and the forward kernel computed it in the 64 steps of one chunk,
-// each lane starting from its own column checkpoint (chunk c-1's end), lane 0 of the tile taking the row above from
-// the row checkpoints.  Replaying exactly that -- G lanes of R rows on the forward's systolic schedule, in ladder keys
-// with per-cell codes (i32_step's cell: v_perm, v_add, v_min3, v_and_or, v_alignbit, + the delete add on 3 of 16
-// rows) -- recomputes the whole tile in 64 steps, where the lane-per-row sweep of sed_traceback_ck_kernel needs up to
-// 127 (its staircase ramps over 64 lanes) at 6 VALU per cell.  A pair's G lanes are a G-th of a wave, so a wave
-// carries NP = 64/G = R pairs, each at its own tile, in lockstep (pair slot s = lanes s G .. s G + G - 1):
-//   1. every lane loads its tile's boundary (its R + 1 column-checkpoint words, a share of the slot's 64 top values
-//      and 63 + G str2 selectors, converted to ladder keys and staged in LDS);
-//   2. the sweep runs as many steps as the furthest entry cell of the wave needs, storing each lane's codes per
-//      G-step group in LDS ([lane][group] uint4: code of step u, row r at bits 2 ((u R + r) & 15) of word (u R + r) / 16);
-//   3. every slot's walker lane (band 0) walks its path through the codes from the entry cell until it leaves the
-//      tile (above it, left of its band's checkpoint column, or at column 0), emitting ops from the sink as before;
-//   4. the exit cell's L (decoded from the top row or the column checkpoint it leaves through) must equal the ops
-//      still to emit (SED_ERR_TB_CHECK: a corrupt checkpoint), and the slot's state goes to its other lanes.
-// The walk is vector code (one op per iteration for every walker at once; ~26 VALU and one LDS read per op).
+// Checkpoint traceback in band slices (sed_traceback_ckb_kernel<RT>; round 5).
+// A 64-row tile is G = 4 forward lanes ("bands") of 16 rows, and the forward kernel computed band b in the 64 steps of
+// one chunk from its own column checkpoint (column J0 - b - 1).  Here each band is recomputed by 16/RT lanes of RT rows,
+// so a pair takes LPP = 64/RT lanes and a wave NP = RT pairs, each at its own tile, in lockstep.  The LPP lanes of a pair
+// form one staircase: lane L (band b = L / (16/RT)) computes column J0 + sigma - L at sweep step sigma, i.e. band b's
+// window (columns J0 - b .. J0 - b + 63) at steps L - b .. L - b + 63, its rows starting from band b's checkpoint.
+// Until its window a lane holds its checkpoint: the first steps run masked per lane (a masked step's code bits are
+// shifted in as if it had run), so no sentinel selector or compensated delete is needed, and at its first step the row
+// above is, by construction, the lane before it (holding, or in its first column).  The cell is i32_step's ladder-key
+// cell on the period-RT ladder (a lane's rows start on multiples of RT): v_perm, v_add, v_min3, v_and_or, v_alignbit and
+// the delete add on one row in RT.  The lane-per-row sweep (sed_traceback_ck_kernel) instead runs a 64-lane staircase:
+// up to 127 steps per tile at 6 VALU per cell.
+// The codes stay in VGPRs (a word per 16/RT steps), are turned into ops by one SWAR add per word, and each pair's path
+// is walked on the scalar unit in asm: with B = 2 RT sigma + 2 r (the op's bit in its lane's code stream) every op moves
+// B by the same amount whether or not it leaves the lane (insert 2 RT, delete 2, update 2 RT + 2: from row 0 at step
+// sigma a delete reaches row RT - 1 of the lane above at sigma - 1); the lane changes on a delete or update from row 0.
+// The exit cell's L is checked against the top row or the column checkpoint the walk leaves through.
+// RT = 2 (2 pairs per wave, 4096 waves for the config-4 shard) and RT = 4 (4 pairs, 2048 waves): DESIGN.md 3.6b.
 // ---------------------------------------------------------------------------
 // forward key (distance or dot) -> the ladder key of the same (D, L) with op 0 on rung c:
 // W = ((D - i del - j ins) << 16) - 8U + SED_KB3 + c, U = i + j - L (the updates on the path)
@@ -2446,320 +2447,74 @@ __device__ __forceinline__ uint32_t ck_to_lad(uint32_t w, const sed_i32_params &
     return w - 7u * U + (SED_KB3 - SED_KB) + c;
 }
 
-// One forward step of a replayed lane (i32_step's ladder-key cell with codes): the cell above the lane's band comes
-// from the lane before it, except on a slot's band 0 (the leader), which takes topin (the tile's row above); at R = 4
-// a slot is one DPP row and row_shr:1 leaves the leader its `old` operand.
-template <int R>
-__device__ __forceinline__ void ckr_step(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
+template <int RT> struct CkbCfg {
+    static_assert(RT == 2 || RT == 4, "RT in {2, 4}");
+    static constexpr int LPP = 64 / RT;              // lanes per pair
+    static constexpr int NP = 64 / LPP;              // pairs per wave
+    static constexpr int LPB = 16 / RT;              // lanes per band
+    static constexpr int LLPB = RT == 4 ? 2 : 3;     // log2(LPB)
+    static constexpr int SMAX = LPP - 1 - 3;         // last lane's first window step (L - b)
+    static constexpr int STEPS = 64 + SMAX;          // 76 (RT = 4), 92 (RT = 2)
+    static constexpr int SPW = 16 / RT;              // steps per code word
+    static constexpr int LSPW = RT == 4 ? 2 : 3;
+    static constexpr int WORDS = (STEPS + SPW - 1) / SPW;  // 19, 12
+    static constexpr int PRO = (SMAX + SPW - 1) / SPW;  // words run with per-lane masks (steps 0 .. SMAX - 1)
+    static constexpr int NX = STEPS + LPP;           // selectors of a pair: column J0 - (LPP - 1) + x
+    static constexpr int NRAW = (NX + 15) / 16 + 2;  // str2 words behind them
+    // the code field (row r) holds (rung(r + 1) + op) & 3: op = field + ADD_r (mod 4), per word
+    static constexpr uint32_t ADD = RT == 4 ? 0x39393939u : 0xCCCCCCCCu;
+    static constexpr uint32_t MOVES = RT == 4 ? 0x800A0208u : 0x80060204u;  // B decrement per op (op 3: out)
+};
+// Ladder<2>: rungs 1, 0 (i even, odd): the delete is free on odd rows, +2 on even rows
+template <> struct Ladder<2> {
+    static constexpr int P = 2;
+    static constexpr uint64_t pat = 0x01ull;
+    static constexpr int rung(int i) { return (int)((pat >> (4 * (i & 1))) & 0xF); }
+};
+
+template <int RT>
+__device__ __forceinline__ void ckb_step(uint32_t (&V)[RT], const uint32_t (&cv)[RT], uint32_t &top_prev,
                                          uint32_t &bottom, const uint32_t topin, const uint32_t selv,
-                                         const bool leader, uint32_t (&W)[4], const int u) {
-    using Lad = Ladder<R>;
+                                         const bool leader, uint32_t &cw) {
+    using Lad = Ladder<RT>;
     constexpr int d0 = Lad::rung(1) - Lad::rung(0);
     const uint32_t dg0 = top_prev + __builtin_amdgcn_perm(cv[0], (uint32_t)(d0 - 6), selv);
     uint32_t topv;
-    if constexpr (R == 4) {
-        topv = seg_shr1<16>(topin, bottom);
+    if constexpr (RT == 4) {
+        topv = seg_shr1<16>(topin, bottom);  // (a pair is one DPP row: row_shr:1 leaves its lane 0 topin)
     } else {
-        topv = dpp_shr1(topin, bottom);
+        topv = dpp_shr1(topin, bottom);      // (a pair spans two DPP rows: its lane 0 takes topin by a select)
         topv = leader ? topin : topv;
     }
     uint32_t up = topv, diag = top_prev;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
+    for (int r = 0; r < RT; ++r) {
         const uint32_t left = V[r];
         const int c = Lad::rung(r + 1), d = c - Lad::rung(r);  // compile-time after unrolling
         const uint32_t mm = umin3(left, d == -1 ? up : up + (uint32_t)(d + 1),
                                   r == 0 ? dg0 : diag + __builtin_amdgcn_perm(cv[r], (uint32_t)(d - 6), selv));
-        const int k = u * R + r;
-        W[k >> 4] = __builtin_amdgcn_alignbit(mm, W[k >> 4], 2);
+        cw = __builtin_amdgcn_alignbit(mm, cw, 2);  // step u, row r at bits 2 (RT u + r) of the word
         up = (mm & ~7u) | (uint32_t)c;
         diag = left;
         V[r] = up;
     }
     top_prev = topv;
-    bottom = V[R - 1];
+    bottom = V[RT - 1];
 }
 
-// (a VGPR budget like the forward kernel's, 5 waves per SIMD: unbounded, the scheduler hoisted every step's v_perm of a
-// group ahead of the min chain, 183 VGPRs at R = 16, and this kernel runs beside the forward kernel's waves.  The LDS is
-// dynamic: with its static size the compiler saw an occupancy of 1-2 waves per SIMD and ignored the budget)
-#ifndef SED_CKR_PRIO
-#define SED_CKR_PRIO 0  // s_setprio of the replay waves (A/B: they run beside the other part's forward waves)
-#endif
-#ifndef SED_CKR_WAVES
-#define SED_CKR_WAVES(R) ((R) == 16 ? 4 : 5)
-#endif
-template <int R> struct CkrLds {
-    static constexpr int G = 64 / R, NP = 64 / G, NG = 64 / G, SELN = 64 + G;
-    // words: codes [64 lanes][NG groups][4], top [NP][64], sel [NP][SELN], left [R][64], raw [NP][8], state [NP][4]
-    static constexpr int codes = 0, top = codes + 64 * NG * 4, sel = top + NP * 64, left = sel + NP * SELN,
-                         raw = left + R * 64, st = raw + NP * 8, words = st + NP * 4;
-};
-template <int R>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SED_CKR_WAVES(R)))) void sed_traceback_ckr_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
+template <int RT>
+__global__ __launch_bounds__(64) void sed_traceback_ckb_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
                                                                const uint32_t *__restrict__ seqa,
                                                                const uint32_t *__restrict__ seqb,
                                                                const uint32_t *__restrict__ ck,
                                                                sed_result *__restrict__ res,
                                                                uint32_t *__restrict__ ops, sed_i32_params prm) {
-    static_assert(R == 4 || R == 8 || R == 16, "R in {4, 8, 16}");
-    constexpr int ROWS = 64 * R, G = Grp<R>::G, NP = 64 / G, NG = 64 / G;  // NP pairs per wave, NG groups per sweep
-    constexpr int LR = R == 4 ? 2 : R == 8 ? 3 : 4, LG = 6 - LR;
-    constexpr int SELN = 64 + G;  // selectors of a slot: column J0 - (G - 1) + x, x < 63 + G
-    constexpr uint64_t PAT = Ladder<R>::pat;
-    constexpr int P = Ladder<R>::P;
-#if SED_CKR_PRIO
-    __builtin_amdgcn_s_setprio(SED_CKR_PRIO);
-#endif
-    using LD = CkrLds<R>;
-    extern __shared__ uint4 ckr_lds[];  // CkrLds<R>::words * 4 bytes (sed_launch_traceback_ck)
-    uint32_t *lw = reinterpret_cast<uint32_t *>(ckr_lds);
-    uint4 *lcodes = ckr_lds;
-    auto ltop = reinterpret_cast<uint32_t (*)[64]>(lw + LD::top);
-    auto lsel = reinterpret_cast<uint32_t (*)[SELN]>(lw + LD::sel);
-    auto lleft = reinterpret_cast<uint32_t (*)[64]>(lw + LD::left);
-    auto lraw = reinterpret_cast<uint32_t (*)[8]>(lw + LD::raw);
-    int4 *lst = reinterpret_cast<int4 *>(lw + LD::st);
-    const int lane = threadIdx.x, slot = lane / G, b = lane % G;
-    const int pair = (int)blockIdx.x * NP + slot;
-    bool live = pair < npairs;
-    sed_pair_desc d{};
-    if (live) d = pd[pair];
-    live = live && !d.lane;
-    const int n = live ? d.n : 0, m = live ? d.m : 0;
-    int i = n, j = m, err = 0;
-    uint32_t q = live ? (uint32_t)res[pair].len : 0u;
-    const int nstripes = (n + ROWS - 1) / ROWS;
-    const int SG = (m + 63 + G - 1) / G * G, nchunks = (SG + 63) >> 6, ngroups = SG / G;
-    const uint32_t *ccp = ck + d.tb_off;
-    const uint32_t *rcp = ccp + sed_ck_col_words(R, nstripes, nchunks);
-    const uint32_t *pa = seqa + d.a_off, *pb = seqb + d.b_off;
-    uint32_t *out = ops + d.ops_off;
-    uint64_t acc = 0;  // (walker) the last 32 ops, the latest (position q) in bits 1:0
-    const uint32_t Kd = (prm.del << 16) + 8u, Ki = (prm.ins << 16) + 8u;
-    (void)Kd;
-    (void)Ki;
-    int guard = 2 * (n + m) + 8;
-    const bool walker = b == 0;
-    // key L of a cell (ladder key w of cell (ii, jj)) == q?
-    auto l_ok = [&](uint32_t w, int ii, int jj) {
-        return (uint32_t)i32_decode<R, true>(w, ii, jj, prm).y == q;
-    };
-    while (true) {
-        const bool act = live && err == 0 && i > 0 && j > 0;  // (uniform per slot)
-        if (!__any(act)) break;
-        // ---- the tile of the slot's cell (i, j) ----
-        int k = 0, Q = 0, c = 0, rowbase = 0, J0 = 0, sge = -1;
-        if (act) {
-            k = (i - 1) / ROWS;
-            const int t = ((i - 1) % ROWS) >> LR;
-            Q = t / G;
-            c = (j - 1 + t) >> 6;
-            rowbase = k * ROWS + 64 * Q;
-            J0 = 64 * c - G * Q + 1;
-            sge = j - J0 + ((i - rowbase - 1) >> LR);  // the entry cell's step in the chunk
-        }
-        int smax = 0;  // steps the sweep needs: the furthest entry of the wave
-#pragma unroll
-        for (int s = 0; s < NP; ++s) smax = max(smax, __builtin_amdgcn_readlane(sge, s * G) + 1);
-        const int ng = (smax + G - 1) / G;
-        // ---- boundary: cost rows, column checkpoints, top row and selectors (staged in LDS) ----
-        const int tl = G * Q + b;                        // this lane's forward lane
-        const int row0 = min(rowbase + R * b, max(n - 1, 0));  // 0-based str1 index of its first row (clamped)
-        const uint32_t wa = act ? pa[row0 >> 4] >> (2 * (row0 & 15)) : 0u;
-        uint32_t cv[R], V[R], top_prev, bottom;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint32_t a = (wa >> (2 * r)) & 3u;
-            cv[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
-        }
-        if (act && c >= 1) {
-            const uint32_t *cp = ccp + sed_ck_col_word(R, k, nchunks, c - 1, 0, tl);
-            uint32_t w[R + 1];
-#pragma unroll
-            for (int r = 0; r <= R; ++r) w[r] = cp[r * 64];
-#pragma unroll
-            for (int r = 0; r < R; ++r) V[r] = ck_to_lad(w[r], prm, (uint32_t)Ladder<R>::rung(r + 1));
-            top_prev = ck_to_lad(w[R], prm, 0u);
-        } else {
-            i32_reset<R, true>(V, top_prev);
-        }
-        bottom = V[R - 1];
-#pragma unroll
-        for (int r = 0; r < R; ++r) lleft[r][lane] = V[r];
-        // the row above the tile at column J0 + x (x = b + G u): the row checkpoints of forward lane G Q - 1, or
-        // lane 63 of the stripe above, at the step that lane computed the column (clamped to the stripe: past
-        // SG the columns are beyond m and never walked); row 0 and columns <= 0 hold the border
-        // (lane b's steps s0 + G u share one address: group (s0 >> LG) + u, slot s0 & (G - 1), so the loads take immediate
-        // offsets; steps outside the stripe's [0, SG) are not loaded)
-        const bool above = Q >= 1 || k >= 1;
-        const int kr = Q >= 1 ? k : k - 1, tr = Q >= 1 ? G * Q - 1 : 63;
-        const int s0 = (Q >= 1 ? 64 * c - 1 : 64 * c + 63) + b;  // (>= -1)
-        const uint32_t *rb = rcp + sed_ck_row_word(R, max(kr, 0), ngroups, 0, tr) +
-                             (int64_t)(s0 >> LG) * SED_CK_RW + (s0 & (G - 1));
-        // str2's packed words of the slot's columns J0 - G .. J0 + 63: at most 6 (R = 16) .. 7 (R = 4) words from
-        // word wb0, two per lane, staged raw in LDS
-        const int wb0 = max(J0 - G, 0) >> 4;
-        const int bw = (max(m, 1) - 1) >> 4;
-#pragma unroll
-        for (int h = 0; h < 2 * 4 / G + 1; ++h) {
-            const int x = b + G * h;
-            if (x < 8) lraw[slot][x] = act ? pb[min(wb0 + x, bw)] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < 64 / G; ++u) {
-            const int x = b + G * u;
-            uint32_t v = SED_KB3;
-            if (act && above && J0 + x >= 1 && s0 + G * u < SG) v = ck_to_lad(rb[u * SED_CK_RW], prm, 0u);
-            ltop[slot][x] = v;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < SELN / G; ++u) {
-            const int x = b + G * u;
-            const int col = J0 - (G - 1) + x;
-            const int ci = min(max(col - 1, 0), max(m - 1, 0));
-            const uint32_t wb = lraw[slot][min((ci >> 4) - wb0, 7)];
-            lsel[slot][x] = col < 1 ? SED_SEL_SENT3 : i32_sel((wb >> ((ci & 15) * 2)) & 3u);
-        }
-        __syncthreads();
-        // ---- sweep: forward steps 64 c .. 64 c + G ng - 1 of the tile's G lanes ----
-        {
-            const uint32_t *tp = ltop[slot];
-            const uint32_t *sp = lsel[slot] + (G - 1 - b);  // this lane's column at step x: J0 - b + x
-            const bool leader = b == 0;
-            for (int g = 0; g < ng; ++g) {
-                uint32_t W[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-                for (int u = 0; u < G; ++u) ckr_step<R>(V, cv, top_prev, bottom, tp[G * g + u], sp[G * g + u], leader, W, u);
-                lcodes[lane * NG + g] = make_uint4(W[0], W[1], W[2], W[3]);
-            }
-        }
-        __syncthreads();
-        // ---- walk: each slot's walker from the entry cell until it leaves the tile ----
-        if (walker && act) {
-            const uint32_t *cw = reinterpret_cast<const uint32_t *>(lcodes) + (uint32_t)slot * (uint32_t)(G * NG * 4);
-            int rt = i - rowbase - 1, sg = sge;
-            const uint32_t qin = q;
-            while (true) {
-                const int lb = rt >> LR, rr = rt & (R - 1);
-                const int kk = (sg & (G - 1)) * R + rr;
-                const uint32_t word = cw[((lb * NG + (sg >> LG)) << 2) + (kk >> 4)];
-                const uint32_t code = (word >> (2 * (kk & 15))) & 3u;
-                const uint32_t op = (code - (uint32_t)((PAT >> (4 * ((rr + 1) & (P - 1)))) & 0xFu)) & 3u;
-                if (q == 0u || op == 3u) {  // (a code outside the ladder's range: a corrupt tile)
-                    err = q == 0u ? SED_ERR_TB_LENGTH : SED_ERR_TB_CHECK;
-                    break;
-                }
-                acc = (acc << 2) | op;
-                if ((--q & 15u) == 0u) out[q >> 4] = (uint32_t)acc;
-                if (op == 0u) {
-                    sg -= 1;
-                } else {
-                    sg -= (op == 2u ? 1 : 0) + (rr == 0 ? 1 : 0);
-                    rt -= 1;
-                }
-                if (rt < 0 || sg < 0 || J0 + sg - (rt >> LR) <= 0) break;
-            }
-            i = rowbase + rt + 1;
-            j = J0 + sg - (rt >> LR);
-            if (!err && q == qin) err = SED_ERR_TB_STALL;
-            if (!err && i >= 1 && j >= 1) {  // the exit cell's L must be the ops still to emit
-                if (rt < 0) {
-                    const int x = j - J0;
-                    if (x >= 0 && x < 64 && !l_ok(ltop[slot][x], i, j)) err = SED_ERR_TB_CHECK;
-                } else if (sg < 0) {
-                    const int lb = rt >> LR;
-                    if (j == J0 - lb - 1 && !l_ok(lleft[rt & (R - 1)][slot * G + lb], i, j)) err = SED_ERR_TB_CHECK;
-                }
-            }
-            if (--guard <= 0 && !err) err = SED_ERR_TB_GUARD;
-            lst[slot] = make_int4(i, j, (int)q, err);
-        }
-        __syncthreads();
-        if (act) {
-            const int4 s = lst[slot];
-            i = s.x;
-            j = s.y;
-            q = (uint32_t)s.z;
-            err = s.w;
-        }
-        __syncthreads();  // (lst and the LDS tiles are rewritten by the next visit)
-    }
-    if (walker && live) {
-        if (!err) {  // the border: inserts along row 0, deletes along column 0
-            while (j > 0 || i > 0) {
-                if (q == 0u) {
-                    err = SED_ERR_TB_LENGTH;
-                    break;
-                }
-                const uint32_t op = j > 0 ? 0u : 1u;
-                acc = (acc << 2) | op;
-                if ((--q & 15u) == 0u) out[q >> 4] = (uint32_t)acc;
-                if (op == 0u) --j;
-                else --i;
-            }
-            if (!err && q != 0u) err = SED_ERR_TB_LENGTH;
-        }
-        if (err) res[pair].err = (uint8_t)err;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Checkpoint traceback in quarter bands (sed_traceback_ckq_kernel; round 5, the default at R = 16).
-// The replay above recomputes a tile in 64 steps but needs G lanes per pair, so at R = 16 a wave carries 16 pairs and a
-// config-4 shard only 512 waves: half a wave per SIMD, latency-bound (4.5 ms alone against 2.1 ms for the lane-per-row
-// sweep, profiles/r05/s4).  Here each forward band (16 rows) is recomputed by 4 lanes of 4 rows, so a pair takes 16
-// lanes (one DPP row) and a wave 4 pairs: 2048 waves for the shard.  The 16 lanes of a pair form one staircase: lane
-// L = 4 b + s (band b, quarter s) computes column J0 + sigma - L at sweep step sigma, i.e. band b's window (columns
-// J0 - b .. J0 - b + 63, the forward's chunk) at steps 3 b + s .. 3 b + s + 63, and its rows from band b's column
-// checkpoint.  Until its window a lane holds its checkpoint: the first 12 steps run masked per lane (the code word of
-// a masked step is shifted as if it had run), which needs neither sentinel selectors nor a compensated delete, and
-// its row above at its first step is, by construction, the lane before it (still holding, or in its first column).
-// The cell is i32_step's ladder-key cell on the period-4 ladder (rows of a lane start on multiples of 4): v_perm,
-// v_add, v_min3, v_and_or, v_alignbit + the delete add on 1 row in 4 = 5.25 VALU; 76 steps for the whole tile (72 on
-// average for the furthest entry of the wave's 4 pairs, tools/sim_ckq.py) against up to 127 at 6 per cell.  The codes
-// stay in VGPRs (19 words per lane, 4 steps each) and each pair's path is walked on the scalar unit from its entry
-// cell (readlane per op), as in sed_traceback_ck_kernel; the exit cell's L is checked against the top row or the
-// column checkpoint it leaves through.
-// ---------------------------------------------------------------------------
-#define SED_CKQ_STEPS 76
-#define SED_CKQ_GROUPS 19
-#define SED_CKQ_NX 92  // selectors of a pair: column J0 - 15 + x (x < 91)
-#define SED_RUNG4(x) ((0x1230u >> (4u * ((uint32_t)(x) & 3u))) & 0xFu)  // Ladder<4>::rung
-
-__device__ __forceinline__ void ckq_step(uint32_t (&V)[4], const uint32_t (&cv)[4], uint32_t &top_prev,
-                                         uint32_t &bottom, const uint32_t topin, const uint32_t selv, uint32_t &cw) {
-    using Lad = Ladder<4>;
-    constexpr int d0 = Lad::rung(1) - Lad::rung(0);
-    const uint32_t dg0 = top_prev + __builtin_amdgcn_perm(cv[0], (uint32_t)(d0 - 6), selv);
-    const uint32_t topv = seg_shr1<16>(topin, bottom);  // (row_shr:1: lane 0 of the pair's DPP row keeps topin)
-    uint32_t up = topv, diag = top_prev;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const uint32_t left = V[r];
-        const int c = Lad::rung(r + 1), d = c - Lad::rung(r);  // compile-time after unrolling
-        const uint32_t mm = umin3(left, d == -1 ? up : up + (uint32_t)(d + 1),
-                                  r == 0 ? dg0 : diag + __builtin_amdgcn_perm(cv[r], (uint32_t)(d - 6), selv));
-        cw = __builtin_amdgcn_alignbit(mm, cw, 2);  // step u, row r at bits 8 u + 2 r of the group's word
-        up = (mm & ~7u) | (uint32_t)c;
-        diag = left;
-        V[r] = up;
-    }
-    top_prev = topv;
-    bottom = V[3];
-}
-
-__global__ __launch_bounds__(64) void sed_traceback_ckq_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
-                                                               const uint32_t *__restrict__ seqa,
-                                                               const uint32_t *__restrict__ seqb,
-                                                               const uint32_t *__restrict__ ck,
-                                                               sed_result *__restrict__ res,
-                                                               uint32_t *__restrict__ ops, sed_i32_params prm) {
-    constexpr int R = 16, ROWS = 64 * R, G = 4, NP = 4;
-    __shared__ uint32_t ltop[NP][SED_CKQ_STEPS], lsel[NP][SED_CKQ_NX], lraw[NP][8];
-    const int lane = threadIdx.x, slot = lane >> 4, L = lane & 15, b = L >> 2, s = L & 3;
-    const int sigL = L - b;  // the lane's first step in its band's window (3 b + s)
+    using C = CkbCfg<RT>;
+    constexpr int R = 16, ROWS = 64 * R, G = 4, NP = C::NP, LPP = C::LPP;
+    constexpr uint32_t C0 = (uint32_t)Ladder<RT>::rung(0);  // rung of the rows above a lane (multiples of RT)
+    __shared__ uint32_t ltop[NP][C::STEPS], lsel[NP][C::NX], lraw[NP][C::NRAW];
+    const int lane = threadIdx.x, slot = lane / LPP, L = lane % LPP, b = L >> C::LLPB, s = L & (C::LPB - 1);
+    const int sigL = L - b;  // the lane's first step in its band's window
     const int pair = (int)blockIdx.x * NP + slot;
     bool live = pair < npairs;
     sed_pair_desc d{};
@@ -2787,108 +2542,115 @@ __global__ __launch_bounds__(64) void sed_traceback_ckq_kernel(const sed_pair_de
             c = (j - 1 + t) >> 6;
             rowbase = k * ROWS + 64 * Q;
             J0 = 64 * c - G * Q + 1;
-            sge = j - J0 + ((i - rowbase - 1) >> 2);  // the entry cell's step: column J0 + sigma - L
+            sge = j - J0 + (i - rowbase - 1) / RT;  // the entry cell's step: column J0 + sigma - L
         }
         int smax = 0;
 #pragma unroll
-        for (int p = 0; p < NP; ++p) smax = max(smax, __builtin_amdgcn_readlane(sge, 16 * p) + 1);
-        const int ng = (smax + 3) >> 2;
+        for (int p = 0; p < NP; ++p) smax = max(smax, __builtin_amdgcn_readlane(sge, LPP * p) + 1);
+        const int nw = (smax + C::SPW - 1) / C::SPW;  // code words the sweep must fill
         // ---- boundary: cost rows, column checkpoint, top row and selectors (LDS) ----
         const int tl = G * Q + b;
-        const int row0 = min(rowbase + 4 * L, max(n - 1, 0));  // 0-based str1 index of the lane's first row (clamped)
+        const int row0 = min(rowbase + RT * L, max(n - 1, 0));  // 0-based str1 index of the lane's first row (clamped)
         const uint32_t wa = act ? pa[row0 >> 4] >> (2 * (row0 & 15)) : 0u;
-        uint32_t cv[4], V[4], VI[4], top_prev, bottom;
+        uint32_t cv[RT], V[RT], VI[RT], top_prev, bottom;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < RT; ++r) {
             const uint32_t a = (wa >> (2 * r)) & 3u;
             cv[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
         }
         if (act && c >= 1) {
-            // rows 4 s .. 4 s + 3 of band b at its checkpoint column J0 - b - 1, and the row above the lane's first row
-            // there: band row 4 s - 1, or the band's top_prev (word R) for s = 0
-            const uint32_t *cp = ccp + sed_ck_col_word(R, k, nchunks, c - 1, 4 * s, tl);
-            uint32_t w[4];
+            // rows RT s .. RT s + RT - 1 of band b at its checkpoint column J0 - b - 1, and the row above the lane's first
+            // row there: band row RT s - 1, or the band's top_prev (word R) for s = 0
+            const uint32_t *cp = ccp + sed_ck_col_word(R, k, nchunks, c - 1, RT * s, tl);
+            uint32_t w[RT];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) w[r] = cp[r * 64];
+            for (int r = 0; r < RT; ++r) w[r] = cp[r * 64];
             const uint32_t wt = s ? cp[-64] : cp[R * 64];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) V[r] = ck_to_lad(w[r], prm, (uint32_t)Ladder<4>::rung(r + 1));
-            top_prev = ck_to_lad(wt, prm, 0u);
+            for (int r = 0; r < RT; ++r) V[r] = ck_to_lad(w[r], prm, (uint32_t)Ladder<RT>::rung(r + 1));
+            top_prev = ck_to_lad(wt, prm, C0);
         } else {
-            i32_reset<4, true>(V, top_prev);  // column-0 state (chunk 0: the forward's virtual columns)
+#pragma unroll
+            for (int r = 0; r < RT; ++r) V[r] = SED_KB3 + (uint32_t)Ladder<RT>::rung(r + 1);  // column 0 (chunk 0)
+            top_prev = SED_KB3 + C0;
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) VI[r] = V[r];
-        bottom = V[3];
-        // the row above the tile at column J0 + x (x = L + 16 u < 76), as in sed_traceback_ckr_kernel
+        for (int r = 0; r < RT; ++r) VI[r] = V[r];
+        bottom = V[RT - 1];
+        // the row above the tile at column J0 + x (x = L + LPP u): the row checkpoints of forward lane G Q - 1, or lane 63
+        // of the stripe above, at the step that lane computed the column (steps past SG: columns beyond m, not loaded);
+        // lane L's steps s0 + LPP u share one address with immediate offsets
         const bool above = Q >= 1 || k >= 1;
         const int kr = Q >= 1 ? k : k - 1, tr = Q >= 1 ? G * Q - 1 : 63;
         const int s0 = (Q >= 1 ? 64 * c - 1 : 64 * c + 63) + L;
         const uint32_t *rb = rcp + sed_ck_row_word(R, max(kr, 0), ngroups, 0, tr) +
                              (int64_t)(s0 >> 2) * SED_CK_RW + (s0 & 3);
-        const int wb0 = max(J0 - 16, 0) >> 4;  // str2 words of the selectors' columns (at most 7)
-        if (L < 8) lraw[slot][L] = act ? pb[min(wb0 + L, (max(m, 1) - 1) >> 4)] : 0u;
+        const int wb0 = max(J0 - LPP, 0) >> 4;  // str2 words of the selectors' columns
 #pragma unroll
-        for (int u = 0; u < 5; ++u) {
-            const int x = L + 16 * u;
-            if (x < SED_CKQ_STEPS) {
-                uint32_t v = SED_KB3;
-                if (act && above && J0 + x >= 1 && s0 + 16 * u < SG) v = ck_to_lad(rb[u * 4 * SED_CK_RW], prm, 0u);
+        for (int u = 0; u * LPP < C::NRAW; ++u) {
+            const int x = L + LPP * u;
+            if (x < C::NRAW) lraw[slot][x] = act ? pb[min(wb0 + x, (max(m, 1) - 1) >> 4)] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u * LPP < C::STEPS; ++u) {
+            const int x = L + LPP * u;
+            if (x < C::STEPS) {
+                uint32_t v = SED_KB3 + C0;
+                if (act && above && J0 + x >= 1 && s0 + LPP * u < SG) v = ck_to_lad(rb[u * (LPP / 4) * SED_CK_RW], prm, C0);
                 ltop[slot][x] = v;
             }
         }
         __syncthreads();
 #pragma unroll
-        for (int u = 0; u < 6; ++u) {
-            const int x = L + 16 * u;
-            if (x < SED_CKQ_NX) {
-                const int col = J0 - 15 + x;
+        for (int u = 0; u * LPP < C::NX; ++u) {
+            const int x = L + LPP * u;
+            if (x < C::NX) {
+                const int col = J0 - (LPP - 1) + x;
                 const int ci = min(max(col - 1, 0), max(m - 1, 0));
-                const uint32_t wb = lraw[slot][min(max((ci >> 4) - wb0, 0), 7)];
+                const uint32_t wb = lraw[slot][min(max((ci >> 4) - wb0, 0), C::NRAW - 1)];
                 lsel[slot][x] = col < 1 ? SED_SEL_SENT3 : i32_sel((wb >> ((ci & 15) * 2)) & 3u);
             }
         }
         __syncthreads();
-        // ---- sweep ----
-        uint32_t CW[SED_CKQ_GROUPS];
+        // ---- sweep: code word w holds steps SPW w .. SPW w + SPW - 1 ----
+        uint32_t CW[C::WORDS];
         {
             const uint32_t *tp = ltop[slot];
-            const uint32_t *sp = lsel[slot] + (15 - L);  // the lane's column at step x: J0 + x - L
+            const uint32_t *sp = lsel[slot] + (LPP - 1 - L);  // the lane's column at step x: J0 + x - L
+            const bool leader = L == 0;
 #pragma unroll
-            for (int g = 0; g < 3; ++g) {  // steps 0 .. 11: lanes before their window hold (masked)
+            for (int w = 0; w < C::PRO; ++w) {  // lanes before their window hold (masked)
                 uint32_t cw = 0u;
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int sig = 4 * g + u;
-                    if (sig >= sigL) ckq_step(V, cv, top_prev, bottom, tp[sig], sp[sig], cw);
-                    else cw >>= 8;
+                for (int u = 0; u < C::SPW; ++u) {
+                    const int sig = C::SPW * w + u;
+                    if (sig >= sigL) ckb_step<RT>(V, cv, top_prev, bottom, tp[sig], sp[sig], leader, cw);
+                    else cw >>= 2 * RT;
                 }
-                CW[g] = cw;
+                CW[w] = cw;
             }
 #pragma unroll
-            for (int g = 3; g < SED_CKQ_GROUPS; ++g) {
-                if (g < ng) {  // (uniform; no break: the loop unrolls, so every code word sits in its own VGPR)
+            for (int w = C::PRO; w < C::WORDS; ++w) {
+                if (w < nw) {  // (uniform; no break: the loop unrolls, so every code word sits in its own VGPR)
                     uint32_t cw = 0u;
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) ckq_step(V, cv, top_prev, bottom, tp[4 * g + u], sp[4 * g + u], cw);
-                    CW[g] = cw;
+                    for (int u = 0; u < C::SPW; ++u) {
+                        const int sig = C::SPW * w + u;
+                        if (sig < C::STEPS) ckb_step<RT>(V, cv, top_prev, bottom, tp[sig], sp[sig], leader, cw);
+                        else cw >>= 2 * RT;
+                    }
+                    CW[w] = cw;
                 }
             }
         }
-        // the codes as ops: field (step u, row r) of a word holds (rung(r + 1) + op) & 3 and rung(r + 1) = 3, 2, 1, 0 for
-        // r = 0 .. 3, so op = field + r + 1 (mod 4): one SWAR mod-4 add of 0x39393939 per word, off the scalar walk
+        // the codes as ops: field (row r) holds (rung(r + 1) + op) & 3, so op = field + ADD_r (mod 4): a SWAR mod-4 add
 #pragma unroll
-        for (int g = 0; g < SED_CKQ_GROUPS; ++g)
-            CW[g] = ((CW[g] & 0x55555555u) + 0x11111111u) ^ ((CW[g] ^ 0x39393939u) & 0xAAAAAAAAu);
-        // ---- walk: each pair's path on the scalar unit, word by word ----
-        // State B = 8 sigma + 2 r (bit index of the cell's op in its lane's code stream: word B >> 5, bit B & 31) and the
-        // lane LP.  Every op moves B uniformly (insert 8, delete 2, update 10), also into the lane above: from row 0 at
-        // step sigma a delete reaches row 3 of lane L - 1 at sigma - 1, i.e. B - 2.  The lane changes on a delete or
-        // update from row 0, and the walk leaves the tile above lane 0 or below the lane's bound lim (its window starts
-        // at step 3 b + s; chunk 0: column 0).
+        for (int w = 0; w < C::WORDS; ++w)
+            CW[w] = ((CW[w] & 0x55555555u) + (C::ADD & 0x55555555u)) ^ ((CW[w] ^ C::ADD) & 0xAAAAAAAAu);
+        // ---- walk: each pair's path on the scalar unit (state B = 2 RT sigma + 2 r and the lane LP) ----
 #pragma unroll 1
         for (int p = 0; p < NP; ++p) {
-            const int pl = 16 * p;
+            const int pl = LPP * p;
             if (!__builtin_amdgcn_readlane(act ? 1 : 0, pl)) continue;
             const int si0 = __builtin_amdgcn_readlane(i, pl), sj0 = __builtin_amdgcn_readlane(j, pl);
             const int sJ0 = __builtin_amdgcn_readlane(J0, pl), srb = __builtin_amdgcn_readlane(rowbase, pl);
@@ -2897,68 +2659,70 @@ __global__ __launch_bounds__(64) void sed_traceback_ckq_kernel(const sed_pair_de
             uint32_t *sout = (uint32_t *)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uintptr_t)out, pl)) |
                                           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uintptr_t)out >> 32), pl) << 32));
             const int rt0 = si0 - srb - 1;
-            int LP = pl + (rt0 >> 2);
-            int B = 8 * (sj0 - sJ0 + (rt0 >> 2)) + 2 * (rt0 & 3);
-            auto lim_of = [&](const int Lw) { return 8 * max(Lw - (Lw >> 2), Lw - sJ0 + 1); };
+            int LP = pl + rt0 / RT;
+            int B = 2 * RT * (sj0 - sJ0 + rt0 / RT) + 2 * (rt0 % RT);
+            // below lim the walk leaves lane L's window (step L - b) or, in chunk 0, reaches column 0
+            auto lim_of = [&](const int Lw) { return 2 * RT * max(Lw - (Lw >> C::LLPB), Lw - sJ0 + 1); };
             int lim = lim_of(LP - pl);
             bool above = false, stop = false;
 #pragma unroll
-            for (int w = SED_CKQ_GROUPS - 1; w >= 0; --w) {
+            for (int w = C::WORDS - 1; w >= 0; --w) {
                 if (stop) continue;  // (no break: the loop unrolls, CW[w] is a fixed VGPR)
                 int lo = max(32 * w, lim);
-                // One op per iteration, written as scalar asm: the compiler turned the combined conditions into lane
-                // masks (~30 SALU per op).  Here: ~15 SALU + the v_readlane on the common path; the script word
-                // completed at q (a multiple of 16, below the visit's first q) is stored from the SGPRs; a delete or
-                // update from row 0 moves to the lane above (above the tile: ab = 1) and recomputes the bound.
+                // One op per iteration in scalar asm (the compiler turned the combined conditions into lane masks, ~30
+                // SALU per op): ~15 SALU + the v_readlane on the common path.  The script word completed at q (a multiple
+                // of 16 below the visit's first q) is stored from the SGPRs; a delete or update from row 0 moves to the
+                // lane above (above the tile: ab = 1) and recomputes the bound.
                 uint32_t op, t, t2, ab = 0;
                 uint32_t vo, vd;
                 asm volatile(
-                    "Lwl%=:\n\t"
+                    "Lbl%=:\n\t"
                     "s_cmp_lt_i32 %[B], %[lo]\n\t"
-                    "s_cbranch_scc1 Lwx%=\n\t"
+                    "s_cbranch_scc1 Lbx%=\n\t"
                     "v_readlane_b32 %[t], %[cw], %[LP]\n\t"
                     "s_lshr_b32 %[t], %[t], %[B]\n\t"
                     "s_and_b32 %[op], %[t], 3\n\t"
                     "s_lshl2_add_u32 %[acc], %[acc], %[op]\n\t"
                     "s_add_u32 %[q], %[q], -1\n\t"
                     "s_and_b32 %[t], %[q], 15\n\t"
-                    "s_cbranch_scc1 Lwn%=\n\t"
+                    "s_cbranch_scc1 Lbn%=\n\t"
                     "s_cmp_lt_u32 %[q], %[qin]\n\t"
-                    "s_cbranch_scc0 Lwn%=\n\t"
+                    "s_cbranch_scc0 Lbn%=\n\t"
                     "s_lshr_b32 %[t], %[q], 2\n\t"
                     "s_and_b32 %[t], %[t], -4\n\t"
                     "s_waitcnt expcnt(0)\n\t"
                     "v_mov_b32 %[vo], %[t]\n\t"
                     "v_mov_b32 %[vd], %[acc]\n\t"
                     "global_store_dword %[vo], %[vd], %[out]\n"
-                    "Lwn%=:\n\t"
-                    "s_and_b32 %[t2], %[B], 6\n\t"
+                    "Lbn%=:\n\t"
+                    "s_and_b32 %[t2], %[B], %[rmask]\n\t"
                     "s_lshl_b32 %[t], %[op], 3\n\t"
-                    "s_lshr_b32 %[t], 0x800a0208, %[t]\n\t"
+                    "s_lshr_b32 %[t], %[moves], %[t]\n\t"
                     "s_and_b32 %[t], %[t], 0xff\n\t"
                     "s_sub_u32 %[B], %[B], %[t]\n\t"
                     "s_cmp_lg_u32 %[t2], 0\n\t"
-                    "s_cbranch_scc1 Lwl%=\n\t"
+                    "s_cbranch_scc1 Lbl%=\n\t"
                     "s_cmp_eq_u32 %[op], 0\n\t"
-                    "s_cbranch_scc1 Lwl%=\n\t"
+                    "s_cbranch_scc1 Lbl%=\n\t"
                     "s_sub_u32 %[LP], %[LP], 1\n\t"
                     "s_cmp_lt_i32 %[LP], %[pl]\n\t"
-                    "s_cbranch_scc1 Lwa%=\n\t"
+                    "s_cbranch_scc1 Lba%=\n\t"
                     "s_sub_u32 %[t], %[LP], %[pl]\n\t"
-                    "s_lshr_b32 %[t2], %[t], 2\n\t"
+                    "s_lshr_b32 %[t2], %[t], %[llpb]\n\t"
                     "s_sub_u32 %[t2], %[t], %[t2]\n\t"
                     "s_sub_u32 %[t], %[t], %[J0m1]\n\t"
                     "s_max_i32 %[t], %[t], %[t2]\n\t"
-                    "s_lshl_b32 %[lim], %[t], 3\n\t"
+                    "s_lshl_b32 %[lim], %[t], %[lrt]\n\t"
                     "s_max_i32 %[lo], %[lim], %[w32]\n\t"
-                    "s_branch Lwl%=\n"
-                    "Lwa%=:\n\t"
+                    "s_branch Lbl%=\n"
+                    "Lba%=:\n\t"
                     "s_mov_b32 %[ab], 1\n"
-                    "Lwx%=:"
+                    "Lbx%=:"
                     : [B] "+s"(B), [LP] "+s"(LP), [q] "+s"(sq), [acc] "+s"(sacc), [lo] "+s"(lo), [lim] "+s"(lim),
                       [op] "=&s"(op), [t] "=&s"(t), [t2] "=&s"(t2), [ab] "+s"(ab), [vo] "=&v"(vo), [vd] "=&v"(vd)
                     : [cw] "v"(CW[w]), [qin] "s"(qin), [pl] "s"(pl), [J0m1] "s"(sJ0 - 1), [w32] "s"(32 * w),
-                      [out] "s"(sout)
+                      [out] "s"(sout), [rmask] "i"(2 * RT - 2), [moves] "s"(C::MOVES), [llpb] "i"(C::LLPB),
+                      [lrt] "i"(RT == 4 ? 3 : 2)
                     : "scc", "memory");
                 (void)op;
                 (void)t;
@@ -2968,29 +2732,30 @@ __global__ __launch_bounds__(64) void sed_traceback_ckq_kernel(const sed_pair_de
                 if (ab) above = true;
                 if (above || B < lim) stop = true;
             }
-            const int rt = above ? -1 : 4 * (LP - pl) + ((B >> 1) & 3), sg = B >> 3;
+            const int rt = above ? -1 : RT * (LP - pl) + ((B >> 1) & (RT - 1));
+            const int sg = B >> (RT == 4 ? 3 : 2);  // (floor: B < 0 above the tile's first columns)
+            const int Lx = above ? -1 : LP - pl;
             int serr = sq > qin ? SED_ERR_TB_LENGTH : 0;
-            const int si = srb + rt + 1, sj = sJ0 + sg - (rt >> 2);
+            const int si = srb + rt + 1, sj = sJ0 + sg - Lx;
             if (!serr && sq == qin) serr = SED_ERR_TB_STALL;
             if (!serr && si >= 1 && sj >= 1) {  // the exit cell's L must be the ops still to emit
                 uint32_t key = 0u;
                 bool chk = false;
                 if (rt < 0) {
                     const int x = sj - sJ0;
-                    if (x >= 0 && x < SED_CKQ_STEPS) {
+                    if (x >= 0 && x < C::STEPS) {
                         key = ltop[p][x];
                         chk = true;
                     }
-                } else {
-                    const int lw = rt >> 2;
-                    if (sj == sJ0 - (lw >> 2) - 1) {
-                        const int rr = rt & 3;
-                        const uint32_t vr = rr == 0 ? VI[0] : rr == 1 ? VI[1] : rr == 2 ? VI[2] : VI[3];
-                        key = (uint32_t)__builtin_amdgcn_readlane((int)vr, pl + lw);
-                        chk = true;
-                    }
+                } else if (sj == sJ0 - (Lx >> C::LLPB) - 1) {  // left through the band's checkpoint column
+                    const int rr = rt & (RT - 1);
+                    uint32_t vr = VI[0];
+#pragma unroll
+                    for (int r = 1; r < RT; ++r) vr = rr == r ? VI[r] : vr;
+                    key = (uint32_t)__builtin_amdgcn_readlane((int)vr, pl + Lx);
+                    chk = true;
                 }
-                if (chk && (uint32_t)i32_decode<4, true>(key, si, sj, prm).y != sq) serr = SED_ERR_TB_CHECK;
+                if (chk && (uint32_t)i32_decode<RT, true>(key, si, sj, prm).y != sq) serr = SED_ERR_TB_CHECK;
             }
             const int sguard = __builtin_amdgcn_readlane(guard, pl) - 1;
             if (!serr && sguard <= 0) serr = SED_ERR_TB_GUARD;
@@ -3289,26 +3054,16 @@ hipError_t sed_launch_ck_codes(const sed_launch &L, int max_tiles, const sed_i32
 hipError_t sed_launch_traceback_ck(const sed_launch &L, uint32_t *ops, const sed_i32_params &prm) {
     const dim3 grid(L.npairs), block(64);
     const uint32_t *a = (const uint32_t *)L.seqa, *b = (const uint32_t *)L.seqb;
-    // SED_CK_REPLAY (A/B): 0 = the lane-per-row sweep (sed_traceback_ck_kernel) at every R, 1 = the forward-lane replay
-    // (sed_traceback_ckr_kernel) at every R, 2 = the quarter-band kernel (sed_traceback_ckq_kernel) at R = 16; unset: 2
-    static const int replay_env = [] { const char *e = getenv("SED_CK_REPLAY"); return e ? atoi(e) : 2; }();
-    if (replay_env == 2 && L.R == 16) {
-        SED_LAUNCH(sed_traceback_ckq_kernel, dim3((L.npairs + 3) / 4), block, 0, L, L.pd, L.npairs, a, b, L.tb, L.res,
-                   ops, prm);
-        return hipGetLastError();
-    }
-    if (replay_env == 1) {
-        const dim3 gr((L.npairs + L.R - 1) / L.R);  // R pairs per wave
-        switch (L.R) {
-#define CASE(RR)                                                                                                  \
-    case RR:                                                                                                      \
-        SED_LAUNCH(sed_traceback_ckr_kernel<RR>, gr, block, CkrLds<RR>::words * 4, L, L.pd, L.npairs, a, b, L.tb, \
-                   L.res, ops, prm);                                                                              \
-        break;
-            CASE(4) CASE(8) CASE(16)
-#undef CASE
-        default: return hipErrorInvalidValue;
-        }
+    // SED_CK_TB (A/B): 0 = the lane-per-row sweep (sed_traceback_ck_kernel), 2 / 4 = band slices of 2 / 4 rows per lane
+    // (sed_traceback_ckb_kernel, R = 16 only; slower, profiles/r05/s9); unset: 0
+    static const int ckb_env = [] { const char *e = getenv("SED_CK_TB"); return e ? atoi(e) : 0; }();
+    if (L.R == 16 && (ckb_env == 2 || ckb_env == 4)) {
+        if (ckb_env == 2)
+            SED_LAUNCH(sed_traceback_ckb_kernel<2>, dim3((L.npairs + 1) / 2), block, 0, L, L.pd, L.npairs, a, b, L.tb,
+                       L.res, ops, prm);
+        else
+            SED_LAUNCH(sed_traceback_ckb_kernel<4>, dim3((L.npairs + 3) / 4), block, 0, L, L.pd, L.npairs, a, b, L.tb,
+                       L.res, ops, prm);
         return hipGetLastError();
     }
     switch (L.R) {
