@@ -791,7 +791,7 @@ def main():
                     "sed_lane_i32_kernel")] if nl else []))
     tb_kernels = []
     if want_script and nl < P:
-        tb_kernels = {2: ["sed_traceback_ck_kernel", "sed_traceback_ckb_kernel"], 3: ["sed_tb_stripemap_kernel", "sed_tb_stripeemit_kernel"],
+        tb_kernels = {2: ["sed_traceback_ck_kernel"], 3: ["sed_tb_stripemap_kernel", "sed_tb_stripeemit_kernel"],
                       4: ["sed_tb_stripemap_kernel", "sed_tb_stripeemit_kernel", "sed_traceback_kernel",
                           "sed_traceback_window_kernel"],
                       1: ["sed_traceback_kernel", "sed_traceback_window_kernel"]}.get(batch.traceback_mode, [])

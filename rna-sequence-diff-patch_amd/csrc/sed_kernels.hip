@@ -2415,380 +2415,6 @@ __global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_des
 }
 
 // ---------------------------------------------------------------------------
-// Checkpoint traceback in band slices (sed_traceback_ckb_kernel<RT>; round 5).
-// A 64-row tile is G = 4 forward lanes ("bands") of 16 rows, and the forward kernel computed band b in the 64 steps of
-// one chunk from its own column checkpoint (column J0 - b - 1).  Here each band is recomputed by 16/RT lanes of RT rows,
-// so a pair takes LPP = 64/RT lanes and a wave NP = RT pairs, each at its own tile, in lockstep.  The LPP lanes of a pair
-// form one staircase: lane L (band b = L / (16/RT)) computes column J0 + sigma - L at sweep step sigma, i.e. band b's
-// window (columns J0 - b .. J0 - b + 63) at steps L - b .. L - b + 63, its rows starting from band b's checkpoint.
-// Until its window a lane holds its checkpoint: the first steps run masked per lane (a masked step's code bits are
-// shifted in as if it had run), so no sentinel selector or compensated delete is needed, and at its first step the row
-// above is, by construction, the lane before it (holding, or in its first column).  The cell is i32_step's ladder-key
-// cell on the period-RT ladder (a lane's rows start on multiples of RT): v_perm, v_add, v_min3, v_and_or, v_alignbit and
-// the delete add on one row in RT.  The lane-per-row sweep (sed_traceback_ck_kernel) instead runs a 64-lane staircase:
-// up to 127 steps per tile at 6 VALU per cell.
-// The codes stay in VGPRs (a word per 16/RT steps), are turned into ops by one SWAR add per word, and each pair's path
-// is walked on the scalar unit in asm: with B = 2 RT sigma + 2 r (the op's bit in its lane's code stream) every op moves
-// B by the same amount whether or not it leaves the lane (insert 2 RT, delete 2, update 2 RT + 2: from row 0 at step
-// sigma a delete reaches row RT - 1 of the lane above at sigma - 1); the lane changes on a delete or update from row 0.
-// The exit cell's L is checked against the top row or the column checkpoint the walk leaves through.
-// RT = 2 (2 pairs per wave, 4096 waves for the config-4 shard) and RT = 4 (4 pairs, 2048 waves): DESIGN.md 3.6b.
-// ---------------------------------------------------------------------------
-// forward key (distance or dot) -> the ladder key of the same (D, L) with op 0 on rung c:
-// W = ((D - i del - j ins) << 16) - 8U + SED_KB3 + c, U = i + j - L (the updates on the path)
-__device__ __forceinline__ uint32_t ck_to_lad(uint32_t w, const sed_i32_params &prm, uint32_t c) {
-    if (prm.dot) {  // k = A X + U, D - i del - j ins = -X
-        const uint32_t k = w - SED_KB_DOT;
-        const uint32_t X = __umulhi(k, prm.dotM) >> (prm.dotS - 32u);
-        const uint32_t U = k - __umul24(prm.dotA, X);
-        return SED_KB3 + c - (X << 16) - 8u * U;
-    }
-    const uint32_t U = (SED_KB - w) & 0xFFFFu;  // w = ((D - i del - j ins) << 16) - U + SED_KB
-    return w - 7u * U + (SED_KB3 - SED_KB) + c;
-}
-
-template <int RT> struct CkbCfg {
-    static_assert(RT == 2 || RT == 4, "RT in {2, 4}");
-    static constexpr int LPP = 64 / RT;              // lanes per pair
-    static constexpr int NP = 64 / LPP;              // pairs per wave
-    static constexpr int LPB = 16 / RT;              // lanes per band
-    static constexpr int LLPB = RT == 4 ? 2 : 3;     // log2(LPB)
-    static constexpr int SMAX = LPP - 1 - 3;         // last lane's first window step (L - b)
-    static constexpr int STEPS = 64 + SMAX;          // 76 (RT = 4), 92 (RT = 2)
-    static constexpr int SPW = 16 / RT;              // steps per code word
-    static constexpr int LSPW = RT == 4 ? 2 : 3;
-    static constexpr int WORDS = (STEPS + SPW - 1) / SPW;  // 19, 12
-    static constexpr int PRO = (SMAX + SPW - 1) / SPW;  // words run with per-lane masks (steps 0 .. SMAX - 1)
-    static constexpr int NX = STEPS + LPP;           // selectors of a pair: column J0 - (LPP - 1) + x
-    static constexpr int NRAW = (NX + 15) / 16 + 2;  // str2 words behind them
-    // the code field (row r) holds (rung(r + 1) + op) & 3: op = field + ADD_r (mod 4), per word
-    static constexpr uint32_t ADD = RT == 4 ? 0x39393939u : 0xCCCCCCCCu;
-    static constexpr uint32_t MOVES = RT == 4 ? 0x800A0208u : 0x80060204u;  // B decrement per op (op 3: out)
-};
-// Ladder<2>: rungs 1, 0 (i even, odd): the delete is free on odd rows, +2 on even rows
-template <> struct Ladder<2> {
-    static constexpr int P = 2;
-    static constexpr uint64_t pat = 0x01ull;
-    static constexpr int rung(int i) { return (int)((pat >> (4 * (i & 1))) & 0xF); }
-};
-
-template <int RT>
-__device__ __forceinline__ void ckb_step(uint32_t (&V)[RT], const uint32_t (&cv)[RT], uint32_t &top_prev,
-                                         uint32_t &bottom, const uint32_t topin, const uint32_t selv,
-                                         const bool leader, uint32_t &cw) {
-    using Lad = Ladder<RT>;
-    constexpr int d0 = Lad::rung(1) - Lad::rung(0);
-    const uint32_t dg0 = top_prev + __builtin_amdgcn_perm(cv[0], (uint32_t)(d0 - 6), selv);
-    uint32_t topv;
-    if constexpr (RT == 4) {
-        topv = seg_shr1<16>(topin, bottom);  // (a pair is one DPP row: row_shr:1 leaves its lane 0 topin)
-    } else {
-        topv = dpp_shr1(topin, bottom);      // (a pair spans two DPP rows: its lane 0 takes topin by a select)
-        topv = leader ? topin : topv;
-    }
-    uint32_t up = topv, diag = top_prev;
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-        const uint32_t left = V[r];
-        const int c = Lad::rung(r + 1), d = c - Lad::rung(r);  // compile-time after unrolling
-        const uint32_t mm = umin3(left, d == -1 ? up : up + (uint32_t)(d + 1),
-                                  r == 0 ? dg0 : diag + __builtin_amdgcn_perm(cv[r], (uint32_t)(d - 6), selv));
-        cw = __builtin_amdgcn_alignbit(mm, cw, 2);  // step u, row r at bits 2 (RT u + r) of the word
-        up = (mm & ~7u) | (uint32_t)c;
-        diag = left;
-        V[r] = up;
-    }
-    top_prev = topv;
-    bottom = V[RT - 1];
-}
-
-template <int RT>
-__global__ __launch_bounds__(64) void sed_traceback_ckb_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
-                                                               const uint32_t *__restrict__ seqa,
-                                                               const uint32_t *__restrict__ seqb,
-                                                               const uint32_t *__restrict__ ck,
-                                                               sed_result *__restrict__ res,
-                                                               uint32_t *__restrict__ ops, sed_i32_params prm) {
-    using C = CkbCfg<RT>;
-    constexpr int R = 16, ROWS = 64 * R, G = 4, NP = C::NP, LPP = C::LPP;
-    constexpr uint32_t C0 = (uint32_t)Ladder<RT>::rung(0);  // rung of the rows above a lane (multiples of RT)
-    __shared__ uint32_t ltop[NP][C::STEPS], lsel[NP][C::NX], lraw[NP][C::NRAW];
-    const int lane = threadIdx.x, slot = lane / LPP, L = lane % LPP, b = L >> C::LLPB, s = L & (C::LPB - 1);
-    const int sigL = L - b;  // the lane's first step in its band's window
-    const int pair = (int)blockIdx.x * NP + slot;
-    bool live = pair < npairs;
-    sed_pair_desc d{};
-    if (live) d = pd[pair];
-    live = live && !d.lane;
-    const int n = live ? d.n : 0, m = live ? d.m : 0;
-    int i = n, j = m, err = 0;
-    uint32_t q = live ? (uint32_t)res[pair].len : 0u, acc = 0u;  // acc: the last 16 ops, the latest in bits 1:0
-    int guard = 2 * (n + m) + 8;
-    const int nstripes = (n + ROWS - 1) / ROWS;
-    const int SG = (m + 63 + G - 1) / G * G, nchunks = (SG + 63) >> 6, ngroups = SG / G;
-    const uint32_t *ccp = ck + d.tb_off;
-    const uint32_t *rcp = ccp + sed_ck_col_words(R, nstripes, nchunks);
-    const uint32_t *pa = seqa + d.a_off, *pb = seqb + d.b_off;
-    uint32_t *out = ops + d.ops_off;
-    while (true) {
-        const bool act = live && err == 0 && i > 0 && j > 0;  // (uniform per pair)
-        if (!__any(act)) break;
-        // ---- the tile of the pair's cell (i, j) ----
-        int k = 0, Q = 0, c = 0, rowbase = 0, J0 = 0, sge = -1;
-        if (act) {
-            k = (i - 1) / ROWS;
-            const int t = ((i - 1) % ROWS) >> 4;
-            Q = t >> 2;
-            c = (j - 1 + t) >> 6;
-            rowbase = k * ROWS + 64 * Q;
-            J0 = 64 * c - G * Q + 1;
-            sge = j - J0 + (i - rowbase - 1) / RT;  // the entry cell's step: column J0 + sigma - L
-        }
-        int smax = 0;
-#pragma unroll
-        for (int p = 0; p < NP; ++p) smax = max(smax, __builtin_amdgcn_readlane(sge, LPP * p) + 1);
-        const int nw = (smax + C::SPW - 1) / C::SPW;  // code words the sweep must fill
-        // ---- boundary: cost rows, column checkpoint, top row and selectors (LDS) ----
-        const int tl = G * Q + b;
-        const int row0 = min(rowbase + RT * L, max(n - 1, 0));  // 0-based str1 index of the lane's first row (clamped)
-        const uint32_t wa = act ? pa[row0 >> 4] >> (2 * (row0 & 15)) : 0u;
-        uint32_t cv[RT], V[RT], VI[RT], top_prev, bottom;
-#pragma unroll
-        for (int r = 0; r < RT; ++r) {
-            const uint32_t a = (wa >> (2 * r)) & 3u;
-            cv[r] = a == 0 ? prm.costrow[0] : a == 1 ? prm.costrow[1] : a == 2 ? prm.costrow[2] : prm.costrow[3];
-        }
-        if (act && c >= 1) {
-            // rows RT s .. RT s + RT - 1 of band b at its checkpoint column J0 - b - 1, and the row above the lane's first
-            // row there: band row RT s - 1, or the band's top_prev (word R) for s = 0
-            const uint32_t *cp = ccp + sed_ck_col_word(R, k, nchunks, c - 1, RT * s, tl);
-            uint32_t w[RT];
-#pragma unroll
-            for (int r = 0; r < RT; ++r) w[r] = cp[r * 64];
-            const uint32_t wt = s ? cp[-64] : cp[R * 64];
-#pragma unroll
-            for (int r = 0; r < RT; ++r) V[r] = ck_to_lad(w[r], prm, (uint32_t)Ladder<RT>::rung(r + 1));
-            top_prev = ck_to_lad(wt, prm, C0);
-        } else {
-#pragma unroll
-            for (int r = 0; r < RT; ++r) V[r] = SED_KB3 + (uint32_t)Ladder<RT>::rung(r + 1);  // column 0 (chunk 0)
-            top_prev = SED_KB3 + C0;
-        }
-#pragma unroll
-        for (int r = 0; r < RT; ++r) VI[r] = V[r];
-        bottom = V[RT - 1];
-        // the row above the tile at column J0 + x (x = L + LPP u): the row checkpoints of forward lane G Q - 1, or lane 63
-        // of the stripe above, at the step that lane computed the column (steps past SG: columns beyond m, not loaded);
-        // lane L's steps s0 + LPP u share one address with immediate offsets
-        const bool above = Q >= 1 || k >= 1;
-        const int kr = Q >= 1 ? k : k - 1, tr = Q >= 1 ? G * Q - 1 : 63;
-        const int s0 = (Q >= 1 ? 64 * c - 1 : 64 * c + 63) + L;
-        const uint32_t *rb = rcp + sed_ck_row_word(R, max(kr, 0), ngroups, 0, tr) +
-                             (int64_t)(s0 >> 2) * SED_CK_RW + (s0 & 3);
-        const int wb0 = max(J0 - LPP, 0) >> 4;  // str2 words of the selectors' columns
-#pragma unroll
-        for (int u = 0; u * LPP < C::NRAW; ++u) {
-            const int x = L + LPP * u;
-            if (x < C::NRAW) lraw[slot][x] = act ? pb[min(wb0 + x, (max(m, 1) - 1) >> 4)] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u * LPP < C::STEPS; ++u) {
-            const int x = L + LPP * u;
-            if (x < C::STEPS) {
-                uint32_t v = SED_KB3 + C0;
-                if (act && above && J0 + x >= 1 && s0 + LPP * u < SG) v = ck_to_lad(rb[u * (LPP / 4) * SED_CK_RW], prm, C0);
-                ltop[slot][x] = v;
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u * LPP < C::NX; ++u) {
-            const int x = L + LPP * u;
-            if (x < C::NX) {
-                const int col = J0 - (LPP - 1) + x;
-                const int ci = min(max(col - 1, 0), max(m - 1, 0));
-                const uint32_t wb = lraw[slot][min(max((ci >> 4) - wb0, 0), C::NRAW - 1)];
-                lsel[slot][x] = col < 1 ? SED_SEL_SENT3 : i32_sel((wb >> ((ci & 15) * 2)) & 3u);
-            }
-        }
-        __syncthreads();
-        // ---- sweep: code word w holds steps SPW w .. SPW w + SPW - 1 ----
-        uint32_t CW[C::WORDS];
-        {
-            const uint32_t *tp = ltop[slot];
-            const uint32_t *sp = lsel[slot] + (LPP - 1 - L);  // the lane's column at step x: J0 + x - L
-            const bool leader = L == 0;
-#pragma unroll
-            for (int w = 0; w < C::PRO; ++w) {  // lanes before their window hold (masked)
-                uint32_t cw = 0u;
-#pragma unroll
-                for (int u = 0; u < C::SPW; ++u) {
-                    const int sig = C::SPW * w + u;
-                    if (sig >= sigL) ckb_step<RT>(V, cv, top_prev, bottom, tp[sig], sp[sig], leader, cw);
-                    else cw >>= 2 * RT;
-                }
-                CW[w] = cw;
-            }
-#pragma unroll
-            for (int w = C::PRO; w < C::WORDS; ++w) {
-                if (w < nw) {  // (uniform; no break: the loop unrolls, so every code word sits in its own VGPR)
-                    uint32_t cw = 0u;
-#pragma unroll
-                    for (int u = 0; u < C::SPW; ++u) {
-                        const int sig = C::SPW * w + u;
-                        if (sig < C::STEPS) ckb_step<RT>(V, cv, top_prev, bottom, tp[sig], sp[sig], leader, cw);
-                        else cw >>= 2 * RT;
-                    }
-                    CW[w] = cw;
-                }
-            }
-        }
-        // the codes as ops: field (row r) holds (rung(r + 1) + op) & 3, so op = field + ADD_r (mod 4): a SWAR mod-4 add
-#pragma unroll
-        for (int w = 0; w < C::WORDS; ++w)
-            CW[w] = ((CW[w] & 0x55555555u) + (C::ADD & 0x55555555u)) ^ ((CW[w] ^ C::ADD) & 0xAAAAAAAAu);
-        // ---- walk: each pair's path on the scalar unit (state B = 2 RT sigma + 2 r and the lane LP) ----
-#pragma unroll 1
-        for (int p = 0; p < NP; ++p) {
-            const int pl = LPP * p;
-            if (!__builtin_amdgcn_readlane(act ? 1 : 0, pl)) continue;
-            const int si0 = __builtin_amdgcn_readlane(i, pl), sj0 = __builtin_amdgcn_readlane(j, pl);
-            const int sJ0 = __builtin_amdgcn_readlane(J0, pl), srb = __builtin_amdgcn_readlane(rowbase, pl);
-            const uint32_t qin = (uint32_t)__builtin_amdgcn_readlane((int)q, pl);
-            uint32_t sq = qin, sacc = (uint32_t)__builtin_amdgcn_readlane((int)acc, pl);
-            uint32_t *sout = (uint32_t *)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uintptr_t)out, pl)) |
-                                          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uintptr_t)out >> 32), pl) << 32));
-            const int rt0 = si0 - srb - 1;
-            int LP = pl + rt0 / RT;
-            int B = 2 * RT * (sj0 - sJ0 + rt0 / RT) + 2 * (rt0 % RT);
-            // below lim the walk leaves lane L's window (step L - b) or, in chunk 0, reaches column 0
-            auto lim_of = [&](const int Lw) { return 2 * RT * max(Lw - (Lw >> C::LLPB), Lw - sJ0 + 1); };
-            int lim = lim_of(LP - pl);
-            bool above = false, stop = false;
-#pragma unroll
-            for (int w = C::WORDS - 1; w >= 0; --w) {
-                if (stop) continue;  // (no break: the loop unrolls, CW[w] is a fixed VGPR)
-                int lo = max(32 * w, lim);
-                // One op per iteration in scalar asm (the compiler turned the combined conditions into lane masks, ~30
-                // SALU per op): ~15 SALU + the v_readlane on the common path.  The script word completed at q (a multiple
-                // of 16 below the visit's first q) is stored from the SGPRs; a delete or update from row 0 moves to the
-                // lane above (above the tile: ab = 1) and recomputes the bound.
-                uint32_t op, t, t2, ab = 0;
-                uint32_t vo, vd;
-                asm volatile(
-                    "Lbl%=:\n\t"
-                    "s_cmp_lt_i32 %[B], %[lo]\n\t"
-                    "s_cbranch_scc1 Lbx%=\n\t"
-                    "v_readlane_b32 %[t], %[cw], %[LP]\n\t"
-                    "s_lshr_b32 %[t], %[t], %[B]\n\t"
-                    "s_and_b32 %[op], %[t], 3\n\t"
-                    "s_lshl2_add_u32 %[acc], %[acc], %[op]\n\t"
-                    "s_add_u32 %[q], %[q], -1\n\t"
-                    "s_and_b32 %[t], %[q], 15\n\t"
-                    "s_cbranch_scc1 Lbn%=\n\t"
-                    "s_cmp_lt_u32 %[q], %[qin]\n\t"
-                    "s_cbranch_scc0 Lbn%=\n\t"
-                    "s_lshr_b32 %[t], %[q], 2\n\t"
-                    "s_and_b32 %[t], %[t], -4\n\t"
-                    "s_waitcnt expcnt(0)\n\t"
-                    "v_mov_b32 %[vo], %[t]\n\t"
-                    "v_mov_b32 %[vd], %[acc]\n\t"
-                    "global_store_dword %[vo], %[vd], %[out]\n"
-                    "Lbn%=:\n\t"
-                    "s_and_b32 %[t2], %[B], %[rmask]\n\t"
-                    "s_lshl_b32 %[t], %[op], 3\n\t"
-                    "s_lshr_b32 %[t], %[moves], %[t]\n\t"
-                    "s_and_b32 %[t], %[t], 0xff\n\t"
-                    "s_sub_u32 %[B], %[B], %[t]\n\t"
-                    "s_cmp_lg_u32 %[t2], 0\n\t"
-                    "s_cbranch_scc1 Lbl%=\n\t"
-                    "s_cmp_eq_u32 %[op], 0\n\t"
-                    "s_cbranch_scc1 Lbl%=\n\t"
-                    "s_sub_u32 %[LP], %[LP], 1\n\t"
-                    "s_cmp_lt_i32 %[LP], %[pl]\n\t"
-                    "s_cbranch_scc1 Lba%=\n\t"
-                    "s_sub_u32 %[t], %[LP], %[pl]\n\t"
-                    "s_lshr_b32 %[t2], %[t], %[llpb]\n\t"
-                    "s_sub_u32 %[t2], %[t], %[t2]\n\t"
-                    "s_sub_u32 %[t], %[t], %[J0m1]\n\t"
-                    "s_max_i32 %[t], %[t], %[t2]\n\t"
-                    "s_lshl_b32 %[lim], %[t], %[lrt]\n\t"
-                    "s_max_i32 %[lo], %[lim], %[w32]\n\t"
-                    "s_branch Lbl%=\n"
-                    "Lba%=:\n\t"
-                    "s_mov_b32 %[ab], 1\n"
-                    "Lbx%=:"
-                    : [B] "+s"(B), [LP] "+s"(LP), [q] "+s"(sq), [acc] "+s"(sacc), [lo] "+s"(lo), [lim] "+s"(lim),
-                      [op] "=&s"(op), [t] "=&s"(t), [t2] "=&s"(t2), [ab] "+s"(ab), [vo] "=&v"(vo), [vd] "=&v"(vd)
-                    : [cw] "v"(CW[w]), [qin] "s"(qin), [pl] "s"(pl), [J0m1] "s"(sJ0 - 1), [w32] "s"(32 * w),
-                      [out] "s"(sout), [rmask] "i"(2 * RT - 2), [moves] "s"(C::MOVES), [llpb] "i"(C::LLPB),
-                      [lrt] "i"(RT == 4 ? 3 : 2)
-                    : "scc", "memory");
-                (void)op;
-                (void)t;
-                (void)t2;
-                (void)vo;
-                (void)vd;
-                if (ab) above = true;
-                if (above || B < lim) stop = true;
-            }
-            const int rt = above ? -1 : RT * (LP - pl) + ((B >> 1) & (RT - 1));
-            const int sg = B >> (RT == 4 ? 3 : 2);  // (floor: B < 0 above the tile's first columns)
-            const int Lx = above ? -1 : LP - pl;
-            int serr = sq > qin ? SED_ERR_TB_LENGTH : 0;
-            const int si = srb + rt + 1, sj = sJ0 + sg - Lx;
-            if (!serr && sq == qin) serr = SED_ERR_TB_STALL;
-            if (!serr && si >= 1 && sj >= 1) {  // the exit cell's L must be the ops still to emit
-                uint32_t key = 0u;
-                bool chk = false;
-                if (rt < 0) {
-                    const int x = sj - sJ0;
-                    if (x >= 0 && x < C::STEPS) {
-                        key = ltop[p][x];
-                        chk = true;
-                    }
-                } else if (sj == sJ0 - (Lx >> C::LLPB) - 1) {  // left through the band's checkpoint column
-                    const int rr = rt & (RT - 1);
-                    uint32_t vr = VI[0];
-#pragma unroll
-                    for (int r = 1; r < RT; ++r) vr = rr == r ? VI[r] : vr;
-                    key = (uint32_t)__builtin_amdgcn_readlane((int)vr, pl + Lx);
-                    chk = true;
-                }
-                if (chk && (uint32_t)i32_decode<RT, true>(key, si, sj, prm).y != sq) serr = SED_ERR_TB_CHECK;
-            }
-            const int sguard = __builtin_amdgcn_readlane(guard, pl) - 1;
-            if (!serr && sguard <= 0) serr = SED_ERR_TB_GUARD;
-            if (slot == p) {
-                i = si;
-                j = sj;
-                q = sq;
-                acc = sacc;
-                err = serr;
-                guard = sguard;
-            }
-        }
-        __syncthreads();  // (the LDS tiles are rewritten by the next visit)
-    }
-    if (L == 0 && live) {
-        if (!err) {  // the border: inserts along row 0, deletes along column 0
-            while (j > 0 || i > 0) {
-                if (q == 0u) {
-                    err = SED_ERR_TB_LENGTH;
-                    break;
-                }
-                const uint32_t op = j > 0 ? 0u : 1u;
-                acc = (acc << 2) | op;
-                if ((--q & 15u) == 0u) out[q >> 4] = acc;
-                if (op == 0u) --j;
-                else --i;
-            }
-            if (!err && q != 0u) err = SED_ERR_TB_LENGTH;
-        }
-        if (err) res[pair].err = (uint8_t)err;
-    }
-}
-
 // SPLIT batches with checkpoints (config 2, GUI pairs; sed_runtime.cpp: split_ck).  The SPLIT forward kernel runs the
 // distance (or dot) keys, 2-3 VALU per cell instead of the ladder keys' 5.2, and stores checkpoints after the pair's
 // per-cell code region; this kernel then recomputes every 64 x 64 tile from them at once (one wave per tile, the
@@ -3054,18 +2680,6 @@ hipError_t sed_launch_ck_codes(const sed_launch &L, int max_tiles, const sed_i32
 hipError_t sed_launch_traceback_ck(const sed_launch &L, uint32_t *ops, const sed_i32_params &prm) {
     const dim3 grid(L.npairs), block(64);
     const uint32_t *a = (const uint32_t *)L.seqa, *b = (const uint32_t *)L.seqb;
-    // SED_CK_TB (A/B): 0 = the lane-per-row sweep (sed_traceback_ck_kernel), 2 / 4 = band slices of 2 / 4 rows per lane
-    // (sed_traceback_ckb_kernel, R = 16 only; slower, profiles/r05/s9); unset: 0
-    static const int ckb_env = [] { const char *e = getenv("SED_CK_TB"); return e ? atoi(e) : 0; }();
-    if (L.R == 16 && (ckb_env == 2 || ckb_env == 4)) {
-        if (ckb_env == 2)
-            SED_LAUNCH(sed_traceback_ckb_kernel<2>, dim3((L.npairs + 1) / 2), block, 0, L, L.pd, L.npairs, a, b, L.tb,
-                       L.res, ops, prm);
-        else
-            SED_LAUNCH(sed_traceback_ckb_kernel<4>, dim3((L.npairs + 3) / 4), block, 0, L, L.pd, L.npairs, a, b, L.tb,
-                       L.res, ops, prm);
-        return hipGetLastError();
-    }
     switch (L.R) {
     case 4: SED_LAUNCH(sed_traceback_ck_kernel<4>, grid, block, 0, L, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
     case 8: SED_LAUNCH(sed_traceback_ck_kernel<8>, grid, block, 0, L, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
