@@ -628,8 +628,11 @@ def load_es(path):
 def batch_plan(strs1, strs2, userCosts=False):
     """The reference's KeyError for the first offending pair, if any (sedcost.check_batch), then the batch's plan."""
     table = _table(userCosts)
-    sedcost.check_batch(table, strs1, strs2)
-    return sedcost.build_plan(table, strs1, strs2)
+    u = None  # the batch's symbols, once for both steps
+    if sedcost._all_str(strs1) and sedcost._all_str(strs2):
+        u = (sedcost.distinct_many(strs1), sedcost.distinct_many(strs2))
+    sedcost.check_batch(table, strs1, strs2, u)
+    return sedcost.build_plan(table, strs1, strs2, u)
 
 
 def _packed(plan, strs1, strs2):

@@ -233,3 +233,27 @@ def test_batch_plan_and_packing_match_per_string(tables):
     for f in ("codes_a", "codes_b", "len_a", "len_b", "off_a", "off_b", "ops_off"):
         assert np.array_equal(getattr(p1, f), getattr(p0, f)), f
     assert p1.npairs == p0.npairs == 50
+
+
+def test_distinct_first_occurrence_order():
+    """sedcost.distinct (the delete-pass scan with the remembered alphabet, a histogram past 16 new symbols) equals
+    dict.fromkeys on random strings over small, IUPAC-sized and large byte alphabets, non-latin text and empty
+    strings, in any order of calls (the remembered symbols change between them)."""
+    import random
+    rnd = random.Random(11)
+    pools = ["ACGU", "ACGUN", "ACGUYRWSKMDVHBNX", "".join(chr(i) for i in range(1, 256)), "aé€Ω", "\x00A"]
+    for _ in range(4000):
+        pool = rnd.choice(pools)
+        s = "".join(rnd.choice(pool) for _ in range(rnd.randint(0, 80)))
+        assert sedcost.distinct(s) == list(dict.fromkeys(s)), s
+        assert sedcost.distinct_many([s, s[::-1], ""]) == list(dict.fromkeys(s + s[::-1])), s
+    assert sedcost.distinct(list("ACCA")) == ["A", "C"]
+
+
+def test_encode_many_repeated_query(tables):
+    """The one-query-many-documents fast path of encode_many (codes tiled once) equals per-string encoding."""
+    plan = sedcost.build_plan(tables[False], ["ACGUN"], ["ACGU"])
+    for strs in (["ACGUNNA"] * 7, ["A"] * 2, ["ACG", "ACG", "AC"], [""] * 3):
+        codes, lens = plan.encode_many(strs)
+        want = np.concatenate([plan.encode(s) for s in strs]) if strs else np.zeros(0, np.uint8)
+        assert np.array_equal(codes, want) and lens.tolist() == [len(s) for s in strs], strs
