@@ -2389,8 +2389,12 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
 #endif
 }
 
+// waves per SIMD the checkpoint traceback is compiled for (A/B: SED_CKTB_WAVES; 1 = the compiler's choice)
+#ifndef SED_CKTB_WAVES
+#define SED_CKTB_WAVES 1
+#endif
 template <int R>
-__global__ __launch_bounds__(64) void sed_traceback_ck_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SED_CKTB_WAVES))) void sed_traceback_ck_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
                                                               const uint32_t *__restrict__ seqa,
                                                               const uint32_t *__restrict__ seqb,
                                                               const uint32_t *__restrict__ ck,
