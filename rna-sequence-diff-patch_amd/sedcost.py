@@ -12,6 +12,8 @@ and raises the same KeyError the reference would raise at the first offending
 cell in row-major order (insert / delete keys first, as the border loops read
 them before any update lookup, StringEditDistance.py:156,174).
 """
+import operator
+
 import numpy as np
 
 UPDATE, INSERT, DELETE = "update", "insert", "delete"
@@ -219,33 +221,49 @@ def _batch_resolves(table, strs1, strs2, u=None):
 
 
 _PLANS = {}  # pair_plan's cache: resolved costs -> CostPlan
+_GETTERS = {}  # (sorted str1 symbols, sorted str2 symbols) -> [(str1 symbol, itemgetter of the str2 symbols it is
+#               compared with, their count)] for the rows with at least one such symbol
+
+
+def _row_getters(u1, u2):
+    g = _GETTERS.get((u1, u2))
+    if g is None:
+        g = []
+        for a in u1:
+            la = a.lower()
+            keys = [b for b in u2 if la != b.lower()]
+            if keys:
+                g.append((a, operator.itemgetter(*keys), len(keys)))
+        if len(_GETTERS) > 4096:
+            _GETTERS.clear()
+        _GETTERS[(u1, u2)] = g
+    return g
 
 
 def pair_plan(table, s1, s2):
     """check_pair(table, s1, s2) then build_plan(table, [s1], [s2]) for one pair of non-empty strs, with the plan
     cached by the costs the pair resolves to.  The table is read on every call (the GUI edits user_costs in place,
-    gui.py:193-252), and any lookup that fails goes through check_pair, which raises the reference's exception."""
-    d1 = dict.fromkeys(s1 if len(s1) <= 256 else distinct(s1))
-    d2 = dict.fromkeys(s2 if len(s2) <= 256 else distinct(s2))
+    gui.py:193-252), and any lookup that fails goes through check_pair, which raises the reference's exception.
+    The key takes the symbol sets in sorted order: two pairs over the same symbols share one plan whatever order
+    the symbols first occur in (timing.py's random IUPAC pairs, wf_score's documents), so set_costs is skipped and
+    no plan is rebuilt.  A plan's alphabet order is that of the first pair it was built for; codes go through
+    plan.code, so any order encodes any pair over the same sets."""
+    u1 = tuple(sorted(set(s1) if len(s1) <= 256 else distinct(s1)))
+    u2 = tuple(sorted(set(s2) if len(s2) <= 256 else distinct(s2)))
     try:
         ins, dele = table[INSERT], table[DELETE]
         vals = []
-        upd = None
-        for a in d1:
-            la = a.lower()
-            row = None
-            for b in d2:
-                if la != b.lower():
-                    if row is None:
-                        if upd is None:
-                            upd = table[UPDATE]
-                        row = upd[a]
-                    vals.append(row[b])
+        rows = _row_getters(u1, u2)
+        if rows:
+            upd = table[UPDATE]
+            for a, g, cnt in rows:
+                v = g(upd[a])
+                vals.append(v if cnt > 1 else (v,))
     except (KeyError, TypeError, IndexError, AttributeError):
         check_pair(table, s1, s2)  # the reference's exception, if any
         return build_plan(table, [s1], [s2])
-    # (the symbols of both strings in first-occurrence order fix the alphabet and which combinations are resolved)
-    key = (tuple(d1), tuple(d2), tuple(vals), tuple(type(v) for v in vals), ins, type(ins), dele, type(dele))
+    vals = tuple(vals)
+    key = (u1, u2, vals, tuple(tuple(map(type, v)) for v in vals), ins, type(ins), dele, type(dele))
     try:
         plan = _PLANS.get(key)
     except TypeError:  # unhashable cost values
