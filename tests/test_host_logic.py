@@ -257,3 +257,31 @@ def test_encode_many_repeated_query(tables):
         codes, lens = plan.encode_many(strs)
         want = np.concatenate([plan.encode(s) for s in strs]) if strs else np.zeros(0, np.uint8)
         assert np.array_equal(codes, want) and lens.tolist() == [len(s) for s in strs], strs
+
+
+def test_pair_plan_shared_by_symbol_sets_and_fresh_after_edits(tables):
+    """pair_plan caches one plan per (str1 symbols, str2 symbols, resolved costs): pairs over the same symbols in any
+    order share it; editing the table in place (the GUI's cost editors), including an int/float change of one
+    value, gives a new plan with the new value; a missing entry raises the reference's KeyError."""
+    import copy
+    t = copy.deepcopy(tables[True])
+    p1 = sedcost.pair_plan(t, "ACGU", "UGCA")
+    p2 = sedcost.pair_plan(t, "UUGCAA", "CAGU")
+    assert p1 is p2
+    for s1, s2 in (("ACGU", "UGCA"), ("UUGCAA", "CAGU")):
+        want = sedcost.build_plan(t, [s1], [s2])
+        for a in set(s1):
+            for b in set(s2):
+                assert p2.sub[p2.code[a], p2.code[b]] == want.sub[want.code[a], want.code[b]]
+    old = t["update"]["A"]["C"]
+    t["update"]["A"]["C"] = float(old) + 0.5
+    p3 = sedcost.pair_plan(t, "CAGU", "GUCA")
+    assert p3 is not p1 and p3.sub[p3.code["A"], p3.code["C"]] == float(old) + 0.5
+    t["update"]["A"]["C"] = int(old) if float(old).is_integer() else old
+    t["update"]["A"]["C"] = float(t["update"]["A"]["C"])
+    t["update"]["A"]["G"] = int(t["update"]["A"]["G"])
+    p4 = sedcost.pair_plan(t, "ACGU", "UGCA")
+    assert p4.sub_int[p4.code["A"], p4.code["G"]] == 1
+    del t["update"]["G"]["U"]
+    with pytest.raises(KeyError):
+        sedcost.pair_plan(t, "GA", "AU")
