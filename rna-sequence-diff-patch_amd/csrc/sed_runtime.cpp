@@ -672,11 +672,12 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     }
     b->ck = want_tb && mode == SED_MODE_I32 && !split && (R == 4 || R == 8 || R == 16) && c->opt_tb != 1 &&
             (c->opt_tb == 2 || (npairs > 256 && sum_nm >= 512.0 * sum_len));
-    // SED_PIPELINE is a hint: checkpoint batches run their traceback after the DP on one stream.  Both
-    // kernels are issue-bound, so overlap only adds contention (config 4: 20.33 ms sequential against
-    // 20.5-20.8 ms pipelined, profiles/r01_ck/ab_pipeline.jsonl) and saves two traceback buffers.
-    static const bool ck_pipe = [] { const char *e = getenv("SED_CK_PIPELINE"); return e && atoi(e) > 0; }();
-    if (b->ck && !ck_pipe) b->nbuf = 1;
+    // SED_PIPELINE is a hint: checkpoint batches run their traceback after the DP on one stream (in parts on
+    // several, run_batch_parts).  Both kernels are issue-bound, so overlapping a run's traceback with the next run's
+    // forward only adds contention (config 4: 20.33 ms sequential against 20.5-20.8 ms pipelined in round 1,
+    // profiles/r01_ck/ab_pipeline.jsonl; 11.13 against 9.78 ms for 2 pipelined parts in round 5,
+    // profiles/r05/s14/ab.jsonl) and saves two checkpoint buffers.
+    if (b->ck) b->nbuf = 1;
     // few pairs with per-cell codes (config 2, the GUI): the traceback walks the stripes of a pair in parallel
     // (a map of every stripe's exits, then one wave per stripe segment) instead of one ~n+m step chain;
     // SED_TBPAR=0/1 overrides (A/B)
