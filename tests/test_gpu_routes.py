@@ -196,7 +196,7 @@ def test_checkpoint_default_route_with_lane_pairs_and_pipeline(gpu, tables):
     _check_all(plan, packed, d, ii, ln, ops)
     b, (d2, ii2, ln2, ops2) = _batch_run(gpu, packed, True, pipeline=True, runs=3)
     b.close()
-    assert np.array_equal(d2, d) and np.array_equal(ln2, ln) and np.array_equal(ops2, ops)
+    _same((d2, ii2, ln2, ops2), (d, ii, ln, ops), packed.ops_off)
 
 
 @pytest.mark.parametrize("user", [False, True])
@@ -230,7 +230,7 @@ def test_checkpoint_dot_keys_route(gpu, tables, user):
                     b.close()
             finally:
                 gpu.set_option(sedgpu.SED_OPT_DOT, 0)
-            assert np.array_equal(d2, d) and np.array_equal(ln2, ln) and np.array_equal(ops2, ops)
+            _same((d2, ii2, ln2, ops2), (d, ii, ln, ops), packed.ops_off)
     finally:
         gpu.set_option(sedgpu.SED_OPT_TB, 0)
         gpu.set_option(sedgpu.SED_OPT_CHAIN, 0)
@@ -391,7 +391,7 @@ def test_repeated_runs_reuse_the_context(gpu, tables):
     first = gpu.run(packed, True)
     for _ in range(300):
         d, ii, ln, ops = gpu.run(packed, True)
-    assert np.array_equal(d, first[0]) and np.array_equal(ops, first[3])
+    _same((d, ii, ln, ops), first, packed.ops_off)
 
 
 @pytest.mark.parametrize("R,split", [(4, 0), (4, 2), (8, 2), (16, 2)])
@@ -528,7 +528,7 @@ def test_dot_keys_on_random_factorable_tables(gpu):
                 assert not b.dot_keys and not b.ladder_dot_keys
             finally:
                 b.close()
-            assert np.array_equal(d2, d) and np.array_equal(ln2, ln) and np.array_equal(ops2, ops)
+            _same((d2, ii2, ln2, ops2), (d, ii, ln, ops), packed.ops_off)
         finally:
             for k in list(opts) + [sedgpu.SED_OPT_DOT]:
                 gpu.set_option(k, 0)
