@@ -80,11 +80,34 @@ def batched_search(query, vector_type, collection, method, return_dict=None, sta
         wfsearch.clear_cache()
         wfsearch.search_collection(query, vector_type, collection, wfsearch.wf_score)
         stamps["second_ms"] = (time.perf_counter() - t2) * 1e3
+        stamps["phases"] = search_phases(query, collection)
         c = sedgpu.context()
         stamps["engine"] = (getattr(c, "served_by", None) or type(c).__name__) + ", batched"
     if return_dict is not None:
         return_dict["wf_score"] = scores
     return scores
+
+
+def search_phases(query, collection, reps=5):
+    """The batched search's phases, warm, in ms: the batch's cost plan, the packed codes, and the engine call (in a
+    forked child: one request to the parent's serving thread)."""
+    seqs = [doc['sequence'] for doc in collection.find({})]
+    queries = [query] * len(seqs)
+    acc = [0.0, 0.0, 0.0]
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        plan = SED.batch_plan(queries, seqs, False)
+        t1 = time.perf_counter()
+        packed = SED._packed(plan, queries, seqs)
+        t2 = time.perf_counter()
+        ctx = sedgpu.context()
+        ctx.set_costs(plan)
+        ctx.run(packed, False, no_len=True)
+        t3 = time.perf_counter()
+        acc[0] += t1 - t0
+        acc[1] += t2 - t1
+        acc[2] += t3 - t2
+    return {k: v * 1e3 / reps for k, v in zip(("plan_ms", "pack_ms", "run_ms"), acc)}
 
 
 def collection():
@@ -127,17 +150,21 @@ def process_model(out):
         got = wfsearch.search_collection(query, "tf", coll, wfsearch.wf_score)
     batch_ms = (time.perf_counter() - t0) * 1e3 / reps
     assert got == want
+    phases = search_phases(query, coll)
     out["process_model"] = {
         "docs": NDOCS, "doc_lengths": "U[24,32] synthetic ACGU", "costs": "costs.json",
         "rounds": rounds, "inproc_per_doc_loop_ms": loop_ms, "inproc_wfsearch_batched_ms": batch_ms,
+        "inproc_phases": phases,
         "fork_engine": os.environ.get("SED_FORK_ENGINE", "parent"),
     }
     for k, r in enumerate(rounds):
         print("forked search round %d (%s): wall %.1f ms, child started at %.2f ms, first result %.2f ms, loop "
               "%.2f ms, then %.4f ms per document" % (k, r["engine"], r["wall_ms"], r["start_ms"], r["first_ms"],
                                                      r["loop_ms"], r["rest_per_call_ms"])
-              + ("; again in the child %.2f ms" % r["second_ms"] if "second_ms" in r else ""))
-    print("in-process: per-document loop %.2f ms, wfsearch batched %.3f ms" % (loop_ms, batch_ms))
+              + ("; again in the child %.2f ms" % r["second_ms"] if "second_ms" in r else "")
+              + ("; phases %s" % {k: round(v, 3) for k, v in r["phases"].items()} if "phases" in r else ""))
+    print("in-process: per-document loop %.2f ms, wfsearch batched %.3f ms; phases %s"
+          % (loop_ms, batch_ms, {k: round(v, 3) for k, v in phases.items()}))
 
 
 def timing_loop(out):

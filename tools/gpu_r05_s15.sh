@@ -13,3 +13,5 @@ bash tools/ab_env.sh ${1:-r05s15} 3 "-" "$P1" "$P3"
 cat $O/ab.jsonl
 env $P3 timeout -k 10 200 python3 tools/c4_timeline.py 10 > $O/timeline_p3.txt 2>&1
 head -8 $O/timeline_p3.txt
+timeout -k 10 300 python3 tools/caller_paths.py $O/caller_paths.json > $O/caller_paths.txt 2>&1
+cat $O/caller_paths.txt
