@@ -1567,6 +1567,11 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
 // ---------------------------------------------------------------------------
 // SW = 16: the fp64 kernel's segment pairs (idx[0 .. npairs)), whose codes have the stripe layout of 16 lanes; SW = 64
 // skips them (d.pad[1]).
+// issue priority of the per-cell-code traceback's waves (A/B: SED_TB_PRIO, s_setprio): pipelined batches run the
+// traceback of run k beside the DP of run k+1
+#ifndef SED_TB_PRIO
+#define SED_TB_PRIO 0
+#endif
 template <int R, int SW = 64>
 __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
                                                            const uint32_t *__restrict__ tb,
@@ -1574,6 +1579,7 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
                                                            uint32_t *__restrict__ ops, const uint64_t pat,
                                                            const int32_t *__restrict__ idx) {
     constexpr int G = Grp<R>::G, P = Ladder<R>::P;
+    if constexpr (SED_TB_PRIO > 0) __builtin_amdgcn_s_setprio(SED_TB_PRIO);
     const int item = blockIdx.x * blockDim.x + threadIdx.x;
     if (item >= npairs) return;
     const int pair = SW == 64 ? item : idx[item];
@@ -2389,9 +2395,16 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
 #endif
 }
 
-// waves per SIMD the checkpoint traceback is compiled for (A/B: SED_CKTB_WAVES; 1 = the compiler's choice)
+// waves per SIMD the checkpoint traceback is compiled for (A/B: SED_CKTB_WAVES; 1 = the compiler's choice), and its
+// waves' issue priority against the other part's forward waves on the same SIMD (SED_CKTB_PRIO, s_setprio).  At
+// priority 1 the traceback's waves issue ahead of the forward's when both are ready, so a part's traceback ends
+// sooner beside the other part's forward and the step's tracebacks-only tail shrinks from ~0.5 to ~0.13 ms: c4
+// 9.74-9.79 against 9.91-9.98 ms at 0, 3 interleaved rounds (profiles/r05/s15; 3 is no different from 1)
 #ifndef SED_CKTB_WAVES
 #define SED_CKTB_WAVES 1
+#endif
+#ifndef SED_CKTB_PRIO
+#define SED_CKTB_PRIO 1
 #endif
 template <int R>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SED_CKTB_WAVES))) void sed_traceback_ck_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
@@ -2400,6 +2413,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SED_CKTB_WAV
                                                               const uint32_t *__restrict__ ck,
                                                               sed_result *__restrict__ res,
                                                               uint32_t *__restrict__ ops, sed_i32_params prm) {
+    if constexpr (SED_CKTB_PRIO > 0) __builtin_amdgcn_s_setprio(SED_CKTB_PRIO);
     const int lane = threadIdx.x;
     const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x);
     if (pair >= npairs) return;
