@@ -1567,10 +1567,12 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
 // ---------------------------------------------------------------------------
 // SW = 16: the fp64 kernel's segment pairs (idx[0 .. npairs)), whose codes have the stripe layout of 16 lanes; SW = 64
 // skips them (d.pad[1]).
-// issue priority of the per-cell-code traceback's waves (A/B: SED_TB_PRIO, s_setprio): pipelined batches run the
-// traceback of run k beside the DP of run k+1
+// issue priority of the per-cell-code traceback's waves on integer (ladder-code) batches (SED_TB_PRIO, s_setprio):
+// pipelined batches run the traceback of run k beside the DP of run k+1, and at priority 1 it no longer trails it.
+// Config 3 (CHAIN): 2.50-2.51 against 2.62-2.72 ms per step at 10 steps, traceback span 0.71 against 1.85-1.95 ms;
+// the fp64 workloads (pat = 0) stay at priority 0: iupac 4.89-4.90 against 4.83-4.89 ms (profiles/r05/s16)
 #ifndef SED_TB_PRIO
-#define SED_TB_PRIO 0
+#define SED_TB_PRIO 1
 #endif
 template <int R, int SW = 64>
 __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
@@ -1579,7 +1581,7 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
                                                            uint32_t *__restrict__ ops, const uint64_t pat,
                                                            const int32_t *__restrict__ idx) {
     constexpr int G = Grp<R>::G, P = Ladder<R>::P;
-    if constexpr (SED_TB_PRIO > 0) __builtin_amdgcn_s_setprio(SED_TB_PRIO);
+    if (SED_TB_PRIO > 0 && pat != 0) __builtin_amdgcn_s_setprio(SED_TB_PRIO);
     const int item = blockIdx.x * blockDim.x + threadIdx.x;
     if (item >= npairs) return;
     const int pair = SW == 64 ? item : idx[item];
