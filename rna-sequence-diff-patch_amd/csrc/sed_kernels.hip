@@ -1569,8 +1569,9 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
 // skips them (d.pad[1]).
 // issue priority of the per-cell-code traceback's waves on integer (ladder-code) batches (SED_TB_PRIO, s_setprio):
 // pipelined batches run the traceback of run k beside the DP of run k+1, and at priority 1 it no longer trails it.
-// Config 3 (CHAIN): 2.50-2.51 against 2.62-2.72 ms per step at 10 steps, traceback span 0.71 against 1.85-1.95 ms;
-// the fp64 workloads (pat = 0) stay at priority 0: iupac 4.89-4.90 against 4.83-4.89 ms (profiles/r05/s16)
+// Config 3 (CHAIN): 2.50-2.51 against 2.62-2.72 ms per step at 10 steps (traceback span 0.71 against 1.85-1.95 ms),
+// the last run's unoverlapped traceback; 2.38 ms at 20 steps either way.  The fp64 workloads (pat = 0) stay at
+// priority 0: iupac 4.89-4.90 against 4.83-4.89 ms (profiles/r05/s16)
 #ifndef SED_TB_PRIO
 #define SED_TB_PRIO 1
 #endif
