@@ -536,6 +536,12 @@ __device__ __forceinline__ void split_feed(const uint64_t *__restrict__ bin64, c
 // (D, L), which is all the checkpoints need; the traceback recomputes the op tie-break.
 // The CK kernel (distance keys, no codes) would fit 80 VGPRs (6 waves per SIMD, spills per chunk only) but
 // ran slower: 12.45 against 12.11 ms at 5 waves (profiles/r02/ab_ck_waves.txt).
+// issue priority of SPLIT's stripe waves (SED_SPLIT_PRIO): a single pair's stripe chain is latency-bound, and the
+// previous run's traceback kernels may share its SIMDs.  Config 2 at 100 steps: 0.2974-0.3008 against 0.2984-0.3039
+// ms per step at 0, 3 interleaved rounds (profiles/r05/s17)
+#ifndef SED_SPLIT_PRIO
+#define SED_SPLIT_PRIO 2
+#endif
 template <int R, bool TB, bool SPLIT, bool LEN = true, bool CK = false, bool DOT = false>
 __global__ __launch_bounds__(SPLIT ? 128 : 256) __attribute__((amdgpu_waves_per_eu(CK ? SED_CK_WAVES : SED_I32_WAVES(R))))
 void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const int2 *__restrict__ tasks,
@@ -547,6 +553,7 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
     static_assert(!CK || (R <= 16 && !TB && !LEN), "checkpoints: R <= 16, distance keys");
     static_assert(!(CK && SPLIT) || R == 4, "SPLIT checkpoints (sed_ck_codes_kernel): R = 4");
     static_assert(!DOT || CK, "dot keys: checkpoint batches only");
+    if constexpr (SPLIT && SED_SPLIT_PRIO > 0) __builtin_amdgcn_s_setprio(SED_SPLIT_PRIO);
     const int lane = threadIdx.x & 63;
     int pair, kfirst = 0;
     if constexpr (SPLIT) {
@@ -1369,6 +1376,12 @@ struct f64_chunk_lds {
 // host sorts them so a wave's four pairs have similar shapes): stripes of 16 R rows, 16-step chunks, a 15-step ramp
 // instead of 63, and every lane move a row DPP (seg_*), so the four segments never exchange data.  The loop bounds
 // are then per lane (uniform within a segment), and a segment whose pair is done sits out with its lanes masked.
+// issue priority of the fp64 DP's waves (SED_F64_PRIO): pipelined fp64 script batches run the traceback of run k
+// beside the DP of run k+1, which now issues first.  iupac 4.83-4.85 against 4.87-4.89 ms per step at 0, timing within
+// noise, 3 interleaved rounds (profiles/r05/s17)
+#ifndef SED_F64_PRIO
+#define SED_F64_PRIO 1
+#endif
 template <int R, bool TB, bool TYPED, bool FULL, int SW = 64>
 __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
                                                          const uint8_t *__restrict__ seqa,
@@ -1377,6 +1390,7 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
                                                          sed_result *__restrict__ res,
                                                          const double *__restrict__ gtab, sed_f64_params prm,
                                                          sed_full_out fo, const int32_t *__restrict__ idx) {
+    if constexpr (SED_F64_PRIO > 0) __builtin_amdgcn_s_setprio(SED_F64_PRIO);
     static_assert(SW == 64 || (SW == 16 && !FULL), "segments of 16 lanes: no full-matrix output");
     constexpr int ROWS = SW * R;
     constexpr int G = Grp<R>::G;
