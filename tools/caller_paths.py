@@ -81,6 +81,20 @@ def batched_search(query, vector_type, collection, method, return_dict=None, sta
         wfsearch.search_collection(query, vector_type, collection, wfsearch.wf_score)
         stamps["second_ms"] = (time.perf_counter() - t2) * 1e3
         stamps["phases"] = search_phases(query, collection)
+        prof = os.environ.get("CALLER_PATHS_PROFILE")  # a file: cProfile of one more search in this child
+        if prof:
+            import cProfile
+            import io
+            import pstats
+            pr = cProfile.Profile()
+            wfsearch.clear_cache()
+            pr.enable()
+            wfsearch.search_collection(query, vector_type, collection, wfsearch.wf_score)
+            pr.disable()
+            out = io.StringIO()
+            pstats.Stats(pr, stream=out).sort_stats("cumulative").print_stats(25)
+            with open(prof, "a") as f:
+                f.write(out.getvalue())
         c = sedgpu.context()
         stamps["engine"] = (getattr(c, "served_by", None) or type(c).__name__) + ", batched"
     if return_dict is not None:
