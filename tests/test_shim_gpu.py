@@ -212,7 +212,8 @@ def _ref_search_collection(query, vector_type, collection, method, return_dict=N
 def test_create_search_threads_process_model(SED):
     """gui.py:360 runs wagnerFisher in the GUI process (HIP initialised there), then
     IRMethods.create_search_threads forks a Process per method and another for wf_score, delivering through
-    Manager dicts (IRMethods.py:480-515).  The forked children get an engine worker; results match G7."""
+    Manager dicts (IRMethods.py:480-515).  The forked children are served by a thread of this process over a socket
+    pair made at fork time (sedgpu._before_fork); results match G7."""
     import multiprocessing as mp
     import seqio
     import sedgpu
@@ -242,6 +243,48 @@ def test_create_search_threads_process_model(SED):
     manager.shutdown()
     dp = SED.wagnerFisher("ACGU", "AGU")  # the parent's own context still works
     assert dp[len(dp) - 1][len(dp[0]) - 1].value == 1
+
+
+def _child_searches(query, coll, return_dict, key):
+    """A forked child: the reference's per-document search, then the batched one (wfsearch), both delivered."""
+    import wfsearch
+    per_doc = _ref_search_collection(query, "tf", coll, wfsearch.wf_score)
+    wfsearch.clear_cache()
+    batched = wfsearch.search_collection(query, "tf", coll, wfsearch.wf_score)
+    return_dict[key] = (per_doc, batched)
+
+
+def test_concurrent_forked_children_served_by_the_parent(SED):
+    """Four children forked at once from a HIP process (a multiprocessing pool's shape), each running the
+    per-document and the batched search, while the parent keeps calling wagnerFisher on its own context: the
+    parent serves them on as many threads and pooled contexts at the same time.  Every child's results match G7,
+    and so do the parent's."""
+    import multiprocessing as mp
+    import seqio
+    import sedgpu
+    g7 = load_golden("g7_ingest_search.json")
+    coll = seqio.ListCollection.from_sequences(list(g7["test_input"].values()))
+    SED.wagnerFisher("AGRGA", "AGGGAA", True)
+    assert isinstance(sedgpu.context(), sedgpu.Context)
+    fork = mp.get_context("fork")
+    manager = fork.Manager()
+    out = manager.dict()
+    searches = g7["searches"][:4]
+    jobs = [fork.Process(target=_child_searches, args=(s["query"], coll, out, k)) for k, s in enumerate(searches)]
+    for p in jobs:
+        p.start()
+    for _ in range(50):  # the parent's own calls while the children are served
+        dp = SED.wagnerFisher("ACGU", "AGU")
+        assert dp[len(dp) - 1][len(dp[0]) - 1].value == 1
+    for p in jobs:
+        p.join(timeout=180)
+        assert p.exitcode == 0
+    for k, s in enumerate(searches):
+        want = [[seq, float.fromhex(h)] for seq, h in s["scores"]]
+        per_doc, batched = out[k]
+        assert [[a, b] for a, b in per_doc] == want, k
+        assert [[a, b] for a, b in batched] == want, k
+    manager.shutdown()
 
 
 def test_import_time_demo_globals(SED):
