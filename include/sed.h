@@ -158,6 +158,7 @@ int sed_batch_packed_pairs(const sed_batch *b);       /* pairs computed two per 
 int sed_batch_bitpar_pairs(const sed_batch *b);       /* lane pairs computed bit-parallel (SED_OPT_BITPAR) */
 int sed_batch_scaled_pairs(const sed_batch *b);       /* fp64 lane pairs on the scaled-integer DP (SED_OPT_SCALED) */
 int sed_batch_segment_pairs(const sed_batch *b);      /* fp64 wave pairs run in 16-lane segments (SED_OPT_SEG) */
+int sed_batch_split_tasks(const sed_batch *b);        /* SPLIT: workgroups (pair, stripe) per run, 0 = not SPLIT */
 /* The byte factorisation behind SED_OPT_DOT, without a device (tests): for the 4 x 4 table sub (a -> b, row-major)
  * and insert/delete costs, the dot keys for pairs with min(n, m) <= maxmin (ladder_maxsum = 0) or the ladder dot
  * keys for n + m <= ladder_maxsum.  out[0..3] = row vectors, out[4..7] = column vectors (4 signed bytes each),

@@ -65,7 +65,7 @@ struct sed_f64_params {
     double ins, del;
     int32_t ins_int, del_int;
     int32_t K;
-    int32_t pad;
+    uint32_t epoch;  // SPLIT hand-off words' tag, as sed_i32_params::epoch (sed_kernels.hip: sed_wf_f64_split_kernel)
 };
 
 // Full-matrix output (dp proxy materialisation): D[i*(m+1)+j], M = edge mask (1 ins, 2 del, 4 upd) | int << 3.

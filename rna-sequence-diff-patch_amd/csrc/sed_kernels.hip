@@ -1282,7 +1282,9 @@ struct f64_cell_in {
     uint32_t t;
 };
 
-template <int R, bool TB, bool TYPED, bool MASKED, bool FULL, int SW = 64>
+// PF: the caller has moved this step's column symbol (bsel) and read its table entries (epf) a step ahead (the
+// SPLIT kernel's lone waves, whose LDS reads would otherwise stall every step)
+template <int R, bool TB, bool TYPED, bool MASKED, bool FULL, int SW = 64, bool PF = false>
 __device__ __forceinline__ void f64_step(double (&D)[R], uint32_t (&LK)[R], uint32_t (&T)[R],
                                          const uint32_t (&rowbase)[R], const double2 *__restrict__ tab,
                                          double &dtop_prev, uint32_t &ltop_prev, uint32_t &ttop_prev,
@@ -1291,19 +1293,19 @@ __device__ __forceinline__ void f64_step(double (&D)[R], uint32_t (&LK)[R], uint
                                          const uint32_t stin, uint32_t (&W)[4], const int u,
                                          const double cins, const double cdel, const uint32_t tins,
                                          const uint32_t tdel, const bool active, const sed_full_out &fo,
-                                         const int i0, const int j) {
+                                         const int i0, const int j, const double2 *epf = nullptr) {
     // the segment's first lane takes this step's top-row cell and column symbol (dtin .. stin, broadcast LDS reads of
     // the chunk), the others the lane above's bottom cell and previous symbol
     const double dtop = seg_shr1_f64<SW>(dtin, dbot);
     const uint32_t ltop = seg_shr1<SW>(ltin, lbot);
     uint32_t ttop = 0;
     if constexpr (TYPED) ttop = seg_shr1<SW>(ttin, tbot);
-    bsel = seg_shr1<SW>(stin, bsel);
+    if constexpr (!PF) bsel = seg_shr1<SW>(stin, bsel);
     double dup = dtop, ddiag = dtop_prev;
     uint32_t lup = ltop, ldiag = ltop_prev, tup = ttop, tdiag = ttop_prev;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const double2 e = tab[rowbase[r] + bsel];  // x = cost, y = int flag (as double bits)
+        const double2 e = PF ? epf[r] : tab[rowbase[r] + bsel];  // x = cost, y = int flag (as double bits)
         const double dl = D[r];
         const double ca = dl + cins;
         const double cb = dup + cdel;
@@ -1568,6 +1570,259 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
                 res[pair].is_int = TYPED ? (uint8_t)tv : (uint8_t)(dv == 0.0);
                 res[pair].err = 0;
             }
+        }
+    }
+}
+
+// SPLIT fp64 (few long pairs: timing.py's one-call loop, GUI calls over IUPAC symbols).  A lone fp64 wave issues
+// ~20 dependent VALU per cell on one SIMD (a 2000^2 pair took 3.5 ms), so, as in the integer SPLIT kernel, each
+// stripe of 64 R rows is a 128-thread workgroup of its own: all stripes of a pair run at once, each a group or two
+// behind the stripe above.  The hand-off is the integer kernel's tagged words: lane 63's bottom cell of column j
+// travels as three relaxed agent-scope 64-bit stores {tag, D low}, {tag, D high}, {tag, L key | T} (the L key is a
+// multiple of 4, so its bit 0 carries the typing bit), each single-copy atomic and validated on its own, tag = the
+// run's epoch | poison << 31.  The feeder wave (f64_split_feed) polls the stripe above's words, writes the steps'
+// top-row cells and str2 symbols into an LDS ring and publishes how many steps are ready; stripe 0's feeder writes
+// the row-0 border.  The compute wave is sed_wf_f64_kernel's stripe loop (SW = 64) reading the ring.  Codes, the
+// bottom-row-free layout and the result are the one-wave kernel's, so the tracebacks read them unchanged.
+#define SED_F64_RING 256
+struct f64_split_lds {
+    double d[SED_F64_RING];
+    uint32_t l[SED_F64_RING], t[SED_F64_RING], s[SED_F64_RING];
+    double od[16][64];  // every lane's bottom cell of the group's steps (lane 63's are handed off)
+    uint32_t ol[16][64], ot[16][64];
+};
+// the three hand-off planes of stripe k: words [plane][column + 64], (nchunks + 2) * 64 per plane
+__device__ __forceinline__ uint64_t *f64_split_words(uint32_t *bnd, const sed_pair_desc &d, int k, uint32_t plane_words) {
+    return reinterpret_cast<uint64_t *>(bnd + d.bnd_off) + (uint64_t)k * 3u * plane_words;
+}
+__device__ void f64_split_feed(const uint64_t *__restrict__ hin, const uint32_t plane_words, const bool top, const int m,
+                               const int SG, const uint32_t epoch, const uint8_t *__restrict__ pb, const double ins,
+                               const uint32_t tins, f64_split_lds &rg, uint32_t *flag, const int lane) {
+    uint32_t poison = 0, idle = 0;
+    int have = 0;  // steps whose top-row cells are in the ring
+    while (have < SG) {
+        if (have + 64 > (int)lds_flag_get(flag + 1) + SED_F64_RING) {  // ring full: the compute wave is behind
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        const int t = have + lane, col = t + 1;
+        const bool need = !top && t < SG && col <= m;  // columns past m are never stored nor waited for
+        uint64_t w0 = 0, w1 = 0, w2 = 0;
+        if (need) {
+            w0 = load_sc1_u64(hin + (uint32_t)(col + 64));
+            w1 = load_sc1_u64(hin + plane_words + (uint32_t)(col + 64));
+            w2 = load_sc1_u64(hin + 2u * plane_words + (uint32_t)(col + 64));
+        }
+        const uint32_t g0 = (uint32_t)(w0 >> 32), g1 = (uint32_t)(w1 >> 32), g2 = (uint32_t)(w2 >> 32);
+        const bool good = !need || (((g0 & ~SED_PROG_POISON) == epoch) && ((g1 & ~SED_PROG_POISON) == epoch) &&
+                                    ((g2 & ~SED_PROG_POISON) == epoch));
+        const uint64_t bad = __ballot(!good);
+        const int nv = min(bad ? (int)__builtin_ctzll(bad) : 64, SG - have);  // the valid prefix
+        if (__any(lane < nv && need && ((g0 | g1 | g2) & SED_PROG_POISON))) poison = SED_PROG_POISON;
+        if (nv > 0) {
+            if (lane < nv) {
+                const int slot = t & (SED_F64_RING - 1);
+                if (top) {  // row 0: D = j * insert, L key B, typing of insert
+                    rg.d[slot] = (double)col * ins;
+                    rg.l[slot] = SED_F64_LB;
+                    rg.t[slot] = tins;
+                } else {
+                    rg.d[slot] = __longlong_as_double((long long)(((w1 & 0xFFFFFFFFull) << 32) | (w0 & 0xFFFFFFFFull)));
+                    rg.l[slot] = (uint32_t)w2 & ~3u;
+                    rg.t[slot] = (uint32_t)w2 & 1u;
+                }
+                rg.s[slot] = t < m ? (uint32_t)pb[t] : 0u;
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the values before the count
+            have += nv;
+            idle = 0;
+        } else if (++idle > (1u << 22)) {  // the stripe above stopped: give up, let the compute wave drain
+            poison = SED_PROG_POISON;
+            have = SG;
+        } else {
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (lane == 0 && (nv > 0 || poison)) lds_flag_set(flag, (uint32_t)have | poison);
+    }
+}
+
+template <int R, bool TB, bool TYPED, bool FULL>
+__global__ __launch_bounds__(128) void sed_wf_f64_split_kernel(const sed_pair_desc *__restrict__ pd,
+                                                               const int2 *__restrict__ tasks,
+                                                               const uint8_t *__restrict__ seqa,
+                                                               const uint8_t *__restrict__ seqb,
+                                                               uint32_t *__restrict__ tb, uint32_t *__restrict__ bnd,
+                                                               sed_result *__restrict__ res,
+                                                               const double *__restrict__ gtab, sed_f64_params prm,
+                                                               sed_full_out fo) {
+    if constexpr (SED_SPLIT_PRIO > 0) __builtin_amdgcn_s_setprio(SED_SPLIT_PRIO);
+    static_assert(!(FULL && TB), "full-matrix output: distance kernel");
+    constexpr int ROWS = 64 * R;
+    constexpr int G = Grp<R>::G;
+    __shared__ double2 tab[SED_MAX_K * SED_MAX_K];
+    __shared__ f64_split_lds rg;
+    __shared__ uint32_t split_flag[2];
+    const int K = prm.K;
+    for (int e = threadIdx.x; e < K * K; e += blockDim.x) tab[e] = make_double2(gtab[2 * e], gtab[2 * e + 1]);
+    if (threadIdx.x < 2) split_flag[threadIdx.x] = 0u;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int2 task = tasks[blockIdx.x];
+    const int pair = __builtin_amdgcn_readfirstlane(task.x), k = __builtin_amdgcn_readfirstlane(task.y);
+    const sed_pair_desc d = pd[pair];
+    const int n = d.n, m = d.m;
+    if constexpr (FULL) {  // border cells (stripe 0's compute wave): row 0 (insert edges) and column 0 (delete edges)
+        if (k == 0 && threadIdx.x < 64) {
+            for (int j = lane; j <= m; j += 64) {
+                const double v = (double)j * prm.ins;
+                const uint32_t t = (j == 0) ? 1u : (TYPED ? (uint32_t)prm.ins_int : (uint32_t)(v == 0.0));
+                fo.D[j] = v;
+                fo.M[j] = (uint8_t)((j == 0 ? 0u : 1u) | (t << 3));
+            }
+            for (int i = 1 + lane; i <= n; i += 64) {
+                const double v = (double)i * prm.del;
+                const uint32_t t = TYPED ? (uint32_t)prm.del_int : (uint32_t)(v == 0.0);
+                fo.D[(uint64_t)i * (m + 1)] = v;
+                fo.M[(uint64_t)i * (m + 1)] = (uint8_t)(2u | (t << 3));
+            }
+        }
+    }
+    if (n == 0 || m == 0) {
+        if (threadIdx.x == 0) {
+            res[pair].dist = (n == 0) ? (double)m * prm.ins : (double)n * prm.del;
+            res[pair].len = n + m;
+            res[pair].is_int = (n == 0 && m == 0) ? 1 : (n == 0 ? prm.ins_int : prm.del_int);
+            res[pair].err = 0;
+        }
+        return;
+    }
+    const int nstripes = (n + ROWS - 1) / ROWS;
+    const int SG = (m + 63 + G - 1) / G * G;
+    const int nchunks = (SG + 63) >> 6;
+    const uint32_t plane_words = (uint32_t)(nchunks + 2) * 64u;
+    const uint8_t *pa = seqa + d.a_off;
+    const uint8_t *pb = seqb + d.b_off;
+    const uint32_t tins = (uint32_t)prm.ins_int, tdel = (uint32_t)prm.del_int;
+    if (threadIdx.x >= 64) {  // the feeder wave
+        f64_split_feed(k > 0 ? f64_split_words(bnd, d, k - 1, plane_words) : nullptr, plane_words, k == 0, m, SG,
+                       prm.epoch, pb, prm.ins, tins, rg, split_flag, lane);
+        return;
+    }
+    uint64_t *hout = f64_split_words(bnd, d, k, plane_words);
+    const int row0 = k * ROWS + lane * R;
+    double D[R];
+    uint32_t LK[R], T[R], rowbase[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int ri = row0 + r;
+        const uint32_t a = (ri < n) ? pa[ri] : 0u;
+        rowbase[r] = a * (uint32_t)K;
+        D[r] = (double)(ri + 1) * prm.del;
+        LK[r] = SED_F64_LB;
+        T[r] = tdel;
+    }
+    double dtop_prev = (double)row0 * prm.del;
+    uint32_t ltop_prev = SED_F64_LB;
+    uint32_t ttop_prev = (row0 == 0) ? 1u : tdel;
+    double dbot = 0.0;
+    uint32_t lbot = 0, tbot = 0, bsel = 0;
+    uint32_t W[4] = {0, 0, 0, 0};
+    uint32_t *tbk = TB ? tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * 256u : nullptr;
+    const bool last = (k == nstripes - 1);
+    const uint32_t tag = prm.epoch;
+    bool ok = true;
+    int ready = 0;  // steps the feeder has published as ready (last read)
+    for (int s = 0; s < SG; s += G) {
+        if (ready < s + G) {  // the ring holds this group's top-row cells (LDS only)
+            uint32_t f = lds_flag_get(split_flag), spins = 0;
+            while (ok && (int)(f & ~SED_PROG_POISON) < s + G) {
+                if (++spins > (1u << 24)) ok = false;
+                __builtin_amdgcn_s_sleep(1);
+                f = lds_flag_get(split_flag);
+            }
+            if (f & SED_PROG_POISON) ok = false;
+            ready = (int)(f & ~SED_PROG_POISON);
+            asm volatile("" ::: "memory");
+        }
+        // the group's steps as one straight-line block per variant (a lone wave is latency-bound: a branch per step
+        // kept the compiler from overlapping one step's table reads with the previous step's arithmetic)
+        // The group's top-row cells and symbols are read from the ring at its start, and each step's column symbol
+        // and table entries are fetched one step ahead (PF).
+        auto group = [&](auto masked_tag) {
+            constexpr bool MASKED = decltype(masked_tag)::value;
+            double dg[G];
+            uint32_t lg[G], tg[G], sg[G];
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                const int slot = (s + u) & (SED_F64_RING - 1);
+                dg[u] = rg.d[slot];
+                lg[u] = rg.l[slot];
+                tg[u] = TYPED ? rg.t[slot] : 0u;
+                sg[u] = rg.s[slot];
+            }
+            double2 en[R];
+            uint32_t bn = dpp_shr1(sg[0], bsel);
+#pragma unroll
+            for (int r = 0; r < R; ++r) en[r] = tab[rowbase[r] + bn];
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                const int j = s + u - lane + 1;
+                const bool active = (j >= 1) && (j <= m);
+                double2 e[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) e[r] = en[r];
+                bsel = bn;
+                if (u + 1 < G) {
+                    bn = dpp_shr1(sg[u + 1], bsel);
+#pragma unroll
+                    for (int r = 0; r < R; ++r) en[r] = tab[rowbase[r] + bn];
+                }
+                f64_step<R, TB, TYPED, MASKED, FULL, 64, true>(D, LK, T, rowbase, tab, dtop_prev, ltop_prev, ttop_prev,
+                                                               dbot, lbot, tbot, bsel, dg[u], lg[u], tg[u], 0u, W, u,
+                                                               prm.ins, prm.del, tins, tdel, active, fo, row0 + 1, j, e);
+                // every lane's bottom cell, lane 63's read back below: a write under lane == 63 put a branch (exec
+                // skip) between every two steps
+                rg.od[u][lane] = dbot;
+                rg.ol[u][lane] = lbot;
+                if (TYPED) rg.ot[u][lane] = tbot;
+                __builtin_amdgcn_sched_barrier(0);  // (the next step's table reads stay a step ahead of their use)
+            }
+        };
+        if ((s >= 63) && (s + G - 1 < m))
+            group(BoolTag<false>{});
+        else
+            group(BoolTag<true>{});
+        if constexpr (TB) store_tb(tbk + ((uint64_t)(s / G) * 64u + lane) * 4u, W);
+        if (!last && lane < G) {  // lane u hands off column s + u - 62 (lane 63's cell of step s + u)
+            const int col = s + lane - 62;
+            if (col >= 1 && col <= m) {
+                const uint32_t tg = tag | (ok ? 0u : SED_PROG_POISON);
+                const uint64_t bits = (uint64_t)__double_as_longlong(rg.od[lane][63]);
+                const uint32_t lt = rg.ol[lane][63] | (TYPED ? rg.ot[lane][63] : 0u);
+                store_tagged(hout + (uint32_t)(col + 64), tg, (uint32_t)bits);
+                store_tagged(hout + plane_words + (uint32_t)(col + 64), tg, (uint32_t)(bits >> 32));
+                store_tagged(hout + 2u * plane_words + (uint32_t)(col + 64), tg, lt);
+            }
+        }
+        asm volatile("" ::: "memory");
+        if (lane == 0) lds_flag_set(split_flag + 1, (uint32_t)(s + G));  // this group's ring slots are free again
+    }
+    if (last) {
+        const int w = (n - 1) % ROWS;
+        if (lane == w / R) {
+            const int rf = w % R;
+            double dv = 0.0;
+            uint32_t lv = 0, tv = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                dv = (r == rf) ? D[r] : dv;
+                lv = (r == rf) ? LK[r] : lv;
+                tv = (r == rf) ? T[r] : tv;
+            }
+            res[pair].dist = dv;
+            res[pair].len = n + m - (int32_t)((SED_F64_LB - lv) >> 2);
+            res[pair].is_int = TYPED ? (uint8_t)tv : (uint8_t)(dv == 0.0);
+            res[pair].err = ok ? 0 : SED_ERR_SPLIT_TIMEOUT;  // a timed-out wait anywhere up the chain poisons the pair
         }
     }
 }
@@ -2656,15 +2911,32 @@ static hipError_t launch_f64_R(const sed_launch &L, const double *gtab, const se
     return hipGetLastError();
 }
 
+// SPLIT (L.ntasks > 0): one 128-thread workgroup per (pair, stripe) task, R = 4
+template <bool TB, bool TYPED, bool FULL = false>
+static hipError_t launch_f64_split(const sed_launch &L, const double *gtab, const sed_f64_params &prm,
+                                   const sed_full_out &fo = sed_full_out{}) {
+    SED_LAUNCH((sed_wf_f64_split_kernel<4, TB, TYPED, FULL>), dim3(L.ntasks), dim3(128), 0, L, L.pd, L.tasks,
+               (const uint8_t *)L.seqa, (const uint8_t *)L.seqb, L.tb, L.bnd, L.res, gtab, prm, fo);
+    return hipGetLastError();
+}
+
 hipError_t sed_launch_f64_full(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed,
                                const sed_full_out &fo) {
     if (L.R != 4 || L.tb) return hipErrorInvalidValue;
+    if (L.ntasks > 0)
+        return typed ? launch_f64_split<false, true, true>(L, gtab, prm, fo)
+                     : launch_f64_split<false, false, true>(L, gtab, prm, fo);
     return typed ? launch_f64_R<4, false, true, true>(L, gtab, prm, fo)
                  : launch_f64_R<4, false, false, true>(L, gtab, prm, fo);
 }
 
 hipError_t sed_launch_f64(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed) {
     const bool tb = L.tb != nullptr;
+    if (L.ntasks > 0) {
+        if (L.R != 4) return hipErrorInvalidValue;
+        if (typed) return tb ? launch_f64_split<true, true>(L, gtab, prm) : launch_f64_split<false, true>(L, gtab, prm);
+        return tb ? launch_f64_split<true, false>(L, gtab, prm) : launch_f64_split<false, false>(L, gtab, prm);
+    }
     switch (L.R) {
 #define CASE(RR)                                                                                    \
     case RR:                                                                                        \

@@ -141,6 +141,11 @@ struct sed_batch {
     bool split_ck = false;
     int ck_tiles = 0;
     bool split = false;
+    // SPLIT hand-off words' tag: the last run's epoch (1..32767), kept across fills, so that a refilled batch (the
+    // per-call path fills the context's scratch batch every call) needs no memset; the buffer is zeroed when it is
+    // (re)allocated (d_bnd.cap differs from bnd_zero_cap) and when the epoch wraps
+    uint32_t split_epoch = 0;
+    size_t bnd_zero_cap = 0;
     bool ck = false;           // traceback from checkpoints + recompute (sed_kernels.hip: CK) instead of codes
     bool dot = false;          // CK forward kernel on dot keys (dot_keys below)
     bool lad = false;          // CHAIN kernel with the L field on ladder dot keys (dot_keys ladder mode)
@@ -546,6 +551,19 @@ int choose_R_f64(const int32_t *len_a, const int32_t *len_b, int npairs, bool la
     return cost[1] < cost[0] ? 8 : 4;
 }
 
+// the next run's SPLIT epoch, zeroing the hand-off words first when no word may carry a tag of its own (see split_epoch)
+hipError_t next_split_epoch(sed_batch *b, hipStream_t s, uint32_t *epoch) {
+    *epoch = b->split_epoch % 32767u + 1u;
+    b->split_epoch = *epoch;
+    if (!b->split || b->bnd_words == 0) return hipSuccess;
+    if (*epoch == 1 || b->d_bnd.cap != b->bnd_zero_cap) {
+        hipError_t e = hipMemsetAsync(b->d_bnd.p, 0, b->d_bnd.cap, s);
+        if (e != hipSuccess) return e;
+        b->bnd_zero_cap = b->d_bnd.cap;
+    }
+    return hipSuccess;
+}
+
 // Event-log entries {DP start, DP end, traceback start, traceback end}, created ahead of the runs
 // that use them (outside any timed loop for up to `more` runs).  Batches in parts also get the parts' entries
 // (plog), up to the same count, so no event is created while runs are being timed.
@@ -654,6 +672,14 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         split = c->opt_split == 1 || (npairs <= 256 && max_n > 256 && c->opt_chain != 1 && c->opt_chain < 3);
         if (split && !c->opt_R) R = 4;
         if (split && R != 4 && R != 8 && R != 16 && R != 32) split = false;
+    } else if (mode != SED_MODE_I32 && c->opt_split != 2 && !seg_ok) {
+        // fp64 SPLIT (sed_wf_f64_split_kernel, R = 4): batches of few pairs, whose lone fp64 waves are otherwise one
+        // SIMD each.  It also runs the one-stripe pairs (tools/fp64_call_scaling.py, profiles/r05/s25: 30 nt 39.9
+        // against 40.6 us per call, 200 nt 72 against 87, 500 nt 151 against 255, 2000 nt 544 against 3497), since
+        // its lone wave reads each step's table entries a step ahead; distance-only batches whose pairs all fit the
+        // lane kernels keep those
+        split = (c->opt_split == 1 || (npairs <= 256 && nwave_f64 > 0)) && (!c->opt_R || c->opt_R == 4);
+        if (split) R = 4;
     }
     b->split = split;
     b->mode = mode;
@@ -688,7 +714,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     b->tbpar_items = b->tbpar_kmax = 0;
     // SPLIT script batches: checkpoints + a tile-parallel recompute of the codes (dot or distance keys in the forward:
     // 2-3 VALU per cell against the ladder keys' 5.2 on the latency-bound stripe chain)
-    b->split_ck = want_tb && split && R == 4 && c->opt_splitck != 2;
+    b->split_ck = want_tb && split && mode == SED_MODE_I32 && R == 4 && c->opt_splitck != 2;
     b->ck_tiles = 0;
 
     // ---- layout ----
@@ -743,7 +769,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
                 if (b->split_ck) b->ck_tiles = std::max<int>(b->ck_tiles, (int)(nstripes * R * nchunks));
             }
             // SPLIT: 64-bit {epoch tag, value} words per column and stripe (the tagged hand-off, sed_kernels.hip)
-            if (nstripes > 1) bndw += (nchunks + 2) * SW * (packed ? (split ? 2 : 1) : 4) * (split ? nstripes : 1);
+            // (fp64: D, L and T planes; SPLIT: three 64-bit {tag, D low | D high | L key and T} words)
+            if (nstripes > 1) bndw += (nchunks + 2) * SW * (packed ? (split ? 2 : 1) : (split ? 6 : 4)) * (split ? nstripes : 1);
             if (b->tbpar && nstripes >= 3) {  // {exit column, ops} per stripe and column
                 mapw += nstripes * (uint64_t)(mm + 1) * 2;
                 // workgroups of 256 columns per middle stripe, and one for the sink's stripe
@@ -1272,14 +1299,10 @@ int run_batch(sed_batch *b) {
         ++idp;
     };
     if (ndp == 0 && lg[0] && (e = hipEventRecord(lg[0], ds)) != hipSuccess) return c->hipfail(e, "event record");
-    // SPLIT hand-off words carry the run's epoch (1..32767), so the buffer is zeroed only on a batch's first run
-    // (runs restarts at 0 on every fill) and when the epoch wraps; every kernel writes all result fields, err
-    // included
+    // SPLIT hand-off words carry the run's epoch (1..32767, next_split_epoch); every kernel writes all result
+    // fields, err included
     sed_i32_params ip = b->ip;
-    ip.epoch = (uint32_t)(b->runs % 32767u) + 1u;
-    if (b->split && b->bnd_words && ip.epoch == 1 &&
-        (e = hipMemsetAsync(b->d_bnd.p, 0, 4 * b->bnd_words, ds)) != hipSuccess)
-        return c->hipfail(e, "memset hand-off words");
+    if ((e = next_split_epoch(b, ds, &ip.epoch)) != hipSuccess) return c->hipfail(e, "memset hand-off words");
     const bool len = want_tb || !(b->flags & SED_NO_LEN);
     if (b->nparts > 1 && want_tb) return run_batch_parts(b, lg, L, ip, len);
     if (b->nwave_x2 > 0) {
@@ -1316,8 +1339,11 @@ int run_batch(sed_batch *b) {
             }
         } else if (b->mode == SED_MODE_I32)
             e = sed_launch_i32(L, ip, len);
-        else
-            e = sed_launch_f64(L, (const double *)c->gtab.p, b->fp, b->mode == SED_MODE_F64_TYPED);
+        else {
+            sed_f64_params fp = b->fp;
+            fp.epoch = ip.epoch;
+            e = sed_launch_f64(L, (const double *)c->gtab.p, fp, b->mode == SED_MODE_F64_TYPED);
+        }
         if (e != hipSuccess) return c->hipfail(e, "DP kernel launch");
     }
     if (b->nseg > 0) {  // fp64 pairs in 16-lane segments, four per wave
@@ -1683,6 +1709,8 @@ int sed_batch_bitpar_pairs(const sed_batch *b) {
 
 int sed_batch_segment_pairs(const sed_batch *b) { return b ? b->nseg : SED_E_ARG; }
 
+int sed_batch_split_tasks(const sed_batch *b) { return b ? (b->split ? b->ntasks : 0) : SED_E_ARG; }
+
 int sed_batch_scaled_pairs(const sed_batch *b) {
     return b ? (b->scaled ? b->nlane - b->nbitpar_f64 : 0) : SED_E_ARG;
 }
@@ -1933,11 +1961,13 @@ int sed_full_matrix(sed_ctx *c, const uint8_t *codes_a, int32_t n, const uint8_t
     L.bnd = (uint32_t *)tmp.d_bnd.p;
     L.res = (sed_result *)tmp.p_res[0];
     L.R = 4;
-    L.tasks = nullptr;
-    L.ntasks = 0;
+    L.tasks = tmp.split ? (const int2 *)tmp.p_tasks : nullptr;  // (a pair past 32 symbols: SPLIT)
+    L.ntasks = tmp.split ? tmp.ntasks : 0;
     L.stream = c->stream;
     sed_full_out fo{(double *)fD.p, (uint8_t *)fM.p, n, m};
-    hipError_t e = sed_launch_f64_full(L, (const double *)c->gtab.p, tmp.fp, tmp.mode == SED_MODE_F64_TYPED, fo);
+    sed_f64_params fp = tmp.fp;
+    hipError_t e = next_split_epoch(&tmp, c->stream, &fp.epoch);
+    if (e == hipSuccess) e = sed_launch_f64_full(L, (const double *)c->gtab.p, fp, tmp.mode == SED_MODE_F64_TYPED, fo);
     if (e == hipSuccess) e = hipMemcpyAsync(D, fD.p, 8 * cells, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(M, fM.p, cells, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);

@@ -82,6 +82,7 @@ SIGNATURES = [
     ("sed_batch_bitpar_pairs", C.c_int, [C.c_void_p]),
     ("sed_batch_scaled_pairs", C.c_int, [C.c_void_p]),
     ("sed_batch_segment_pairs", C.c_int, [C.c_void_p]),
+    ("sed_batch_split_tasks", C.c_int, [C.c_void_p]),
     ("sed_batch_traceback_mode", C.c_int, [C.c_void_p]),
     ("sed_batch_chain_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("sed_batch_run", C.c_int, [C.c_void_p]),
@@ -401,6 +402,11 @@ class Batch:
     def segment_pairs(self):
         """fp64 wave pairs computed in 16-lane segments, four per wave (SED_OPT_SEG)."""
         return self._lib.sed_batch_segment_pairs(self.ptr)
+
+    @property
+    def split_tasks(self):
+        """SPLIT batches: the (pair, stripe) workgroups of a run, 0 otherwise (SED_OPT_SPLIT)."""
+        return self._lib.sed_batch_split_tasks(self.ptr)
 
     def run(self):
         self.ctx._check(self._lib.sed_batch_run(self.ptr), "sed_batch_run")

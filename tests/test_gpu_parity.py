@@ -694,6 +694,70 @@ def test_checkpoint_route_every_R_stripe_and_chain(gpu, tables, R, chain):
 
 
 @pytest.mark.parametrize("table_name", ["costs.json", "int_literals", "frac_indel"])
+def test_fp64_split_vs_oracle(gpu, tables, table_name):
+    """fp64 SPLIT (sed_wf_f64_split_kernel): batches of <= 256 pairs with a pair past 256 rows run one 128-thread
+    workgroup per 256-row stripe, the stripes handing their bottom rows down through tagged {D low, D high, L key |
+    typing} words (timing.py's one-call loop at 300-500 nt, GUI calls over IUPAC symbols; timing.py:45-57,
+    StringEditDistance.py:92-128).  Ragged IUPAC pairs of 257..1400 rows, one-stripe and empty sides, m past and
+    below a chunk, scripts and distances, every pair against the oracle and identical to SED_OPT_SPLIT = 2 (lone
+    waves); the forced route (SED_OPT_SPLIT = 1) on the same batch."""
+    table = tables[False] if table_name == "costs.json" else load_golden("g8_cost_tables.json")["tables"][table_name]
+    pairs = _random_pairs(9100 + len(table_name), 14, IUPAC, 257, 1400, related=True)
+    pairs += _random_pairs(9200 + len(table_name), 6, IUPAC, 1, 700)
+    rng = np.random.default_rng(9300)
+    for n, m in ((257, 1), (1000, 5), (300, 64), (513, 65), (768, 700), (200, 900), (1, 1200)):
+        pairs.append(("".join(rng.choice(list(IUPAC), size=n)), "".join(rng.choice(list(IUPAC), size=m))))
+    pairs += [("", "ACG" * 100), ("GUA" * 100, ""), ("", "")]
+    plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
+    gpu.set_costs(plan)
+    for script in (True, False):
+        b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs],
+                                                 [plan.encode(y) for _, y in pairs]), script)
+        try:
+            assert b.mode in ("f64", "f64-typed") and b.rows_per_lane == 4
+            assert b.split_tasks == sum(-(-len(a) // 256) if a and y else 1 for a, y in pairs), b.split_tasks
+        finally:
+            b.close()
+        got = gpu_run(gpu, table, pairs, script=script)
+        _oracle_check(table, pairs, got)
+        assert gpu_run(gpu, table, pairs, script=script, split=2) == got, (table_name, script)
+        assert gpu_run(gpu, table, pairs, script=script, split=1) == got, (table_name, script)
+    # the run repeated on one batch: the hand-off words of run k + 1 carry another epoch than run k's
+    b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs], [plan.encode(y) for _, y in pairs]),
+                     True)
+    try:
+        for _ in range(3):
+            b.run()
+            b.sync()
+    finally:
+        b.close()
+
+
+def test_fp64_split_full_matrix(gpu, tables):
+    """The dp proxy's full matrix (sed_full_matrix, fp64 at R = 4) of pairs past 256 rows runs SPLIT: every cell's
+    value, typing and edge mask identical to the lone-wave kernel's (SED_OPT_SPLIT = 2), the sink to the oracle's."""
+    rng = np.random.default_rng(9400)
+    shapes = ((600, 450), (257, 300), (1000, 40), (300, 1))
+    for user in (False, True):
+        table = tables[user]
+        for n, m in shapes:
+            a = "".join(rng.choice(list(IUPAC), size=n))
+            b = "".join(rng.choice(list(IUPAC), size=m))
+            plan = sedcost.build_plan(table, [a], [b])
+            gpu.set_costs(plan)
+            D, M = gpu.full_matrix(plan.encode(a), plan.encode(b))
+            gpu.set_option(sedgpu.SED_OPT_SPLIT, 2)
+            try:
+                D2, M2 = gpu.full_matrix(plan.encode(a), plan.encode(b))
+            finally:
+                gpu.set_option(sedgpu.SED_OPT_SPLIT, 0)
+            assert np.array_equal(D.view(np.uint64), D2.view(np.uint64)) and np.array_equal(M, M2), (user, n, m)
+            o = oracle.pair(oracle.Costs.from_plan(plan), plan.encode(a), plan.encode(b))
+            assert (float(D[n, m]), bool(M[n, m] >> 3)) == (o["dist"], bool(o["is_int"])), (user, n, m)
+
+
+
+@pytest.mark.parametrize("table_name", ["costs.json", "int_literals", "frac_indel"])
 def test_fp64_segments_vs_oracle(gpu, tables, table_name):
     """fp64 batches of > 256 wave pairs run the pairs their cost model favours in 16-lane segments, four per wave
     (sed_wf_f64_kernel SW = 16: row DPP moves, 16-step chunks, a 15-step ramp) with the per-cell-code traceback of
