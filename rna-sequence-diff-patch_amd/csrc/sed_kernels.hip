@@ -1585,19 +1585,20 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
 // the row-0 border.  The compute wave is sed_wf_f64_kernel's stripe loop (SW = 64) reading the ring.  Codes, the
 // bottom-row-free layout and the result are the one-wave kernel's, so the tracebacks read them unchanged.
 #define SED_F64_RING 256
-struct f64_split_lds {
+template <int G> struct f64_split_lds {
     double d[SED_F64_RING];
     uint32_t l[SED_F64_RING], t[SED_F64_RING], s[SED_F64_RING];
-    double od[16][64];  // every lane's bottom cell of the group's steps (lane 63's are handed off)
-    uint32_t ol[16][64], ot[16][64];
+    double od[G][64];  // every lane's bottom cell of the group's steps (lane 63's are handed off)
+    uint32_t ol[G][64], ot[G][64];
 };
 // the three hand-off planes of stripe k: words [plane][column + 64], (nchunks + 2) * 64 per plane
 __device__ __forceinline__ uint64_t *f64_split_words(uint32_t *bnd, const sed_pair_desc &d, int k, uint32_t plane_words) {
     return reinterpret_cast<uint64_t *>(bnd + d.bnd_off) + (uint64_t)k * 3u * plane_words;
 }
+template <int G>
 __device__ void f64_split_feed(const uint64_t *__restrict__ hin, const uint32_t plane_words, const bool top, const int m,
                                const int SG, const uint32_t epoch, const uint8_t *__restrict__ pb, const double ins,
-                               const uint32_t tins, f64_split_lds &rg, uint32_t *flag, const int lane) {
+                               const uint32_t tins, f64_split_lds<G> &rg, uint32_t *flag, const int lane) {
     uint32_t poison = 0, idle = 0;
     int have = 0;  // steps whose top-row cells are in the ring
     while (have < SG) {
@@ -1660,7 +1661,7 @@ __global__ __launch_bounds__(128) void sed_wf_f64_split_kernel(const sed_pair_de
     constexpr int ROWS = 64 * R;
     constexpr int G = Grp<R>::G;
     __shared__ double2 tab[SED_MAX_K * SED_MAX_K];
-    __shared__ f64_split_lds rg;
+    __shared__ f64_split_lds<Grp<R>::G> rg;
     __shared__ uint32_t split_flag[2];
     const int K = prm.K;
     for (int e = threadIdx.x; e < K * K; e += blockDim.x) tab[e] = make_double2(gtab[2 * e], gtab[2 * e + 1]);
@@ -1704,7 +1705,7 @@ __global__ __launch_bounds__(128) void sed_wf_f64_split_kernel(const sed_pair_de
     const uint8_t *pb = seqb + d.b_off;
     const uint32_t tins = (uint32_t)prm.ins_int, tdel = (uint32_t)prm.del_int;
     if (threadIdx.x >= 64) {  // the feeder wave
-        f64_split_feed(k > 0 ? f64_split_words(bnd, d, k - 1, plane_words) : nullptr, plane_words, k == 0, m, SG,
+        f64_split_feed<G>(k > 0 ? f64_split_words(bnd, d, k - 1, plane_words) : nullptr, plane_words, k == 0, m, SG,
                        prm.epoch, pb, prm.ins, tins, rg, split_flag, lane);
         return;
     }
@@ -1748,44 +1749,53 @@ __global__ __launch_bounds__(128) void sed_wf_f64_split_kernel(const sed_pair_de
         // kept the compiler from overlapping one step's table reads with the previous step's arithmetic)
         // The group's top-row cells and symbols are read from the ring at its start, and each step's column symbol
         // and table entries are fetched one step ahead (PF).
+        // (ring entries in blocks of 16 steps: the R = 2 group's 32 would take ~160 VGPRs at once)
         auto group = [&](auto masked_tag) {
             constexpr bool MASKED = decltype(masked_tag)::value;
-            double dg[G];
-            uint32_t lg[G], tg[G], sg[G];
-#pragma unroll
-            for (int u = 0; u < G; ++u) {
-                const int slot = (s + u) & (SED_F64_RING - 1);
-                dg[u] = rg.d[slot];
-                lg[u] = rg.l[slot];
-                tg[u] = TYPED ? rg.t[slot] : 0u;
-                sg[u] = rg.s[slot];
-            }
+            constexpr int HB = G < 16 ? G : 16;
             double2 en[R];
-            uint32_t bn = dpp_shr1(sg[0], bsel);
+            uint32_t bn = dpp_shr1(rg.s[s & (SED_F64_RING - 1)], bsel);
 #pragma unroll
             for (int r = 0; r < R; ++r) en[r] = tab[rowbase[r] + bn];
 #pragma unroll
-            for (int u = 0; u < G; ++u) {
-                const int j = s + u - lane + 1;
-                const bool active = (j >= 1) && (j <= m);
-                double2 e[R];
+            for (int h = 0; h < G; h += HB) {
+                double dg[HB];
+                uint32_t lg[HB], tg[HB], sg[HB + 1];
 #pragma unroll
-                for (int r = 0; r < R; ++r) e[r] = en[r];
-                bsel = bn;
-                if (u + 1 < G) {
-                    bn = dpp_shr1(sg[u + 1], bsel);
-#pragma unroll
-                    for (int r = 0; r < R; ++r) en[r] = tab[rowbase[r] + bn];
+                for (int v = 0; v <= HB; ++v) {
+                    const int slot = (s + h + v) & (SED_F64_RING - 1);
+                    if (v < HB) {
+                        dg[v] = rg.d[slot];
+                        lg[v] = rg.l[slot];
+                        tg[v] = TYPED ? rg.t[slot] : 0u;
+                    }
+                    if (v > 0) sg[v] = rg.s[slot];  // (sg[0]: in bn already)
                 }
-                f64_step<R, TB, TYPED, MASKED, FULL, 64, true>(D, LK, T, rowbase, tab, dtop_prev, ltop_prev, ttop_prev,
-                                                               dbot, lbot, tbot, bsel, dg[u], lg[u], tg[u], 0u, W, u,
-                                                               prm.ins, prm.del, tins, tdel, active, fo, row0 + 1, j, e);
-                // every lane's bottom cell, lane 63's read back below: a write under lane == 63 put a branch (exec
-                // skip) between every two steps
-                rg.od[u][lane] = dbot;
-                rg.ol[u][lane] = lbot;
-                if (TYPED) rg.ot[u][lane] = tbot;
-                __builtin_amdgcn_sched_barrier(0);  // (the next step's table reads stay a step ahead of their use)
+#pragma unroll
+                for (int v = 0; v < HB; ++v) {
+                    const int u = h + v;
+                    const int j = s + u - lane + 1;
+                    const bool active = (j >= 1) && (j <= m);
+                    double2 e[R];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) e[r] = en[r];
+                    bsel = bn;
+                    if (u + 1 < G) {
+                        bn = dpp_shr1(sg[v + 1], bsel);
+#pragma unroll
+                        for (int r = 0; r < R; ++r) en[r] = tab[rowbase[r] + bn];
+                    }
+                    f64_step<R, TB, TYPED, MASKED, FULL, 64, true>(D, LK, T, rowbase, tab, dtop_prev, ltop_prev,
+                                                                   ttop_prev, dbot, lbot, tbot, bsel, dg[v], lg[v],
+                                                                   tg[v], 0u, W, u, prm.ins, prm.del, tins, tdel,
+                                                                   active, fo, row0 + 1, j, e);
+                    // every lane's bottom cell, lane 63's read back below: a write under lane == 63 put a branch
+                    // (exec skip) between every two steps
+                    rg.od[u][lane] = dbot;
+                    rg.ol[u][lane] = lbot;
+                    if (TYPED) rg.ot[u][lane] = tbot;
+                    __builtin_amdgcn_sched_barrier(0);  // (the next step's table reads stay a step ahead of their use)
+                }
             }
         };
         if ((s >= 63) && (s + G - 1 < m))
@@ -1935,8 +1945,8 @@ __device__ __forceinline__ uint32_t window_walk(const sed_pair_desc &d, int i, i
                                                 uint32_t *__restrict__ out, const uint64_t pat, uint32_t &bad) {
     constexpr int G = Grp<R>::G, NT = G, NS = R;  // NT * NS = 64 blocks
     constexpr int P = Ladder<R>::P;
-    constexpr int LR = R == 4 ? 2 : R == 8 ? 3 : R == 16 ? 4 : 5, LG = 6 - LR;
-    static_assert((1 << LR) == R, "R must be a power of two in 4..32");
+    constexpr int LR = R == 2 ? 1 : R == 4 ? 2 : R == 8 ? 3 : R == 16 ? 4 : 5, LG = 6 - LR;
+    static_assert((1 << LR) == R, "R must be a power of two in 2..32");
     const int m = d.m;
     const int SG = (m + 63 + G - 1) / G * G;
     const uint64_t stripe_words = (uint64_t)(SG / G) * 256u;
@@ -2049,7 +2059,7 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
 //     script words with atomicOr (the two words a segment shares with its neighbours; the buffer is zeroed).
 // ---------------------------------------------------------------------------
 template <int R> struct CodeCursor {  // per-lane reader of one pair's per-cell codes, one 16-byte block cached
-    static constexpr int G = Grp<R>::G, LR = R == 4 ? 2 : R == 8 ? 3 : R == 16 ? 4 : 5, LG = 6 - LR;
+    static constexpr int G = Grp<R>::G, LR = R == 2 ? 1 : R == 4 ? 2 : R == 8 ? 3 : R == 16 ? 4 : 5, LG = 6 - LR;
     static constexpr int P = Ladder<R>::P;
     const uint32_t *base;
     uint64_t stripe_words;
@@ -2911,18 +2921,22 @@ static hipError_t launch_f64_R(const sed_launch &L, const double *gtab, const se
     return hipGetLastError();
 }
 
-// SPLIT (L.ntasks > 0): one 128-thread workgroup per (pair, stripe) task, R = 4
+// SPLIT (L.ntasks > 0): one 128-thread workgroup per (pair, stripe) task, R = 2 (the default) or 4
 template <bool TB, bool TYPED, bool FULL = false>
 static hipError_t launch_f64_split(const sed_launch &L, const double *gtab, const sed_f64_params &prm,
                                    const sed_full_out &fo = sed_full_out{}) {
-    SED_LAUNCH((sed_wf_f64_split_kernel<4, TB, TYPED, FULL>), dim3(L.ntasks), dim3(128), 0, L, L.pd, L.tasks,
+    if (L.R == 2)
+        SED_LAUNCH((sed_wf_f64_split_kernel<2, TB, TYPED, FULL>), dim3(L.ntasks), dim3(128), 0, L, L.pd, L.tasks,
+                   (const uint8_t *)L.seqa, (const uint8_t *)L.seqb, L.tb, L.bnd, L.res, gtab, prm, fo);
+    else if (L.R == 4)
+        SED_LAUNCH((sed_wf_f64_split_kernel<4, TB, TYPED, FULL>), dim3(L.ntasks), dim3(128), 0, L, L.pd, L.tasks,
                (const uint8_t *)L.seqa, (const uint8_t *)L.seqb, L.tb, L.bnd, L.res, gtab, prm, fo);
     return hipGetLastError();
 }
 
 hipError_t sed_launch_f64_full(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed,
                                const sed_full_out &fo) {
-    if (L.R != 4 || L.tb) return hipErrorInvalidValue;
+    if (L.tb || (L.ntasks > 0 ? (L.R != 2 && L.R != 4) : L.R != 4)) return hipErrorInvalidValue;
     if (L.ntasks > 0)
         return typed ? launch_f64_split<false, true, true>(L, gtab, prm, fo)
                      : launch_f64_split<false, false, true>(L, gtab, prm, fo);
@@ -2933,7 +2947,7 @@ hipError_t sed_launch_f64_full(const sed_launch &L, const double *gtab, const se
 hipError_t sed_launch_f64(const sed_launch &L, const double *gtab, const sed_f64_params &prm, bool typed) {
     const bool tb = L.tb != nullptr;
     if (L.ntasks > 0) {
-        if (L.R != 4) return hipErrorInvalidValue;
+        if (L.R != 2 && L.R != 4) return hipErrorInvalidValue;
         if (typed) return tb ? launch_f64_split<true, true>(L, gtab, prm) : launch_f64_split<false, true>(L, gtab, prm);
         return tb ? launch_f64_split<true, false>(L, gtab, prm) : launch_f64_split<false, false>(L, gtab, prm);
     }
@@ -3012,7 +3026,7 @@ hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops) {
                                L.npairs, L.tb, L.res, ops, pat, nullptr);                                       \
         break;                                                                                                   \
     }
-        CASE(4) CASE(8) CASE(16) CASE(32)
+        CASE(2) CASE(4) CASE(8) CASE(16) CASE(32)  // (R = 2: the fp64 SPLIT route's codes)
 #undef CASE
     default: return hipErrorInvalidValue;
     }
@@ -3033,9 +3047,9 @@ hipError_t sed_launch_traceback_stripes(const sed_launch &L, uint32_t *ops, uint
                            pat);                                                                                 \
         break;                                                                                                   \
     }
-        CASE(4)
+        CASE(2) CASE(4)
 #undef CASE
-    default: return hipErrorInvalidValue;  // the runtime takes this route at R = 4 only
+    default: return hipErrorInvalidValue;  // the runtime takes this route at R = 2 (fp64 SPLIT) and 4 only
     }
     return hipGetLastError();
 }

@@ -638,9 +638,14 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // fp64 batches of more than 256 wave pairs may run short pairs in 16-lane segments (SED_OPT_SEG; the window
     // traceback of smaller batches reads the 64-lane layout only)
     int nwave_f64 = 0;
-    for (int p = 0; p < npairs; ++p)
-        if (len_a[p] > 0 && len_b[p] > 0 && !(f64_lane && len_a[p] <= SED_LANE_MAXN && len_b[p] <= SED_LANE_MAXM))
+    double lane_cells_f64 = 0;  // the largest fp64 lane pair (n m): one lane walks all of it
+    for (int p = 0; p < npairs; ++p) {
+        if (len_a[p] <= 0 || len_b[p] <= 0) continue;
+        if (f64_lane && len_a[p] <= SED_LANE_MAXN && len_b[p] <= SED_LANE_MAXM)
+            lane_cells_f64 = std::max(lane_cells_f64, (double)len_a[p] * len_b[p]);
+        else
             ++nwave_f64;
+    }
     const bool seg_ok = c->opt_seg != 2 && nwave_f64 > 256;
     int R = (mode == SED_MODE_I32 || c->opt_R) ? choose_R(mode, max_n, c->opt_R)
                                                 : choose_R_f64(len_a, len_b, npairs, f64_lane && mode == SED_MODE_F64, seg_ok);
@@ -663,7 +668,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     } else if (c->K > SED_MAX_K) {
         return c->fail(SED_E_ALPHABET, "alphabet of %d symbols exceeds %d", c->K, SED_MAX_K);
     }
-    if (mode == SED_MODE_I32 ? !(R == 4 || R == 8 || R == 16 || R == 32) : !(R == 4 || R == 8))
+    if (mode == SED_MODE_I32 ? !(R == 4 || R == 8 || R == 16 || R == 32) : !(R == 2 || R == 4 || R == 8))
         return c->fail(SED_E_ARG, "unsupported rows-per-lane %d for mode %d", R, mode);
     // SPLIT (integer kernel): one wave per stripe with inter-workgroup hand-offs, for
     // batches too small to fill the GPU with one wave per pair (config 2, GUI calls).
@@ -678,9 +683,16 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         // against 40.6 us per call, 200 nt 72 against 87, 500 nt 151 against 255, 2000 nt 544 against 3497), since
         // its lone wave reads each step's table entries a step ahead; distance-only batches whose pairs all fit the
         // lane kernels keep those
-        split = (c->opt_split == 1 || (npairs <= 256 && nwave_f64 > 0)) && (!c->opt_R || c->opt_R == 4);
-        if (split) R = 4;
+        // R = 2 by default: a lone fp64 wave is issue-bound (~80 VALU per step at R = 4), so halving the rows per
+        // step outweighs the twice as many hand-offs (per call, 500^2: 150 us at R = 4, tools/fp64_call_scaling.py)
+        // A lane pair past 256 cells also goes SPLIT: 30^2 distance-only took 45 us per call on the lane kernel,
+        // 32 us SPLIT (10^2: 27 against 33 us)
+        split = (c->opt_split == 1 || (npairs <= 256 && (nwave_f64 > 0 || lane_cells_f64 > 256.0))) &&
+                (!c->opt_R || c->opt_R == 2 || c->opt_R == 4);
+        if (split) R = c->opt_R ? c->opt_R : 2;
     }
+    if (mode != SED_MODE_I32 && R == 2 && !split)
+        return c->fail(SED_E_ARG, "rows-per-lane 2 runs on the fp64 SPLIT route only");
     b->split = split;
     b->mode = mode;
     b->R = R;
@@ -709,7 +721,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // SED_TBPAR=0/1 overrides (A/B)
     static const int tbpar_env = [] { const char *e = getenv("SED_TBPAR"); return e ? atoi(e) : -1; }();
     // (never with fp64 pairs in 16-lane segments: the stripe kernels read the 64-lane code layout only)
-    b->tbpar = want_tb && !b->ck && R == 4 && (tbpar_env < 0 ? npairs <= 64 : tbpar_env > 0) &&
+    b->tbpar = want_tb && !b->ck && (R == 4 || R == 2) && (tbpar_env < 0 ? npairs <= 64 : tbpar_env > 0) &&
                !(seg_ok && mode != SED_MODE_I32);
     b->tbpar_items = b->tbpar_kmax = 0;
     // SPLIT script batches: checkpoints + a tile-parallel recompute of the codes (dot or distance keys in the forward:

@@ -695,10 +695,10 @@ def test_checkpoint_route_every_R_stripe_and_chain(gpu, tables, R, chain):
 
 @pytest.mark.parametrize("table_name", ["costs.json", "int_literals", "frac_indel"])
 def test_fp64_split_vs_oracle(gpu, tables, table_name):
-    """fp64 SPLIT (sed_wf_f64_split_kernel): batches of <= 256 pairs with a pair past 256 rows run one 128-thread
-    workgroup per 256-row stripe, the stripes handing their bottom rows down through tagged {D low, D high, L key |
-    typing} words (timing.py's one-call loop at 300-500 nt, GUI calls over IUPAC symbols; timing.py:45-57,
-    StringEditDistance.py:92-128).  Ragged IUPAC pairs of 257..1400 rows, one-stripe and empty sides, m past and
+    """fp64 SPLIT (sed_wf_f64_split_kernel): batches of <= 256 pairs run one 128-thread workgroup per stripe of 128
+    rows (R = 2; 256 rows at SED_OPT_ROWS_PER_LANE = 4), the stripes handing their bottom rows down through tagged
+    {D low, D high, L key | typing} words (timing.py's one-call loop at 300-500 nt, GUI calls over IUPAC symbols;
+    timing.py:45-57, StringEditDistance.py:92-128).  Ragged IUPAC pairs of 257..1400 rows, one-stripe and empty sides, m past and
     below a chunk, scripts and distances, every pair against the oracle and identical to SED_OPT_SPLIT = 2 (lone
     waves); the forced route (SED_OPT_SPLIT = 1) on the same batch."""
     table = tables[False] if table_name == "costs.json" else load_golden("g8_cost_tables.json")["tables"][table_name]
@@ -711,15 +711,19 @@ def test_fp64_split_vs_oracle(gpu, tables, table_name):
     plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
     gpu.set_costs(plan)
     for script in (True, False):
-        b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs],
-                                                 [plan.encode(y) for _, y in pairs]), script)
-        try:
-            assert b.mode in ("f64", "f64-typed") and b.rows_per_lane == 4
-            assert b.split_tasks == sum(-(-len(a) // 256) if a and y else 1 for a, y in pairs), b.split_tasks
-        finally:
-            b.close()
+        for R in (2, 4):  # the default (R = 2: stripes of 128 rows) and SED_OPT_ROWS_PER_LANE = 4
+            gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0 if R == 2 else R)
+            b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs],
+                                                     [plan.encode(y) for _, y in pairs]), script)
+            try:
+                assert b.mode in ("f64", "f64-typed") and b.rows_per_lane == R
+                assert b.split_tasks == sum(-(-len(a) // (64 * R)) if a and y else 1 for a, y in pairs), b.split_tasks
+            finally:
+                b.close()
+                gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
         got = gpu_run(gpu, table, pairs, script=script)
         _oracle_check(table, pairs, got)
+        assert gpu_run(gpu, table, pairs, script=script, R=4) == got, (table_name, script)
         assert gpu_run(gpu, table, pairs, script=script, split=2) == got, (table_name, script)
         assert gpu_run(gpu, table, pairs, script=script, split=1) == got, (table_name, script)
     # the run repeated on one batch: the hand-off words of run k + 1 carry another epoch than run k's
