@@ -690,6 +690,18 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         split = (c->opt_split == 1 || (npairs <= 256 && (nwave_f64 > 0 || lane_cells_f64 > 256.0))) &&
                 (!c->opt_R || c->opt_R == 2 || c->opt_R == 4);
         if (split) R = c->opt_R ? c->opt_R : 2;
+        // (automatic route: its hand-off words, 24 B per column and stripe, stay under 4 GB)
+        if (split && c->opt_split != 1 && !c->opt_R) {
+            double words = 0;
+            for (int p = 0; p < npairs; ++p) {
+                const double st = (double)((len_a[p] + 64 * R - 1) / (64 * R)), ch = (double)((len_b[p] + 127) / 64 + 2);
+                if (st > 1) words += st * ch * 64.0 * 6.0;
+            }
+            if (4.0 * words > 4e9) {
+                split = false;
+                R = choose_R_f64(len_a, len_b, npairs, f64_lane && mode == SED_MODE_F64, seg_ok);
+            }
+        }
     }
     if (mode != SED_MODE_I32 && R == 2 && !split)
         return c->fail(SED_E_ARG, "rows-per-lane 2 runs on the fp64 SPLIT route only");
