@@ -1352,11 +1352,13 @@ int run_batch(sed_batch *b) {
             e = sed_launch_i32_chain(L, ip, len);
             if (e == hipSuccess && b->chain_dyn) ++b->chain_launches[k];
         } else if (b->mode == SED_MODE_I32 && b->split_ck) {  // forward with checkpoints, then every tile's codes
+            // (pipelined runs: the codes kernel opens the traceback phase on its stream below, so the next run's
+            // forward follows this one directly: config 2 ran 0.297-0.301 ms per step with it on the DP stream)
             sed_launch Lf = L;
             Lf.ck = true;
-            Lf.ev1 = nullptr;
+            if (ts == ds) Lf.ev1 = nullptr;
             e = sed_launch_i32(Lf, ip, len);
-            if (e == hipSuccess) {
+            if (e == hipSuccess && ts == ds) {
                 sed_launch Lc = L;
                 Lc.ev0 = nullptr;
                 e = sed_launch_ck_codes(Lc, b->ck_tiles, ip);
@@ -1419,6 +1421,12 @@ int run_batch(sed_batch *b) {
             L.stream = ts;
             L.ev0 = lg[2];
             L.ev1 = lg[3];
+            if (b->split_ck && ts != ds) {  // the tile codes of this run's checkpoints (see the DP phase)
+                sed_launch Lc = L;
+                Lc.ev1 = nullptr;
+                if ((e = sed_launch_ck_codes(Lc, b->ck_tiles, ip)) != hipSuccess) return c->hipfail(e, "codes kernel launch");
+                L.ev0 = nullptr;
+            }
             if (b->tbpar) {  // (the map kernel zeroes the scripts the segments OR into)
                 e = sed_launch_traceback_stripes(L, (uint32_t *)b->p_ops, (uint32_t *)b->d_tbmap.p, b->tbpar_items,
                                                  b->tbpar_kmax);
