@@ -5,7 +5,7 @@ SIMDs by design set their issue priority with s_setprio, and the config-4 forwar
   (SED_CKTB_PRIO; c4 9.74-9.86 against 9.91-10.32 ms at 0, profiles/r05/s15, s16);
 - sed_traceback_kernel (per-cell codes, integer batches only: a uniform branch on its ladder pattern): s_setprio 1;
 - sed_wf_f64_kernel (the fp64 DP beside the previous run's traceback): s_setprio 1;
-- the SPLIT forward (config 2's stripe waves): s_setprio 2;
+- the SPLIT forwards (config 2's stripe waves, and the fp64 SPLIT route's): s_setprio 2;
 - the checkpoint forward sed_wf_i32_kernel<16, ..., CK, DOT>: none (its waves must yield to the traceback's).
 A build with other -DSED_*_PRIO values, or a compiler that drops the builtin, fails here."""
 import os
@@ -50,3 +50,5 @@ def test_wave_priorities_in_code_object():
         assert prio.get(k) == {"2"}, (k, prio.get(k))
     for k in of("_Z17sed_wf_i32_kernelILi16ELb0ELb0ELb0ELb1ELb1E"):  # the config-4 forward
         assert not prio.get(k), (k, prio.get(k))
+    for k in of("_Z23sed_wf_f64_split_kernelILi2E"):  # fp64 SPLIT: its stripe waves are latency-bound too
+        assert prio.get(k) == {"2"}, (k, prio.get(k))
