@@ -97,6 +97,9 @@ enum {
                                    or dot keys with checkpoints and every 64 x 64 tile's codes are then recomputed at once
                                    for the stripe-parallel traceback (sed_batch_traceback_mode 4): 0 auto (on), 2 never
                                    (per-cell codes from the ladder-key forward) */
+#define SED_OPT_ZEROCOPY 15     /* small batches (the per-call path) whose kernels write results and scripts with plain
+                                   stores: the kernels write them into the batch's pinned host block, so no download
+                                   follows the run: 0 auto (on), 2 never */
 #define SED_OPT_DEBUG_CORRUPT 9 /* testing only: p + 1 overwrites one checkpoint word of pair p before its traceback,
                                    which must then fail with SED_E_DEVICE naming the pair; 0 off */
 

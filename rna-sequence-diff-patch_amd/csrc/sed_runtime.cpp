@@ -68,6 +68,7 @@ struct sed_ctx {
     int opt_seg = 0;            // SED_OPT_SEG: 0 auto (fp64 pairs the cost model prefers in 16-lane segments), 1 every
                                 // eligible pair, 2 never
     int opt_splitck = 0;        // SED_OPT_SPLITCK: 0 auto (on), 2 never (SPLIT script batches keep the per-cell-code forward)
+    int opt_zc = 0;             // SED_OPT_ZEROCOPY: 0 auto (small batches write results into pinned host memory), 2 never
     int opt_dot = 0;            // SED_OPT_DOT: 0 auto, 2 never (checkpoint batches keep the perm-based distance keys)    // SED_OPT_CHAIN_WAVES: cap on the persistent waves of dynamic CHAIN mode
     int opt_debug_corrupt = 0;  // SED_OPT_DEBUG_CORRUPT: pair + 1 whose sink-tile checkpoint is overwritten
     DevBuf selftest;
@@ -128,6 +129,12 @@ struct sed_batch {
     DevBuf d_small;
     bool small = false;
     size_t o_ops_small = 0;  // small batches: the scripts' offset from the results in d_small
+    // small batches whose kernels write their results and scripts with plain stores (not the stripe-parallel walk's
+    // atomicOr): the kernels write them straight into this pinned host block, so no download follows the run
+    // (sed_run_pair on a 30-nt pair: one copy kernel fewer per call)
+    void *h_out = nullptr;
+    size_t h_out_cap = 0;
+    bool zc = false;
     void *p_pd = nullptr, *p_seqa = nullptr, *p_seqb = nullptr, *p_tasks = nullptr, *p_lane = nullptr,
          *p_chain = nullptr, *p_x2 = nullptr, *p_ops = nullptr, *p_seg = nullptr, *p_res[3] = {nullptr, nullptr, nullptr};
     // timing events: 1 on every run (default), k > 1 on every k-th run, 0 never (sed_batch_set_timing; runs that
@@ -198,6 +205,7 @@ struct sed_batch {
 
     int cur() const { return (int)((runs - 1) % nbuf); }
     ~sed_batch() {
+        if (h_out) (void)hipHostFree(h_out);
         d_pd.release(); d_seqa.release(); d_seqb.release(); d_bnd.release(); d_ops.release(); d_tbmap.release();
         d_tasks.release(); d_lane.release(); d_chain.release(); d_x2.release(); d_small.release(); d_seg.release();
         for (int i = 0; i < 3; ++i) {
@@ -746,6 +754,10 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     std::vector<int2> tasks;
     std::vector<int32_t> lane_idx, seg_idx;
     // lane-per-pair kernels: integer keys (any flags), or fp64 distance-only in "simple typing" mode
+    // a batch of a few pairs (the per-call path) leaves the GPU empty, so one lane walking a pair alone only pays off
+    // for a small distance-only pair: a 30-nt script call took 42 us on the lane kernel and 34 us on the wave kernels,
+    // a 30-nt distance call 19 against 22 us (tools/zc_ab.py SED_OPT_LANE, profiles/r05/s38)
+    const bool few_pairs = npairs <= 16 && c->opt_lane == 0;
     const bool use_lane = !split && c->opt_lane != 2 &&
                           (mode == SED_MODE_I32 || (mode == SED_MODE_F64 && !want_tb && (flags & SED_NO_LEN)));
     uint64_t aw = 0, bw = 0, tbw = 0, bndw = 0, opw = 0, mapw = 0;
@@ -769,7 +781,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         d.bnd_off = bndw;
         d.ops_off = opw;
         d.map_off = (int32_t)mapw;  // stripe-parallel traceback: this pair's exit map
-        if (use_lane && nn >= 1 && nn <= SED_LANE_MAXN && mm >= 1 && mm <= SED_LANE_MAXM) {
+        if (use_lane && nn >= 1 && nn <= SED_LANE_MAXN && mm >= 1 && mm <= SED_LANE_MAXM &&
+            !(few_pairs && (want_tb || (double)nn * mm > 1024.0))) {
             d.lane = 1;
             lane_idx.push_back(p);
             if (want_tb) tbw += 2 * (uint64_t)nn;  // one uint2 of 2-bit ops per row
@@ -996,6 +1009,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
            o_ops = o_res + al(s_res),
            total = o_ops + al(4 * std::max<uint64_t>(1, opw));  // (results and scripts adjacent: one download)
     b->small = b->nbuf == 1 && total <= SED_SMALL_BATCH_BYTES;
+    b->zc = b->small && !b->tbpar && c->opt_zc != 2;
     bool okalloc = b->d_bnd.reserve(4 * std::max<uint64_t>(1, bndw)) && b->d_tbmap.reserve(4 * std::max<uint64_t>(1, mapw));
     if (b->small) {
         okalloc = okalloc && b->d_small.reserve(total);
@@ -1023,7 +1037,22 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         if (!x2.empty()) memcpy(h + o_x2, x2.data(), 4 * x2.size());
         if (!seg_idx.empty()) memcpy(h + o_seg, seg_idx.data(), 4 * seg_idx.size());
         memset(h + o_res, 0, s_res);
-        if ((e = hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+        const size_t up = b->zc ? o_res : total;  // (zero-copy results: the results and scripts stay in h_out)
+        if (b->zc) {
+            const size_t want = total - o_res;
+            if (want > b->h_out_cap) {
+                if (b->h_out) (void)hipHostFree(b->h_out);
+                b->h_out = nullptr;
+                b->h_out_cap = 0;
+                if ((e = hipHostMalloc(&b->h_out, std::max<size_t>(want, 1u << 16), hipHostMallocDefault)) != hipSuccess) {
+                    b->h_out = nullptr;
+                    return c->hipfail(e, "pinned results");
+                }
+                b->h_out_cap = std::max<size_t>(want, 1u << 16);
+            }
+            memset(b->h_out, 0, want);  // (the previous run of this batch has completed: fetch_results waited)
+        }
+        if ((e = hipMemcpyAsync(d, h, up, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
             return c->hipfail(e, "upload");
         c->pin_busy = true;
         b->p_pd = d + o_pd;
@@ -1034,8 +1063,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         b->p_lane = d + o_lane;
         b->p_x2 = d + o_x2;
         b->p_seg = d + o_seg;
-        b->p_res[0] = d + o_res;
-        b->p_ops = d + o_ops;
+        b->p_res[0] = b->zc ? b->h_out : d + o_res;
+        b->p_ops = b->zc ? (char *)b->h_out + (o_ops - o_res) : d + o_ops;
         b->o_ops_small = o_ops - o_res;
     } else {
         b->p_ops = b->d_ops.p;
@@ -1476,15 +1505,19 @@ int fetch_results(sed_batch *b, double *out_dist, uint8_t *out_is_int, int32_t *
         // every kernel ran on the context's stream: one download of the adjacent results and scripts into the pinned
         // staging, ordered after them, and one wait
         const size_t bytes = b->o_ops_small + (want_ops ? 4 * b->ops_words : 0);
-        if (bytes > c->pin_cap && (e = pin_reserve(c, bytes)) != hipSuccess) return c->hipfail(e, "pinned staging");
-        if (np && (e = hipMemcpyAsync(c->pin, b->p_res[0], bytes, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
-            return c->hipfail(e, "download results");
-        c->pin_busy = true;
+        const char *src = (const char *)b->h_out;
+        if (!b->zc) {
+            if (bytes > c->pin_cap && (e = pin_reserve(c, bytes)) != hipSuccess) return c->hipfail(e, "pinned staging");
+            if (np && (e = hipMemcpyAsync(c->pin, b->p_res[0], bytes, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+                return c->hipfail(e, "download results");
+            c->pin_busy = true;
+            src = (const char *)c->pin;
+        }
         int rc = sync_batch(b);
         if (rc != SED_OK) return rc;
         c->pin_busy = false;
-        hr = (const sed_result *)c->pin;
-        hops = (const uint32_t *)((const char *)c->pin + b->o_ops_small);
+        hr = (const sed_result *)src;
+        hops = (const uint32_t *)(src + b->o_ops_small);
     } else {
         int rc = sync_batch(b);
         if (rc != SED_OK) return rc;
@@ -1593,6 +1626,10 @@ int sed_set_option(sed_ctx *c, int key, int value) {
     }
     if (key == SED_OPT_SPLITCK && (value == 0 || value == 2)) {
         c->opt_splitck = value;
+        return SED_OK;
+    }
+    if (key == SED_OPT_ZEROCOPY && (value == 0 || value == 2)) {
+        c->opt_zc = value;
         return SED_OK;
     }
     if (key == SED_OPT_SCALED && (value == 0 || value == 2)) {

@@ -51,6 +51,7 @@ SED_OPT_BITPAR = 11
 SED_OPT_SCALED = 12
 SED_OPT_SEG = 13
 SED_OPT_SPLITCK = 14
+SED_OPT_ZEROCOPY = 15
 MODE_NAMES = {1: "i32", 2: "f64", 3: "f64-typed"}
 
 _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")

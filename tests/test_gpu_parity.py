@@ -149,6 +149,36 @@ def test_edge_lengths(gpu, tables):
             _oracle_check(tables[user], pairs, gpu_run(gpu, tables[user], pairs, mode=mode))
 
 
+def test_zero_copy_results_match_download(gpu, tables):
+    """Small batches (the per-call path) have their kernels write results and scripts straight into pinned host
+    memory (SED_OPT_ZEROCOPY); every small-batch route gives the same answer as with the download: integer lane and
+    wave pairs, fp64 SPLIT, the window traceback (65..256 pairs), distance-only and scripts, empty sides.  The
+    stripe-parallel walk (<= 64 pairs, atomicOr on the script words) keeps the download."""
+    rng = np.random.default_rng(9500)
+    acgu = [("".join(rng.choice(list("ACGU"), size=int(rng.integers(1, 40)))),
+             "".join(rng.choice(list("ACGU"), size=int(rng.integers(1, 40))))) for _ in range(80)]
+    acgu += [("ACGU" * 80, "AGU" * 90), ("", "ACG"), ("GGA", ""), ("", "")]
+    iupac = _random_pairs(9600, 70, IUPAC, 1, 300, related=True) + [("", "ACG"), ("GUA" * 50, "")]
+    for table, pairs in ((tables[True], acgu), (tables[False], acgu[:5]), (tables[False], iupac), (tables[False], iupac[:3])):
+        for flags in (dict(script=True), dict(script=False), dict(script=False, no_len=True)):
+            got = gpu_run(gpu, table, pairs, **flags)
+            gpu.set_option(sedgpu.SED_OPT_ZEROCOPY, 2)
+            try:
+                assert gpu_run(gpu, table, pairs, **flags) == got, (len(pairs), flags)
+            finally:
+                gpu.set_option(sedgpu.SED_OPT_ZEROCOPY, 0)
+            _oracle_check(table, pairs, got, no_len=flags.get("no_len", False))
+    # one pair per call through sed_run_pair, repeated (the batch's pinned block is reused)
+    plan = sedcost.build_plan(tables[False], [a for a, _ in iupac], [b for _, b in iupac])
+    gpu.set_costs(plan)
+    cs = oracle.Costs.from_plan(plan)
+    for a, y in iupac[:20]:
+        d, ii, ln, ops = gpu.run_pair(plan.encode_bytes(a), plan.encode_bytes(y), True)
+        o = oracle.pair(cs, plan.encode(a), plan.encode(y))
+        assert (d, bool(ii), ln) == (o["dist"], bool(o["is_int"]), o["len"])
+        assert "".join(OPCH[c] for c in sedgpu.unpack_ops(ops, np.zeros(1, np.int64), 0, ln)) == oracle.ops_to_str(o["ops"])
+
+
 def test_full_matrix_g1(gpu, tables):
     for r in load_golden("g1_small.json")[::3]:
         plan = sedcost.build_plan(tables[r["user"]], [r["s1"]], [r["s2"]])
