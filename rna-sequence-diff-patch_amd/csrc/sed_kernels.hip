@@ -1733,10 +1733,13 @@ __global__ __launch_bounds__(128) void sed_wf_f64_split_kernel(const sed_pair_de
     const uint32_t tag = prm.epoch;
     bool ok = true;
     int ready = 0;  // steps the feeder has published as ready (last read)
-    for (int s = 0; s < SG; s += G) {
-        if (ready < s + G) {  // the ring holds this group's top-row cells (LDS only)
+    constexpr int HB = G < 16 ? G : 16;  // steps per block of ring reads, waits and hand-offs
+    // until the ring holds the top-row cells of steps < upto (LDS only)
+    auto wait_ready = [&](int upto) {
+        upto = min(upto, SG);  // (the feeder publishes SG steps in all)
+        if (ready < upto) {
             uint32_t f = lds_flag_get(split_flag), spins = 0;
-            while (ok && (int)(f & ~SED_PROG_POISON) < s + G) {
+            while (ok && (int)(f & ~SED_PROG_POISON) < upto) {
                 if (++spins > (1u << 24)) ok = false;
                 __builtin_amdgcn_s_sleep(1);
                 f = lds_flag_get(split_flag);
@@ -1745,20 +1748,42 @@ __global__ __launch_bounds__(128) void sed_wf_f64_split_kernel(const sed_pair_de
             ready = (int)(f & ~SED_PROG_POISON);
             asm volatile("" ::: "memory");
         }
+    };
+    // lane u < HB hands off column s0 + u - 62 (lane 63's cell of step s0 + u, staged at rg.od[u0 + u]), then the
+    // block's ring slots are free again
+    auto handoff = [&](const int s0, const int u0) {
+        if (!last && lane < HB) {
+            const int col = s0 + lane - 62;
+            if (col >= 1 && col <= m) {
+                const uint32_t tg = tag | (ok ? 0u : SED_PROG_POISON);
+                const uint64_t bits = (uint64_t)__double_as_longlong(rg.od[u0 + lane][63]);
+                const uint32_t lt = rg.ol[u0 + lane][63] | (TYPED ? rg.ot[u0 + lane][63] : 0u);
+                store_tagged(hout + (uint32_t)(col + 64), tg, (uint32_t)bits);
+                store_tagged(hout + plane_words + (uint32_t)(col + 64), tg, (uint32_t)(bits >> 32));
+                store_tagged(hout + 2u * plane_words + (uint32_t)(col + 64), tg, lt);
+            }
+        }
+        asm volatile("" ::: "memory");
+        if (lane == 0) lds_flag_set(split_flag + 1, (uint32_t)(s0 + HB));
+    };
+    for (int s = 0; s < SG; s += G) {
+        // a block needs its own steps and the next block's first symbol (the table reads a step ahead)
+        wait_ready(s + (HB < G ? HB + 1 : HB));
         // the group's steps as one straight-line block per variant (a lone wave is latency-bound: a branch per step
         // kept the compiler from overlapping one step's table reads with the previous step's arithmetic)
         // The group's top-row cells and symbols are read from the ring at its start, and each step's column symbol
         // and table entries are fetched one step ahead (PF).
-        // (ring entries in blocks of 16 steps: the R = 2 group's 32 would take ~160 VGPRs at once)
+        // (ring entries in blocks of 16 steps: the R = 2 group's 32 would take ~160 VGPRs at once; each block waits
+        // for its own steps and hands its bottom cells off, so the stripe below trails by 16 steps, not 32)
         auto group = [&](auto masked_tag) {
             constexpr bool MASKED = decltype(masked_tag)::value;
-            constexpr int HB = G < 16 ? G : 16;
             double2 en[R];
             uint32_t bn = dpp_shr1(rg.s[s & (SED_F64_RING - 1)], bsel);
 #pragma unroll
             for (int r = 0; r < R; ++r) en[r] = tab[rowbase[r] + bn];
 #pragma unroll
             for (int h = 0; h < G; h += HB) {
+                if (h > 0) wait_ready(s + h + (h + HB < G ? HB + 1 : HB));
                 double dg[HB];
                 uint32_t lg[HB], tg[HB], sg[HB + 1];
 #pragma unroll
@@ -1796,6 +1821,7 @@ __global__ __launch_bounds__(128) void sed_wf_f64_split_kernel(const sed_pair_de
                     if (TYPED) rg.ot[u][lane] = tbot;
                     __builtin_amdgcn_sched_barrier(0);  // (the next step's table reads stay a step ahead of their use)
                 }
+                handoff(s + h, h);
             }
         };
         if ((s >= 63) && (s + G - 1 < m))
@@ -1803,19 +1829,6 @@ __global__ __launch_bounds__(128) void sed_wf_f64_split_kernel(const sed_pair_de
         else
             group(BoolTag<true>{});
         if constexpr (TB) store_tb(tbk + ((uint64_t)(s / G) * 64u + lane) * 4u, W);
-        if (!last && lane < G) {  // lane u hands off column s + u - 62 (lane 63's cell of step s + u)
-            const int col = s + lane - 62;
-            if (col >= 1 && col <= m) {
-                const uint32_t tg = tag | (ok ? 0u : SED_PROG_POISON);
-                const uint64_t bits = (uint64_t)__double_as_longlong(rg.od[lane][63]);
-                const uint32_t lt = rg.ol[lane][63] | (TYPED ? rg.ot[lane][63] : 0u);
-                store_tagged(hout + (uint32_t)(col + 64), tg, (uint32_t)bits);
-                store_tagged(hout + plane_words + (uint32_t)(col + 64), tg, (uint32_t)(bits >> 32));
-                store_tagged(hout + 2u * plane_words + (uint32_t)(col + 64), tg, lt);
-            }
-        }
-        asm volatile("" ::: "memory");
-        if (lane == 0) lds_flag_set(split_flag + 1, (uint32_t)(s + G));  // this group's ring slots are free again
     }
     if (last) {
         const int w = (n - 1) % ROWS;
