@@ -1,0 +1,119 @@
+"""Time-bounded randomized route fuzz (GPU): random batches through the C-ABI against the C oracle, bit for bit.
+
+Every iteration draws a cost table (costs.json, user_costs.json or one of the G8 GUI tables), an alphabet (ACGU or
+the table's whole alphabet), a batch size around the routing thresholds (1, 16, 17, 64, 65, 256, 257 ... pairs),
+ragged lengths (empty sides included, now and then a pair past 1000 rows), a flag set (script, distance with length,
+distance only) and a routing override (SPLIT on / off, lane kernels off, rows per lane, fp64 forced, zero-copy off,
+16-lane segments on / off, per-cell codes or checkpoints, SPLIT's ladder-key forward), then compares every pair's distance, typing, length and script with the oracle
+(oracle/sed_oracle.c: StringEditDistance.py:92-334).  SED_FUZZ_SECONDS sets the budget (default 20 s) and
+SED_FUZZ_SEED the first seed (default 2026), so the default run is reproducible; a failure names its seed.
+"""
+import os
+import time
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+import oracle
+import sedcost
+import sedgpu
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [1, 1, 2, 3, 5, 16, 17, 40, 64, 65, 100, 256, 257, 300]
+OPTIONS = [
+    (None, 0),
+    (sedgpu.SED_OPT_SPLIT, 1), (sedgpu.SED_OPT_SPLIT, 2),
+    (sedgpu.SED_OPT_LANE, 2),
+    (sedgpu.SED_OPT_ROWS_PER_LANE, 4), (sedgpu.SED_OPT_ROWS_PER_LANE, 8),
+    (sedgpu.SED_OPT_ZEROCOPY, 2),
+    (sedgpu.SED_OPT_SEG, 1), (sedgpu.SED_OPT_SEG, 2),
+    (sedgpu.SED_OPT_TB, 1), (sedgpu.SED_OPT_TB, 2),
+    (sedgpu.SED_OPT_SPLITCK, 2),
+    ("mode", 2), ("mode", 3),  # the fp64 kernels forced (simple / full typing)
+]
+CELL_CAP = 2.5e7  # oracle work per iteration
+
+
+def _tables():
+    out = [("costs.json", load_golden("costs.json")), ("user_costs.json", load_golden("user_costs.json"))]
+    out += sorted(load_golden("g8_cost_tables.json")["tables"].items())
+    return out
+
+
+def _batch(rng, alphabet):
+    npairs = int(rng.choice(SIZES))
+    related = rng.random() < 0.5
+    pairs, cells = [], 0.0
+    for _ in range(npairs):
+        r = rng.random()
+        hi = 40 if r < 0.4 else (600 if r < 0.93 else 1500)
+        n = int(rng.integers(0, hi + 1))
+        m = int(rng.integers(0, hi + 1)) if not related else max(0, n + int(rng.integers(-n // 8 - 1, n // 8 + 2)))
+        if cells + n * m > CELL_CAP:
+            n, m = min(n, 40), min(m, 40)
+        cells += n * m
+        a = "".join(rng.choice(alphabet, size=n))
+        if related:
+            b = "".join(c if rng.random() > 0.15 else rng.choice(alphabet) for c in a)[:m]
+            b += "".join(rng.choice(alphabet, size=max(0, m - len(b))))
+        else:
+            b = "".join(rng.choice(alphabet, size=m))
+        pairs.append((a, b))
+    return pairs
+
+
+def _check(gpu, table, pairs, script, no_len, opt, seed):
+    plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
+    gpu.set_costs(plan)
+    key, val = opt
+    if key == "mode":
+        gpu.set_mode(val)
+    elif key is not None:
+        gpu.set_option(key, val)
+    try:
+        packed = sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs], [plan.encode(b) for _, b in pairs])
+        dist, is_int, ln, ops = gpu.run(packed, script, no_len=no_len)
+    finally:
+        if key == "mode":
+            gpu.set_mode(0)
+        elif key is not None:
+            gpu.set_option(key, 0)
+    cs = oracle.Costs.from_plan(plan)
+    for p, (a, b) in enumerate(pairs):
+        o = oracle.pair(cs, plan.encode(a), plan.encode(b), want_ops=script)
+        where = "seed %d, pair %d of %d (%d x %d), script %s, no_len %s, option %s" % (
+            seed, p, len(pairs), len(a), len(b), script, no_len, opt)
+        assert (float(dist[p]), bool(is_int[p])) == (o["dist"], bool(o["is_int"])), where
+        if not no_len or script:
+            assert int(ln[p]) == o["len"], where
+        if script:
+            got = sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln[p]))
+            assert np.array_equal(got, o["ops"]), where
+
+
+def test_route_fuzz_vs_oracle(gpu):
+    budget = float(os.environ.get("SED_FUZZ_SECONDS", "20"))
+    seed = int(os.environ.get("SED_FUZZ_SEED", "2026"))
+    tabs = _tables()
+    t_end = time.monotonic() + budget
+    t_note = time.monotonic() + 20.0
+    runs = 0
+    while time.monotonic() < t_end or runs < 8:
+        if time.monotonic() > t_note:  # (progress for long budgets)
+            print("route fuzz: %d batches, seed %d" % (runs, seed), flush=True)
+            t_note += 20.0
+        rng = np.random.default_rng(seed)
+        name, table = tabs[int(rng.integers(0, len(tabs)))]
+        full = [s for s in table["update"] if all(s in table["update"][t] for t in table["update"])]
+        acgu = [s for s in "ACGU" if s in full]
+        alphabet = list(acgu if (rng.random() < 0.5 and len(acgu) == 4) else full)
+        pairs = _batch(rng, alphabet)
+        mode = int(rng.integers(0, 3))
+        script, no_len = (True, False) if mode == 0 else ((False, False) if mode == 1 else (False, True))
+        opt = OPTIONS[int(rng.integers(0, len(OPTIONS)))]
+        _check(gpu, table, pairs, script, no_len, opt, seed)
+        seed += 1
+        runs += 1
+    print("route fuzz: %d batches" % runs)
