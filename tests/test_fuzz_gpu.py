@@ -117,3 +117,48 @@ def test_route_fuzz_vs_oracle(gpu):
         seed += 1
         runs += 1
     print("route fuzz: %d batches" % runs)
+
+
+def test_module_fuzz_vs_pyref():
+    """The drop-in module's calls as the reference's callers make them, on random short pairs, against the
+    pure-Python node graph (oracle/pyref.py, pinned to the reference's fixtures by tests/test_pyref.py):
+    wagnerFisher's sink value and int/float typing, create_paths(dp)[0] and generate_es, then generate_rev_es and
+    patching back to str1 (StringEditDistance.py:133-457).  SED_FUZZ_MODULE_SECONDS sets the budget (default 8 s)."""
+    import importlib
+    import sys
+    from conftest import GOLDEN
+    import pyref
+    cwd = os.getcwd()
+    os.chdir(GOLDEN)
+    try:
+        sys.modules.pop("StringEditDistance", None)
+        SED = importlib.import_module("StringEditDistance")
+    finally:
+        os.chdir(cwd)
+    tables = {False: load_golden("costs.json"), True: load_golden("user_costs.json")}
+    iupac = list("AGCUYRWSKMDVHBN")
+    rng = np.random.default_rng(int(os.environ.get("SED_FUZZ_SEED", "2026")) + 7)
+    t_end = time.monotonic() + float(os.environ.get("SED_FUZZ_MODULE_SECONDS", "8"))
+    runs = 0
+    while time.monotonic() < t_end or runs < 20:
+        user = bool(rng.random() < 0.5)
+        al = list("ACGU") if rng.random() < 0.5 else iupac
+        n, m = int(rng.integers(0, 48)), int(rng.integers(0, 48))
+        s1 = "".join(rng.choice(al, size=n))
+        s2 = "".join(c if rng.random() > 0.2 else rng.choice(al) for c in s1)[:m] if rng.random() < 0.5 else \
+            "".join(rng.choice(al, size=m))
+        v, ops, es = pyref.run_pair(s1, s2, tables[user])
+        dp = SED.wagnerFisher(s1, s2, user)
+        got = dp[len(dp) - 1][len(dp[0]) - 1].value
+        assert (got, type(got)) == (v, type(v)), (s1, s2, user)
+        if s1 and s2:
+            path = SED.create_paths(dp)[0]
+            steps = [(b.i - a.i, b.j - a.j) for a, b in zip(path, path[1:])]
+            assert "".join("u" if st == (1, 1) else ("d" if st[0] else "i") for st in steps) == ops, (s1, s2, user)
+            got_es = SED.generate_es(path, s1, s2)
+            assert got_es == es, (s1, s2, user)
+            # (patching returns (error code, string), StringEditDistance.py:457)
+            assert SED.patching(SED.generate_rev_es(got_es), s2) == (0, s1), (s1, s2, user)
+            assert SED.patching(got_es, s1) == (0, s2), (s1, s2, user)
+        runs += 1
+    print("module fuzz: %d pairs" % runs)
