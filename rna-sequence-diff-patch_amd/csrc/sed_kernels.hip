@@ -1576,14 +1576,16 @@ __global__ __launch_bounds__(256) void sed_wf_f64_kernel(const sed_pair_desc *__
 
 // SPLIT fp64 (few long pairs: timing.py's one-call loop, GUI calls over IUPAC symbols).  A lone fp64 wave issues
 // ~20 dependent VALU per cell on one SIMD (a 2000^2 pair took 3.5 ms), so, as in the integer SPLIT kernel, each
-// stripe of 64 R rows is a 128-thread workgroup of its own: all stripes of a pair run at once, each a group or two
-// behind the stripe above.  The hand-off is the integer kernel's tagged words: lane 63's bottom cell of column j
+// stripe of 64 R rows (R = 2 by default, 4 on request) is a 128-thread workgroup of its own: all stripes of a pair
+// run at once, each ~63 steps (its lanes' systolic depth) plus a 16-step block and the hand-off's latency behind the
+// stripe above.  The hand-off is the integer kernel's tagged words: lane 63's bottom cell of column j
 // travels as three relaxed agent-scope 64-bit stores {tag, D low}, {tag, D high}, {tag, L key | T} (the L key is a
 // multiple of 4, so its bit 0 carries the typing bit), each single-copy atomic and validated on its own, tag = the
 // run's epoch | poison << 31.  The feeder wave (f64_split_feed) polls the stripe above's words, writes the steps'
 // top-row cells and str2 symbols into an LDS ring and publishes how many steps are ready; stripe 0's feeder writes
-// the row-0 border.  The compute wave is sed_wf_f64_kernel's stripe loop (SW = 64) reading the ring.  Codes, the
-// bottom-row-free layout and the result are the one-wave kernel's, so the tracebacks read them unchanged.
+// the row-0 border.  The compute wave is sed_wf_f64_kernel's stripe loop (SW = 64) reading the ring, with each step's
+// column symbol and table entries read a step ahead (f64_step PF).  Codes, their layout and the result are the
+// one-wave kernel's, so the tracebacks read them unchanged.
 #define SED_F64_RING 256
 template <int G> struct f64_split_lds {
     double d[SED_F64_RING];
