@@ -2098,7 +2098,7 @@ template <int R> struct CodeCursor {  // per-lane reader of one pair's per-cell 
 
 // map[pd.map_off + 2 * (k * (m + 1) + x)] = {exit column, ops} for stripes 1 .. K-2; the sink's stripe at x = 0.
 // A workgroup takes 256 consecutive columns x0 .. x0+255 of one stripe.  Paths near the diagonal stay in the
-// stripe's 64R rows and within SED_TBMAP_LEFT columns left of x0: the code groups of those steps are one
+// stripe's 64R rows and within SED_TBMAP_LEFT (R = 2: SED_TBMAP_LEFT_R2) columns left of x0: the code groups of those steps are one
 // contiguous run of 1 KiB groups (layout [group][64 lanes][16 B]), copied to LDS once, so a step reads LDS
 // instead of waiting on a global load (a wave's lanes need new blocks at different steps: with global loads
 // nearly every step waited on one).  A path that leaves the staged steps (cells far from the diagonal insert
@@ -2106,8 +2106,19 @@ template <int R> struct CodeCursor {  // per-lane reader of one pair's per-cell 
 // marked unknown (exit 0xFFFFFFFF) and the emit kernel walks that stripe itself if the real path needs it.
 // The last workgroup of a pair walks the sink's stripe from the sink.  Every workgroup also zeroes its share
 // of the pair's script words, which the emit kernel's segments OR into (lane-kernel pairs wrote theirs already).
+#ifndef SED_TBMAP_LEFT
 #define SED_TBMAP_LEFT 512
+#endif
+// R = 2 (the fp64 SPLIT route's 128-row stripes): a path crosses its stripe within fewer columns, and the map's time is
+// its longest walks (lanes far from the path, running left through the staged columns): 1000^2 per call 400 -> 360 us,
+// 2000^2 629 -> 587 us at 192 (tools/script_calls.py, profiles/r05/s47); the 256-row stripes of config 2 keep 512
+// (at 192 its path needed columns past the staged ones, and the emit kernel's fallback walks took 187 against 53 us)
+#ifndef SED_TBMAP_LEFT_R2
+#define SED_TBMAP_LEFT_R2 192
+#endif
+#ifndef SED_TBMAP_RUN
 #define SED_TBMAP_RUN 96
+#endif
 template <int R>
 __global__ __launch_bounds__(256) void sed_tb_stripemap_kernel(const sed_pair_desc *__restrict__ pd,
                                                                const uint32_t *__restrict__ tb,
@@ -2115,7 +2126,8 @@ __global__ __launch_bounds__(256) void sed_tb_stripemap_kernel(const sed_pair_de
                                                                uint32_t *__restrict__ ops, const uint64_t pat) {
     constexpr int ROWS = 64 * R, G = Grp<R>::G, LG = CodeCursor<R>::LG, LR = CodeCursor<R>::LR;
     constexpr int P = Ladder<R>::P;
-    constexpr int NSG = (SED_TBMAP_LEFT + 256 + 64 + 2 * G) / G + 1;  // staged step groups
+    constexpr int LEFT = R == 2 ? SED_TBMAP_LEFT_R2 : SED_TBMAP_LEFT;
+    constexpr int NSG = (LEFT + 256 + 64 + 2 * G) / G + 1;  // staged step groups
     constexpr int NIT = (NSG * 64 + 255) / 256;  // staging trips of the 256 threads
     __shared__ uint4 stage[NIT * 256];
     const __attribute__((address_space(3))) uint32_t *stage32 =
@@ -2153,7 +2165,7 @@ __global__ __launch_bounds__(256) void sed_tb_stripemap_kernel(const sed_pair_de
     }
     // stage the groups of steps s = j' - 1 + t, j' in [x0 - LEFT, x0 + 255], t in [0, 63]
     const uint32_t *tbk = tb + d.tb_off + (uint64_t)k * stripe_words;
-    const int s_lo = max(0, x0 - SED_TBMAP_LEFT - 1), s_hi = min(SG - 1, x0 + 255 + 63);
+    const int s_lo = max(0, x0 - LEFT - 1), s_hi = min(SG - 1, x0 + 255 + 63);
     const int sg_lo = s_lo >> LG, nsg = min(NSG, (s_hi >> LG) - sg_lo + 1);
     const uint4 *src = reinterpret_cast<const uint4 *>(tbk) + (uint64_t)sg_lo * 64u;
     {  // fixed trip count, unguarded stores (clamped loads fill the tail): every load is in flight before the first
