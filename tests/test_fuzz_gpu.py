@@ -139,8 +139,12 @@ def test_module_fuzz_vs_pyref():
     iupac = list("AGCUYRWSKMDVHBN")
     rng = np.random.default_rng(int(os.environ.get("SED_FUZZ_SEED", "2026")) + 7)
     t_end = time.monotonic() + float(os.environ.get("SED_FUZZ_MODULE_SECONDS", "8"))
+    t_note = time.monotonic() + 20.0
     runs = 0
     while time.monotonic() < t_end or runs < 20:
+        if time.monotonic() > t_note:  # (progress for long budgets)
+            print("module fuzz: %d pairs" % runs, flush=True)
+            t_note += 20.0
         user = bool(rng.random() < 0.5)
         al = list("ACGU") if rng.random() < 0.5 else iupac
         n, m = int(rng.integers(0, 48)), int(rng.integers(0, 48))
