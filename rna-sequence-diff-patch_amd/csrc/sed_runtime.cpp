@@ -831,6 +831,13 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     // a SPLIT script batch whose pairs all have an empty side has no tile to recompute: plain per-cell codes (the
     // traceback walks only the border)
     if (b->split_ck && b->ck_tiles == 0) b->split_ck = false;
+    // no pair with 3 stripes or more: the stripe map has nothing to do and the emit kernel walks every pair in one
+    // segment, as the window traceback does without the map launch and the OR into zeroed scripts (so zero-copy
+    // results apply)
+    if (b->tbpar && b->tbpar_kmax < 3 && tbpar_env < 0) {
+        b->tbpar = false;
+        b->tbpar_items = b->tbpar_kmax = 0;
+    }
     // algorithmic traceback bytes: the 2-bit choice of every cell, or (CK) the checkpoints written
     tb_bytes = b->ck ? ck_bytes : cells * 0.25;
     b->tb_words = tbw;

@@ -1,6 +1,6 @@
-"""A few long script calls through sed_run_pair (run under rocprofv3 --kernel-trace to see the traceback kernels):
-config 2's pair (4096^2, user_costs, integer SPLIT with checkpoints) and fp64 IUPAC pairs of 1000^2 and 2000^2
-(costs.json, fp64 SPLIT), five calls each.
+"""A few script calls through sed_run_pair (run under rocprofv3 --kernel-trace to see the traceback kernels):
+config 2's pair (4096^2, user_costs, integer SPLIT with checkpoints), integer pairs of 100^2 and 250^2 (one wave,
+per-cell codes) and fp64 IUPAC pairs of 1000^2 and 2000^2 (costs.json, fp64 SPLIT), five calls each.
 
     python tools/script_calls.py
 """
@@ -26,6 +26,10 @@ def main():
     SED.wagnerFisher("AGRGA", "AGGGAA")
     s1, s2 = synth.pair_strings(0, 4096, 4096)
     cases = [("4096^2 integer", SED._table(True), s1, s2)]
+    for n in (100, 250):
+        a = "".join(random.choice("ACGU") for _ in range(n))
+        b = "".join(c if random.random() > 0.1 else random.choice("ACGU") for c in a)
+        cases.append(("%d^2 integer" % n, SED._table(True), a, b))
     for n in (1000, 2000):
         a = "".join(random.choice(NUC) for _ in range(n))
         b = "".join(c if random.random() > 0.2 else random.choice(NUC) for c in a)
