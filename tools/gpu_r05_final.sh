@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-5 evidence: full GPU suite, smoke, the default bench line (PMC traffic + issue passes, both CPU legs), every
-# other workload with its oracle sample, the per-call latency, the unchanged callers' process model and timing.py loop, fp64 per-call latency by length, the self-launched 2-rank gloo rehearsal, c4 kernel
+# other workload with its oracle sample, the per-call latency, the unchanged callers' process model and timing.py loop, fp64 per-call latency by length, script calls, the self-launched 2-rank gloo rehearsal, c4 kernel
 # traces (2 parts; 1 part = SED_CK_HALVES=1, no overlap) and an SQ pass
 set -e
 O=gpurun_out/${1:-r05final}
@@ -18,6 +18,7 @@ timeout -k 10 200 python3 tools/call_latency.py > $O/call_latency.txt 2>&1
 timeout -k 10 300 python3 tools/caller_paths.py $O/caller_paths.json > $O/caller_paths.txt 2>&1
 timeout -k 10 300 python3 tools/timing_breakdown.py $O/timing_breakdown.txt > /dev/null 2>&1
 timeout -k 10 200 python3 tools/fp64_call_scaling.py $O/fp64_call_scaling.txt > /dev/null 2>&1
+timeout -k 10 200 python3 tools/script_calls.py > $O/script_calls.txt 2>&1
 timeout -k 10 400 python3 bench.py --gpus 2 --dist-backend gloo --traffic none --no-cpu-baseline > $O/dist2_c4_gloo.json 2> $O/dist2.log
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -T -d $O/kt_c4 -o kt --output-format csv -- python3 bench.py --steps 10 --warmup 1 --no-cpu-baseline --traffic none > $O/kt_c4.json 2> $O/kt_c4.log
 SED_CK_HALVES=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats -T -d $O/kt_c4_1part -o kt --output-format csv -- python3 bench.py --steps 10 --warmup 1 --no-cpu-baseline --traffic none > $O/kt_c4_1part.json 2> $O/kt_c4_1part.log
