@@ -427,6 +427,32 @@ def test_stripe_parallel_traceback(gpu, tables, R, split):
         gpu.set_option(sedgpu.SED_OPT_SPLIT, 0)
 
 
+def test_stripe_walk_only_with_three_stripes(gpu, tables):
+    """A few-pair script batch at R = 4 whose pairs all have fewer than 3 stripes (<= 512 rows) has no stripe map
+    to build: it takes the window walk (traceback_mode 1, zero-copy results); one pair of 3 stripes brings the
+    stripe-parallel walk (mode 3) back.  Both against the oracle."""
+    rng = np.random.default_rng(5400)
+    shapes = [(100, 100), (250, 240), (512, 700), (1, 3000), (300, 0)]
+    plan = _plan(tables[True])
+    gpu.set_costs(plan)
+    gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 4)
+    gpu.set_option(sedgpu.SED_OPT_SPLIT, 2)
+    try:
+        for extra, want in (([], 1), ([(513, 600)], 3)):
+            A = [rng.integers(0, 4, size=n).astype(np.uint8) for n, _ in shapes + extra]
+            B = [rng.integers(0, 4, size=m).astype(np.uint8) for _, m in shapes + extra]
+            packed = sedgpu.PackedPairs(A, B)
+            b, (d, ii, ln, ops) = _batch_run(gpu, packed, True, runs=2)
+            try:
+                assert b.traceback_mode == want
+            finally:
+                b.close()
+            _check_all(plan, packed, d, ii, ln, ops, script=True)
+    finally:
+        gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
+        gpu.set_option(sedgpu.SED_OPT_SPLIT, 0)
+
+
 def _same(out, ref, ops_off):
     """Identical results; scripts compared op by op (words past a script's length are unused padding)."""
     for name, x, y in zip(("dist", "is_int", "len"), out, ref):
