@@ -2116,6 +2116,9 @@ template <int R> struct CodeCursor {  // per-lane reader of one pair's per-cell 
 #ifndef SED_TBMAP_LEFT_R2
 #define SED_TBMAP_LEFT_R2 192
 #endif
+#ifndef SED_TBMAP_BANDS  // 1: band maps + compose (sed_tb_bandmap_kernel), 0: one lane per stripe (A/B)
+#define SED_TBMAP_BANDS 1
+#endif
 #ifndef SED_TBMAP_RUN
 #define SED_TBMAP_RUN 96
 #endif
@@ -2210,6 +2213,137 @@ __global__ __launch_bounds__(256) void sed_tb_stripemap_kernel(const sed_pair_de
     uint32_t *mp = map + (uint32_t)d.map_off + 2u * (uint32_t)slot;
     mp[0] = (uint32_t)j;  // 0xFFFFFFFF: unknown
     mp[1] = cnt;
+}
+
+// Band maps (round 5, SED_TBMAP_BANDS = 1, the default): the map kernel above gives one lane a whole stripe, a
+// chain of up to ~700 dependent LDS steps at about one wave per SIMD (config 2: 104 us).  Here a lane walks one
+// 64-row band (band g: rows 64g + 1 .. 64g + 64, from its last row, or from the sink in the sink's band) for every
+// band of stripes 1 .. K-1 and every column: 4x (R = 4) the lanes at 1/4 the chain, each workgroup staging only its
+// band's 64/R forward lanes of the code groups (1/4 the LDS, so many workgroups per CU).  band map entry
+// bm[(g - NB) * (m + 1) + x] = {exit column at row 64g, ops}, or unknown; it follows the stripe map's K (m + 1)
+// entries.  sed_tb_bandcompose_kernel then chains a stripe's NB bands into the stripe map the emit kernel reads.
+template <int R>
+__global__ __launch_bounds__(256) void sed_tb_bandmap_kernel(const sed_pair_desc *__restrict__ pd,
+                                                             const uint32_t *__restrict__ tb,
+                                                             uint32_t *__restrict__ map,
+                                                             uint32_t *__restrict__ ops, const uint64_t pat) {
+    constexpr int ROWS = 64 * R, NB = R, NL = 64 / R, G = Grp<R>::G, LG = CodeCursor<R>::LG, LR = CodeCursor<R>::LR;
+    constexpr int P = Ladder<R>::P;
+    constexpr int LEFT = R == 2 ? SED_TBMAP_LEFT_R2 : SED_TBMAP_LEFT;
+    constexpr int NSG = (LEFT + 256 + 64 + 2 * G) / G + 1;  // staged step groups
+    constexpr int NIT = (NSG * NL + 255) / 256;  // staging trips of the 256 threads
+    __shared__ uint4 stage[NIT * 256];
+    const __attribute__((address_space(3))) uint32_t *stage32 =
+        (const __attribute__((address_space(3))) uint32_t *)(stage);
+    const int p = blockIdx.y;
+    const sed_pair_desc d = pd[p];
+    const int n = d.n, m = d.m;
+    if (d.lane) return;
+    const int tid = threadIdx.x, idx = blockIdx.x * 256 + tid;
+    if (idx < (n + m + 15) / 16) ops[d.ops_off + idx] = 0u;
+    if (n == 0 || m == 0) return;
+    const int K = (n + ROWS - 1) / ROWS;
+    if (K < 3) return;  // walked whole by the emit kernel
+    const int nx = m + 1, nxc = (nx + 255) / 256, nbt = (n + 63) / 64;  // bands NB .. nbt-1 are mapped
+    const int blk = blockIdx.x;
+    if (blk >= (nbt - NB) * nxc) return;
+    const int g = NB + blk / nxc, x0 = (blk % nxc) * 256;
+    const int k = g / NB, t0 = (g % NB) * NL;  // the band's stripe and first forward lane
+    const int SG = (m + 63 + G - 1) / G * G;
+    const uint64_t stripe_words = (uint64_t)(SG / G) * 256u;
+    int j = x0 + tid, i = min(64 * (g + 1), n);
+    const bool live = j <= m;
+    // stage the band's lanes of the groups of steps s = j' - 1 + t, j' in [x0 - LEFT, x0 + 255], t in [0, 63]
+    const uint32_t *tbk = tb + d.tb_off + (uint64_t)k * stripe_words;
+    const int s_lo = max(0, x0 - LEFT - 1), s_hi = min(SG - 1, x0 + 255 + 63);
+    const int sg_lo = s_lo >> LG, nsg = min(NSG, (s_hi >> LG) - sg_lo + 1);
+    const uint4 *src = reinterpret_cast<const uint4 *>(tbk) + (uint64_t)sg_lo * 64u + t0;
+    {  // as in the stripe map kernel: every load in flight before the first wait
+        uint4 v[NIT];
+#pragma unroll
+        for (int u = 0; u < NIT; ++u) {
+            const int e = tid + 256 * u;
+            v[u] = src[e < nsg * NL ? (e / NL) * 64 + (e % NL) : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < NIT; ++u) stage[tid + 256 * u] = v[u];
+    }
+    __syncthreads();
+    if (!live) return;
+    const int top = 64 * g;  // row top belongs to band g - 1
+    uint32_t cnt = 0, run = 0;  // run: consecutive inserts
+    for (;;) {  // the stripe map kernel's loop on the band's staged lanes
+        const int rr = i - 1, t = (rr >> LR) & 63, r = rr & (R - 1);
+        const int s = j - 1 + t;
+        const uint32_t c = ((uint32_t)(s & (G - 1)) << LR) | (uint32_t)r;
+        const uint32_t rel = (uint32_t)((s >> LG) - sg_lo);
+        const bool inside = rel < (uint32_t)nsg;
+        // (t - t0) & (NL - 1): the read after the exit row (t outside the band) stays inside the staged lanes
+        const uint32_t word = stage32[(inside ? rel : 0u) * (NL * 4u) + ((uint32_t)(t - t0) & (NL - 1u)) * 4u + (c >> 4)];
+        if (!((i > top) & (j > 0) & inside & (run <= SED_TBMAP_RUN))) break;
+        const uint32_t op = ((word >> (2u * (c & 15u))) - (uint32_t)(pat >> (4 * (i & (P - 1))))) & 3u;
+        ++cnt;
+        run = op == 0u ? run + 1u : 0u;
+        i -= (int)(op != 0u);
+        j -= (int)(op != 1u);
+    }
+    if (i > top) {
+        if (j == 0) {  // the column-0 border: deletes up to the band above
+            cnt += (uint32_t)(i - top);
+        } else {  // unknown (see the stripe map kernel)
+            j = -1;
+            cnt = 0;
+        }
+    }
+    uint32_t *mp = map + (uint32_t)d.map_off + 2u * ((uint32_t)K * (uint32_t)nx + (uint32_t)(g - NB) * (uint32_t)nx + (uint32_t)(x0 + tid));
+    mp[0] = (uint32_t)j;
+    mp[1] = cnt;
+}
+
+// The stripe map from the band maps: one thread per (stripe k in 1 .. K-2, column x), chaining the stripe's NB
+// bands from its last row, and one for the sink's stripe, from the sink (stored at x = 0, as the stripe map kernel
+// does).  Unknown if any band on the chain is.
+template <int R>
+__global__ __launch_bounds__(256) void sed_tb_bandcompose_kernel(const sed_pair_desc *__restrict__ pd,
+                                                                 uint32_t *__restrict__ map) {
+    constexpr int ROWS = 64 * R, NB = R;
+    const int p = blockIdx.y;
+    const sed_pair_desc d = pd[p];
+    const int n = d.n, m = d.m;
+    if (d.lane || n == 0 || m == 0) return;
+    const int K = (n + ROWS - 1) / ROWS;
+    if (K < 3) return;
+    const int nx = m + 1, idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx > (K - 2) * nx) return;
+    int k, g, x;
+    uint32_t slot;
+    if (idx == (K - 2) * nx) {  // the sink: from (n, m) in the band holding row n
+        k = K - 1;
+        g = (n - 1) / 64;
+        x = m;
+        slot = (uint32_t)k * nx;
+    } else {
+        k = 1 + idx / nx;
+        x = idx % nx;
+        g = (k + 1) * NB - 1;
+        slot = (uint32_t)k * nx + x;
+    }
+    uint32_t *mp = map + (uint32_t)d.map_off;
+    const uint32_t *bm = mp + 2u * (uint32_t)K * nx;
+    uint32_t cnt = 0;
+    for (; g >= k * NB; --g) {
+        const uint32_t e = 2u * ((uint32_t)(g - NB) * nx + (uint32_t)x);
+        const uint32_t xn = bm[e];
+        if (xn == 0xFFFFFFFFu) {
+            x = -1;
+            cnt = 0;
+            break;
+        }
+        cnt += bm[e + 1u];
+        x = (int)xn;
+    }
+    mp[2u * slot] = (uint32_t)x;
+    mp[2u * slot + 1u] = cnt;
 }
 
 // The exit column and op count of stripe k's segment from cell (i, j), walked here (entries the map kernel left
@@ -3064,12 +3198,19 @@ hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops) {
 // of a pair ((K-2)(m+1)+1), kmax = the most stripes of a pair
 hipError_t sed_launch_traceback_stripes(const sed_launch &L, uint32_t *ops, uint32_t *map, int items, int kmax) {
     // items: map workgroups x 256 of the largest pair, and at least every pair's script words; >= one block
-    const dim3 gmap((max(items, 1) + 255) / 256, L.npairs), gemit(L.npairs, max(kmax, 1));
+    // (the compose grid: (K-2)(m+1)+1 threads per pair, at most items / 256 / R + 1 blocks, sed_runtime.cpp)
+    const dim3 gmap((max(items, 1) + 255) / 256, L.npairs), gemit(L.npairs, max(kmax, 1)),
+        gcomp((max(items, 1) + 255) / 256 / max(L.R, 1) + 1, L.npairs);
     switch (L.R) {
 #define CASE(RR)                                                                                                 \
     case RR: {                                                                                                   \
         const uint64_t pat = L.tb_ladder ? Ladder<RR>::pat : 0ull;                                               \
-        hipExtLaunchKernelGGL((sed_tb_stripemap_kernel<RR>), gmap, dim3(256), 0, L.stream, L.ev0, nullptr, 0, L.pd, L.tb, map, ops, pat); \
+        if (SED_TBMAP_BANDS) {                                                                                   \
+            hipExtLaunchKernelGGL((sed_tb_bandmap_kernel<RR>), gmap, dim3(256), 0, L.stream, L.ev0, nullptr, 0, L.pd, L.tb, map, ops, pat); \
+            hipLaunchKernelGGL((sed_tb_bandcompose_kernel<RR>), gcomp, dim3(256), 0, L.stream, L.pd, map);          \
+        } else {                                                                                                 \
+            hipExtLaunchKernelGGL((sed_tb_stripemap_kernel<RR>), gmap, dim3(256), 0, L.stream, L.ev0, nullptr, 0, L.pd, L.tb, map, ops, pat); \
+        }                                                                                                        \
         hipExtLaunchKernelGGL((sed_tb_stripeemit_kernel<RR>), gemit, dim3(64), 0, L.stream, nullptr, L.ev1, 0, L.pd, L.tb, L.res, ops, map, \
                            pat);                                                                                 \
         break;                                                                                                   \

@@ -808,10 +808,12 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
             // SPLIT: 64-bit {epoch tag, value} words per column and stripe (the tagged hand-off, sed_kernels.hip)
             // (fp64: D, L and T planes; SPLIT: three 64-bit {tag, D low | D high | L key and T} words)
             if (nstripes > 1) bndw += (nchunks + 2) * SW * (packed ? (split ? 2 : 1) : (split ? 6 : 4)) * (split ? nstripes : 1);
-            if (b->tbpar && nstripes >= 3) {  // {exit column, ops} per stripe and column
-                mapw += nstripes * (uint64_t)(mm + 1) * 2;
-                // workgroups of 256 columns per middle stripe, and one for the sink's stripe
-                b->tbpar_items = std::max<int>(b->tbpar_items, (int)(((nstripes - 2) * ((mm + 256) / 256) + 1) * 256));
+            if (b->tbpar && nstripes >= 3) {  // {exit column, ops} per stripe and column, then per 64-row band and column
+                const uint64_t nbands = ((uint64_t)nn + 63) / 64 - R;  // the bands of stripes 1 .. K-1
+                mapw += (nstripes + nbands) * (uint64_t)(mm + 1) * 2;
+                // band map: workgroups of 256 columns per band (a superset of the stripe map kernel's middle
+                // stripes + sink; the compose kernel's grid is derived from it, sed_launch_traceback_stripes)
+                b->tbpar_items = std::max<int>(b->tbpar_items, (int)(nbands * ((mm + 256) / 256) * 256));
             }
             b->tbpar_kmax = std::max<int>(b->tbpar_kmax, (int)(nstripes >= 3 ? nstripes : 1));
             if (split) {
