@@ -2113,8 +2113,10 @@ template <int R> struct CodeCursor {  // per-lane reader of one pair's per-cell 
 // its longest walks (lanes far from the path, running left through the staged columns): 1000^2 per call 400 -> 360 us,
 // 2000^2 629 -> 587 us at 192 (tools/script_calls.py, profiles/r05/s47); the 256-row stripes of config 2 keep 512
 // (at 192 its path needed columns past the staged ones, and the emit kernel's fallback walks took 187 against 53 us)
+// With the band maps (64-row walks) 128 staged columns serve R = 2 better still: 1000^2 343 -> 335 us, 2000^2 572 -> 563 us
+// per call (96: 335 / 562; profiles/r05/s57)
 #ifndef SED_TBMAP_LEFT_R2
-#define SED_TBMAP_LEFT_R2 192
+#define SED_TBMAP_LEFT_R2 128
 #endif
 #ifndef SED_TBMAP_BANDS  // 1: band maps + compose (sed_tb_bandmap_kernel), 0: one lane per stripe (A/B)
 #define SED_TBMAP_BANDS 1
