@@ -129,7 +129,9 @@ int sed_set_costs(sed_ctx *ctx, int K, const double *sub, const uint8_t *sub_int
  * Pair p: str1 = codes_a[off_a[p] .. +len_a[p]), str2 = codes_b[off_b[p] .. +len_b[p]).
  * out_dist[p]  = dp[n][m].value as fp64; out_is_int[p] = 1 when it is a Python int.
  * out_len[p]   = number of ops in the canonical script.
- * With SED_WANT_SCRIPT: out_ops + ops_off[p] receives ceil((n+m)/16) words for pair p.
+ * With SED_WANT_SCRIPT: out_ops + ops_off[p] receives ceil((n+m)/16) words for pair p: the out_len[p] ops, then
+ * zeros (the bits past the last op in its word and every spare word after it, on every route, so a pair's words
+ * are a function of its script alone; the device buffers of sed_batch_device_results / _export hold the same).
  * Script batches whose traceback workspace (~n*m/4 bytes per pair) exceeds SED_TB_BUDGET_GB
  * (environment, default 48) run as several consecutive launches. */
 int sed_run_batch(sed_ctx *ctx,

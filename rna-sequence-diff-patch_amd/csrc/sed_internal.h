@@ -34,6 +34,16 @@ struct sed_result {
 #define SED_ERR_TB_GUARD 4       // traceback: more tile visits than any path can need
 #define SED_ERR_TB_LENGTH 5      // traceback: the walk's op count differs from the sink's L
 
+// Script padding.  A pair's script region holds ceil((n+m)/16) words; its ops fill ceil(len/16) of them.  Every walk
+// starts its op accumulator at 0, so the bits past the last op inside the last op word are 0 already; this zeroes the
+// spare words after it (lanes lane, lane + stride, ...), so the packed buffer is a function of the scripts alone,
+// whatever the buffer held before (sed.h).  Every script-writing kernel calls it once per pair.
+__device__ __forceinline__ void zero_script_tail(uint32_t *__restrict__ out, int len, int n, int m, int lane,
+                                                 int stride) {
+    const int end = (n + m + 15) >> 4;
+    for (int w = ((len > 0 ? len : 0) + 15) / 16 + lane; w < end; w += stride) out[w] = 0u;
+}
+
 // Integer kernel constants (offset-key space, see sed_kernels.hip):
 //   costrow[a]   byte b = (cost(a -> b) - insert - delete - 1) & 0xFF  (32-bit keys)
 //   costrow16[a] byte b = (cost(a -> b) - insert - delete) & 0xFF      (16-bit packed distance keys)

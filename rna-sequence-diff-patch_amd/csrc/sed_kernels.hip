@@ -1941,6 +1941,7 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
     while (j > 0) { emit(0u); --j; }
     while (i > 0) { emit(1u); --i; }
     if (bad || q != 0) res[pair].err = SED_ERR_TB_LENGTH;
+    zero_script_tail(out, res[pair].len, n, m, 0, 1);
 }
 
 
@@ -2059,6 +2060,7 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
     uint32_t bad = 0;
     const uint32_t q = window_walk<R, false>(d, d.n, d.m, 0, q0, lane, tb, ops + d.ops_off, pat, bad);
     if ((bad | q) && lane == 0) res[pair].err = SED_ERR_TB_LENGTH;
+    zero_script_tail(ops + d.ops_off, (int)q0, d.n, d.m, lane, 64);
 }
 
 
@@ -2837,6 +2839,7 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
     if (lane == 0) out[((n + m + 15) >> 4) + 63] = err | ((uint32_t)visit << 8);  // (debug: no error, the dumps stay)
 #else
     if (err && lane == 0) res[pair].err = (uint8_t)err;
+    zero_script_tail(out, (int)q0, n, m, lane, 64);
 #endif
 }
 

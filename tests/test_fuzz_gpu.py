@@ -4,7 +4,8 @@ Every iteration draws a cost table (costs.json, user_costs.json or one of the G8
 the table's whole alphabet), a batch size around the routing thresholds (1, 16, 17, 64, 65, 256, 257 ... pairs),
 ragged lengths (empty sides included, now and then a pair past 1000 rows), a flag set (script, distance with length,
 distance only) and a routing override (SPLIT on / off, lane kernels off, rows per lane, fp64 forced, zero-copy off,
-16-lane segments on / off, per-cell codes or checkpoints, SPLIT's ladder-key forward), then compares every pair's distance, typing, length and script with the oracle
+16-lane segments on / off, per-cell codes or checkpoints, SPLIT's ladder-key forward), then compares every pair's distance, typing, length and script with the oracle, and checks that the script
+region's bits past the last op are zero (sed.h)
 (oracle/sed_oracle.c: StringEditDistance.py:92-334).  SED_FUZZ_SECONDS sets the budget (default 20 s) and
 SED_FUZZ_SEED the first seed (default 2026), so the default run is reproducible; a failure names its seed.
 """
@@ -14,7 +15,7 @@ import time
 import numpy as np
 import pytest
 
-from conftest import load_golden
+from conftest import load_golden, padding_errors
 import oracle
 import sedcost
 import sedgpu
@@ -91,6 +92,8 @@ def _check(gpu, table, pairs, script, no_len, opt, seed):
         if script:
             got = sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln[p]))
             assert np.array_equal(got, o["ops"]), where
+            assert not padding_errors(ops, packed.ops_off, packed.len_a, packed.len_b, ln, [p]), \
+                "nonzero script padding: " + where
 
 
 def test_route_fuzz_vs_oracle(gpu):

@@ -1,11 +1,13 @@
 """GPU parity of the production routes large batches take (config 3's dynamic CHAIN mode, the default
 checkpoint traceback with lane-kernel pairs in the same batch, pipelined batches) and the traceback's
-error path.  Every pair is checked against the C oracle (multithreaded), op by op."""
+error path.  Every pair is checked against the C oracle (multithreaded), op by op, and every script region's
+padding past the last op is zero (sed.h), so runs of one batch on two routes compare as whole buffers."""
 import os
 
 import numpy as np
 import pytest
 
+from conftest import padding_errors
 import oracle
 import sedcost
 import sedgpu
@@ -52,6 +54,8 @@ def _check_all(plan, packed, dist, is_int, ln, ops, script=True, no_len=False):
                if not np.array_equal(sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln[p])),
                                      oops[ooff[p]:ooff[p] + ol[p]])]
         assert not bad, bad[:10]
+        bad = padding_errors(ops, packed.ops_off, packed.len_a, packed.len_b, ln)
+        assert not bad, ("nonzero script padding", bad[:10])
 
 
 def _batch_run(ctx, packed, script, no_len=False, pipeline=False, runs=1):
@@ -116,6 +120,7 @@ def test_dynamic_chain_config3_route(gpu, tables, user):
     gpu.set_costs(plan)
     packed = sedgpu.PackedPairs(A, B)
     # scripts on the automatic route (per-cell codes at this size) and forced onto checkpoints (SED_OPT_TB = 2)
+    ref = None
     for script, no_len, tb in ((True, False, 0), (True, False, 2), (False, False, 0), (False, True, 0)):
         gpu.set_option(sedgpu.SED_OPT_TB, tb)
         try:
@@ -135,6 +140,10 @@ def test_dynamic_chain_config3_route(gpu, tables, user):
         finally:
             b.close()
         _check_all(plan, packed, d, ii, ln, ops, script=script, no_len=no_len)
+        if script and ref is None:
+            ref = (d, ii, ln, ops)
+        elif script:
+            _same((d, ii, ln, ops), ref, packed.ops_off)  # checkpoints against per-cell codes, whole buffers
     # the ladder dot keys against the perm ladder on the same batch (SED_OPT_DOT = 2)
     if not user:
         gpu.set_option(sedgpu.SED_OPT_DOT, 2)
@@ -146,7 +155,8 @@ def test_dynamic_chain_config3_route(gpu, tables, user):
                 b.close()
         finally:
             gpu.set_option(sedgpu.SED_OPT_DOT, 0)
-        _check_all(plan, packed, d2, ii2, ln2, ops2)  # (the packed buffers' bits past each script may differ)
+        _check_all(plan, packed, d2, ii2, ln2, ops2)
+        _same((d2, ii2, ln2, ops2), ref, packed.ops_off)
 
 
 def test_dynamic_chain_capped_waves(gpu, tables):
@@ -314,9 +324,7 @@ def test_checkpoint_parts_on_streams(gpu, tables):
         finally:
             gpu.set_option(sedgpu.SED_OPT_DEBUG_CORRUPT, 0)
         d2, ii2, ln2, ops2 = gpu.run(packed, True)
-        assert np.array_equal(d2, d) and np.array_equal(ln2, ln)
-        assert all(np.array_equal(sedgpu.unpack_ops(ops2, packed.ops_off, p, int(ln[p])),
-                                  sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln[p]))) for p in range(len(A)))
+        _same((d2, ii2, ln2, ops2), (d, ii, ln, ops), packed.ops_off)
     finally:
         gpu.set_option(sedgpu.SED_OPT_TB, 0)
         gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
@@ -371,9 +379,8 @@ def test_headline_config4_route(gpu, tables):
         b.close()
     P = len(A)
     assert np.array_equal(d6[:P], d) and np.array_equal(ii6[:P], ii) and np.array_equal(ln6[:P], ln)
-    bad = [p for p in range(P) if not np.array_equal(sedgpu.unpack_ops(ops6, packed6.ops_off, p, int(ln[p])),
-                                                     sedgpu.unpack_ops(ops, packed.ops_off, p, int(ln[p])))]
-    assert not bad, bad[:10]
+    W = int(packed.ops_off[P])  # the common pairs' script words sit at the same offsets in both buffers
+    assert np.array_equal(ops6[:W], ops[:W]), np.flatnonzero(ops6[:W] != ops[:W])[:8]
     tail = sedgpu.PackedPairs(a4 + a5, b4 + b5)
     o = tail.ops_off
     _check_all(plan, tail, d6[P:], ii6[P:], ln6[P:],
@@ -454,13 +461,9 @@ def test_stripe_walk_only_with_three_stripes(gpu, tables):
 
 
 def _same(out, ref, ops_off):
-    """Identical results; scripts compared op by op (words past a script's length are unused padding)."""
-    for name, x, y in zip(("dist", "is_int", "len"), out, ref):
+    """Identical results, the packed script buffers word for word (padding included: zero on every route)."""
+    for name, x, y in zip(("dist", "is_int", "len", "ops"), out, ref):
         assert np.array_equal(x, y), (name, np.flatnonzero(x != y)[:8])
-    bad = [p for p in range(len(ref[2]))
-           if not np.array_equal(sedgpu.unpack_ops(out[3], ops_off, p, int(ref[2][p])),
-                                 sedgpu.unpack_ops(ref[3], ops_off, p, int(ref[2][p])))]
-    assert not bad, bad
 
 
 @pytest.mark.parametrize("R,pipeline", [(4, False), (4, True), (16, False)])
