@@ -437,6 +437,14 @@ def shard_inputs(workload, P, n, m, world, r):
     return A, B, None, None
 
 
+def shard_bounds(workload, P, world, r):
+    """[first, stop) of rank r's shard as shard_inputs draws it: pair ids, or config 5's query rows."""
+    if workload in ("c5", "c5n"):
+        import sedshard
+        return sedshard.shard_range(P, world, r)
+    return r * P, (r + 1) * P
+
+
 def valid_scripts(plan, A, B, dist, ln, ops, ops_off, exact_int):
     """Pairs (of A, B) whose script passes script_costs and whose cost equals the reported distance."""
     good = 0
@@ -853,6 +861,8 @@ def main():
         "issue": issue, "issue_source": issue_src,
         "traceback_ms": float(np.mean(tb_ms)) if want_script else None,
         "gather_ms": gather_ms,
+        # each rank's [first, stop) pair ids (config 5: query rows), regenerated from the seeds on rank 0 to verify
+        "shards": [list(shard_bounds(args.workload, Pw, world, r)) for r in range(world)],
         "cpu_baseline": cpu_obj if cpu is not None else None,
     }
     if issue and line["valu"] is not None:

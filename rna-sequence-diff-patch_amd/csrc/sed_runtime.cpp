@@ -21,6 +21,7 @@ namespace {
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
+    uint64_t gen = 0;  // bumped by every (re)allocation: memory of a new generation may hold anything
     void release() {
         if (p) (void)hipFree(p);
         p = nullptr;
@@ -37,6 +38,7 @@ struct DevBuf {
             return false;
         }
         cap = want;
+        ++gen;
         return true;
     }
 };
@@ -135,6 +137,9 @@ struct sed_batch {
     void *h_out = nullptr;
     size_t h_out_cap = 0;
     bool zc = false;
+    // a zero-copy run was enqueued on the context's stream and not yet waited for (set before its first launch, so a
+    // run that failed halfway counts too): the kernels may still store into h_out
+    bool zc_busy = false;
     void *p_pd = nullptr, *p_seqa = nullptr, *p_seqb = nullptr, *p_tasks = nullptr, *p_lane = nullptr,
          *p_chain = nullptr, *p_x2 = nullptr, *p_ops = nullptr, *p_seg = nullptr, *p_res[3] = {nullptr, nullptr, nullptr};
     // timing events: 1 on every run (default), k > 1 on every k-th run, 0 never (sed_batch_set_timing; runs that
@@ -150,9 +155,10 @@ struct sed_batch {
     bool split = false;
     // SPLIT hand-off words' tag: the last run's epoch (1..32767), kept across fills, so that a refilled batch (the
     // per-call path fills the context's scratch batch every call) needs no memset; the buffer is zeroed when it is
-    // (re)allocated (d_bnd.cap differs from bnd_zero_cap) and when the epoch wraps
+    // (re)allocated (d_bnd.gen differs from bnd_zero_gen: a failed and a later successful reserve may return new
+    // memory of the old capacity, so the capacity does not tell) and when the epoch wraps
     uint32_t split_epoch = 0;
-    size_t bnd_zero_cap = 0;
+    uint64_t bnd_zero_gen = 0;
     bool ck = false;           // traceback from checkpoints + recompute (sed_kernels.hip: CK) instead of codes
     bool dot = false;          // CK forward kernel on dot keys (dot_keys below)
     bool lad = false;          // CHAIN kernel with the L field on ladder dot keys (dot_keys ladder mode)
@@ -205,6 +211,7 @@ struct sed_batch {
 
     int cur() const { return (int)((runs - 1) % nbuf); }
     ~sed_batch() {
+        if (zc_busy) (void)hipStreamSynchronize(ctx->stream);
         if (h_out) (void)hipHostFree(h_out);
         d_pd.release(); d_seqa.release(); d_seqb.release(); d_bnd.release(); d_ops.release(); d_tbmap.release();
         d_tasks.release(); d_lane.release(); d_chain.release(); d_x2.release(); d_small.release(); d_seg.release();
@@ -564,10 +571,10 @@ hipError_t next_split_epoch(sed_batch *b, hipStream_t s, uint32_t *epoch) {
     *epoch = b->split_epoch % 32767u + 1u;
     b->split_epoch = *epoch;
     if (!b->split || b->bnd_words == 0) return hipSuccess;
-    if (*epoch == 1 || b->d_bnd.cap != b->bnd_zero_cap) {
+    if (*epoch == 1 || b->d_bnd.gen != b->bnd_zero_gen) {
         hipError_t e = hipMemsetAsync(b->d_bnd.p, 0, b->d_bnd.cap, s);
         if (e != hipSuccess) return e;
-        b->bnd_zero_cap = b->d_bnd.cap;
+        b->bnd_zero_gen = b->d_bnd.gen;
     }
     return hipSuccess;
 }
@@ -606,7 +613,10 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
             if (e == hipSuccess && ps) e = hipStreamSynchronize(ps);
         if (e == hipSuccess && b->dp2_stream) e = hipStreamSynchronize(b->dp2_stream);
         if (e == hipSuccess && b->tb_stream) e = hipStreamSynchronize(b->tb_stream);
+        // zero-copy runs store into h_out from the context's stream, which a refill memsets below
+        if (e == hipSuccess && b->zc_busy) e = hipStreamSynchronize(c->stream);
         if (e != hipSuccess) return c->hipfail(e, "previous run");
+        b->zc_busy = false;
     }
     if (npairs < 0 || (npairs > 0 && (!codes_a || !off_a || !len_a || !codes_b || !off_b || !len_b)))
         return c->fail(SED_E_ARG, "bad batch arguments");
@@ -654,7 +664,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         else
             ++nwave_f64;
     }
-    const bool seg_ok = c->opt_seg != 2 && nwave_f64 > 256;
+    bool seg_ok = c->opt_seg != 2 && nwave_f64 > 256;
     int R = (mode == SED_MODE_I32 || c->opt_R) ? choose_R(mode, max_n, c->opt_R)
                                                 : choose_R_f64(len_a, len_b, npairs, f64_lane && mode == SED_MODE_F64, seg_ok);
     if (mode == SED_MODE_I32) {
@@ -685,7 +695,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         split = c->opt_split == 1 || (npairs <= 256 && max_n > 256 && c->opt_chain != 1 && c->opt_chain < 3);
         if (split && !c->opt_R) R = 4;
         if (split && R != 4 && R != 8 && R != 16 && R != 32) split = false;
-    } else if (mode != SED_MODE_I32 && c->opt_split != 2 && !seg_ok) {
+    } else if (mode != SED_MODE_I32 && c->opt_split != 2 && (!seg_ok || c->opt_split == 1)) {
         // fp64 SPLIT (sed_wf_f64_split_kernel, R = 4): batches of few pairs, whose lone fp64 waves are otherwise one
         // SIMD each.  It also runs the one-stripe pairs (tools/fp64_call_scaling.py, profiles/r05/s25: 30 nt 39.9
         // against 40.6 us per call, 200 nt 72 against 87, 500 nt 151 against 255, 2000 nt 544 against 3497), since
@@ -711,8 +721,9 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
             }
         }
     }
-    if (mode != SED_MODE_I32 && R == 2 && !split)
-        return c->fail(SED_E_ARG, "rows-per-lane 2 runs on the fp64 SPLIT route only");
+    if (split && mode != SED_MODE_I32) seg_ok = false;  // (SED_OPT_SPLIT = 1 over the segments of > 256 wave pairs)
+    // rows per lane 2 is the fp64 SPLIT route's; an fp64 batch that does not take it runs the automatic R
+    if (mode != SED_MODE_I32 && R == 2 && !split) R = choose_R_f64(len_a, len_b, npairs, f64_lane && mode == SED_MODE_F64, seg_ok);
     b->split = split;
     b->mode = mode;
     b->R = R;
@@ -1059,7 +1070,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
                 }
                 b->h_out_cap = std::max<size_t>(want, 1u << 16);
             }
-            memset(b->h_out, 0, want);  // (the previous run of this batch has completed: fetch_results waited)
+            memset(b->h_out, 0, want);  // (no run of this batch is in flight: zc_busy was waited for above)
         }
         if ((e = hipMemcpyAsync(d, h, up, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
             return c->hipfail(e, "upload");
@@ -1313,6 +1324,7 @@ int run_batch(sed_batch *b) {
     const int k = (int)(b->runs % b->nbuf);
     const bool want_tb = (b->flags & SED_WANT_SCRIPT) != 0;
     hipError_t e;
+    if (b->zc) b->zc_busy = true;
     // The run's events time it (sed_batch_times) and, when buffers rotate, order their reuse (evk below; two-slot lane
     // batches order by stream instead).  Untimed runs (sed_batch_set_timing) launch without them.
     const bool need_ev = b->nbuf > 1 && !(b->alt_dp && b->nbuf == 2 && !want_tb);
@@ -1497,6 +1509,7 @@ int sync_batch(sed_batch *b) {
     if (e == hipSuccess && b->dp2_stream) e = hipStreamSynchronize(b->dp2_stream);
     for (hipStream_t ps : b->part_stream)
         if (e == hipSuccess && ps) e = hipStreamSynchronize(ps);
+    if (e == hipSuccess) b->zc_busy = false;
     return e == hipSuccess ? SED_OK : c->hipfail(e, "kernel execution");
 }
 

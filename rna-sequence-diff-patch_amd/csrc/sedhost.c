@@ -26,11 +26,52 @@ static PyObject *K_OPERATION, *K_SOURCE, *K_DESTINATION, *K_CHARACTER, *K_INDEX;
 static PyObject *S_INSERT, *S_DELETE, *S_UPDATE;
 
 /* ------------------------------------------------------------------ es_from_ops */
+/* Leaves shared by every record (immutable objects, so sharing is invisible to callers): the one-character strings
+ * of code points < 256 (CPython's own singletons, looked up without a call) and the index ints 0 .. G_INTS_MAX - 1,
+ * created once and kept, so a 4096^2 script's ~8500 index ints are neither allocated nor freed per call. */
+#define G_INTS_MAX (1 << 20)
+static PyObject *g_chars[256];
+static PyObject **g_ints;
+static Py_ssize_t g_nints;
+
+static int ints_reserve(Py_ssize_t want) {
+    if (want <= g_nints) return 0;
+    if (want > G_INTS_MAX) want = G_INTS_MAX;
+    if (want <= g_nints) return 0;
+    PyObject **p = (PyObject **)PyMem_Realloc(g_ints, sizeof(PyObject *) * (size_t)want);
+    if (!p) {
+        PyErr_NoMemory();
+        return -1;
+    }
+    g_ints = p;
+    for (Py_ssize_t k = g_nints; k < want; ++k) {
+        if (!(g_ints[k] = PyLong_FromSsize_t(k))) {
+            g_nints = k;
+            return -1;
+        }
+    }
+    g_nints = want;
+    return 0;
+}
+
+static PyObject *int_of(Py_ssize_t i) {
+    if (i >= 0 && i < g_nints) {
+        Py_INCREF(g_ints[i]);
+        return g_ints[i];
+    }
+    return PyLong_FromSsize_t(i);
+}
+
 static PyObject *char_at(PyObject *s, Py_ssize_t len, Py_ssize_t i) {
     if (i < 0) i += len;
     if (i < 0 || i >= len) {
         PyErr_SetString(PyExc_IndexError, "string index out of range");
         return NULL;
+    }
+    if (PyUnicode_KIND(s) == PyUnicode_1BYTE_KIND) {
+        PyObject *ch = g_chars[((const unsigned char *)PyUnicode_DATA(s))[i]];
+        Py_INCREF(ch);
+        return ch;
     }
     return PyUnicode_Substring(s, i, i + 1);
 }
@@ -38,7 +79,7 @@ static PyObject *char_at(PyObject *s, Py_ssize_t len, Py_ssize_t i) {
 static PyObject *side(PyObject *s, Py_ssize_t len, Py_ssize_t i) {
     PyObject *ch = char_at(s, len, i);
     if (!ch) return NULL;
-    PyObject *idx = PyLong_FromSsize_t(i);
+    PyObject *idx = int_of(i);
     PyObject *d = PyDict_New();
     if (!idx || !d || PyDict_SetItem(d, K_CHARACTER, ch) || PyDict_SetItem(d, K_INDEX, idx)) {
         Py_XDECREF(d);
@@ -55,7 +96,9 @@ static PyObject *es_from_ops_impl(PyObject *self, PyObject *args) {
     if (!PyArg_ParseTuple(args, "y*UU", &ops, &s1, &s2)) return NULL;
     const unsigned char *op = (const unsigned char *)ops.buf;
     const Py_ssize_t n = ops.len, l1 = PyUnicode_GET_LENGTH(s1), l2 = PyUnicode_GET_LENGTH(s2);
-    PyObject *out = PyList_New(n);
+    PyObject *out = NULL;
+    if (PyUnicode_READY(s1) < 0 || PyUnicode_READY(s2) < 0 || ints_reserve((l1 > l2 ? l1 : l2) + 1) < 0) goto fail;
+    out = PyList_New(n);
     if (!out) goto fail;
     Py_ssize_t r = 0, c = 0;
     for (Py_ssize_t k = 0; k < n; ++k) {
@@ -720,5 +763,7 @@ PyMODINIT_FUNC PyInit__sedhost(void) {
     if (!K_OPERATION || !K_SOURCE || !K_DESTINATION || !K_CHARACTER || !K_INDEX || !S_INSERT || !S_DELETE ||
         !S_UPDATE)
         return NULL;
+    for (int k = 0; k < 256; ++k)
+        if (!(g_chars[k] = PyUnicode_FromOrdinal(k))) return NULL;
     return PyModule_Create(&moddef);
 }

@@ -9,10 +9,12 @@ forks a multiprocessing.Process per similarity method and again for wf_score
 parent initialised it.  context() therefore returns, in such a child, an
 EngineClient that sends every call to an engine that owns a HIP context:
   - by default the parent itself: every fork of a process that holds a Context
-    gets a socket pair, and a thread of the parent serves that child's requests
-    on a Context of its own (created on the child's first call, closed when the
-    child goes away).  A child pays no start-up beyond that sed_create, which is
-    what create_search_threads' two Process rounds need;
+    gets a socket pair.  One selector thread of the parent watches the pairs;
+    a child's first request starts a thread that serves it on a Context of its
+    own (from a pool of two, else a new one), and children that never call the
+    engine cost only their socket.  A child pays no start-up beyond that
+    sed_create, which is what create_search_threads' two Process rounds need.
+    Served children need the parent alive: when it exits, their calls raise;
   - otherwise (SED_FORK_ENGINE=worker, a grandchild, or a fork taken while no
     Context existed) the child starts one engine worker, a fresh interpreter
     running this file, and talks to it over a pipe pair.
@@ -685,9 +687,60 @@ def _serve_child(sock):
         conn.close()
 
 
-# fork hooks: a process holding a HIP Context gives each fork a socket pair to a serving thread of its own
+# fork hooks: a process holding a HIP Context gives each fork a socket pair.  The parent's ends are watched by one
+# selector thread (started at the first fork); a child's first request starts a thread serving that child, and a child
+# that exits without using the engine (a Manager server, a helper) only has its socket closed.  Served children depend
+# on this process: when it exits, their channels close and their next engine call raises SedError.
 _fork_pair = None
 _child_channel = None  # (socket, pid) in a child forked from a HIP process
+_sel_state = None  # parent: (selector, wake read end, wake write end, channels to register)
+_sel_lock = threading.Lock()
+
+
+def _watch_channel(sock):
+    """Hand the parent's end of a new child's socket pair to the selector thread."""
+    global _sel_state
+    with _sel_lock:
+        if _sel_state is None:
+            import selectors
+            sel = selectors.DefaultSelector()
+            wr, ww = socket.socketpair(socket.AF_UNIX, socket.SOCK_STREAM)
+            wr.setblocking(False)
+            sel.register(wr, selectors.EVENT_READ)
+            _sel_state = (sel, wr, ww, [])
+            threading.Thread(target=_channel_selector, args=(_sel_state,), daemon=True,
+                             name="sed-engine-channels").start()
+        _sel_state[3].append(sock)
+        ww = _sel_state[2]
+    ww.send(b"\0")
+
+
+def _channel_selector(state):
+    """The selector thread: waits on every child's channel until its first request (or its end)."""
+    import selectors
+    sel, wake, _, pending = state
+    while True:
+        for key, _ in sel.select():
+            s = key.fileobj
+            if s is wake:
+                try:
+                    wake.recv(4096)
+                except BlockingIOError:
+                    pass
+                with _sel_lock:
+                    new, pending[:] = list(pending), []
+                for x in new:
+                    sel.register(x, selectors.EVENT_READ)
+                continue
+            sel.unregister(s)
+            try:
+                first = s.recv(1, socket.MSG_PEEK)
+            except OSError:
+                first = b""
+            if first:
+                threading.Thread(target=_serve_child, args=(s,), daemon=True, name="sed-engine-fork").start()
+            else:
+                s.close()  # the child closed its end without a request
 
 
 def _before_fork():
@@ -705,7 +758,7 @@ def _after_fork_in_parent():
     pair, _fork_pair = _fork_pair, None
     if pair is not None:
         pair[1].close()
-        threading.Thread(target=_serve_child, args=(pair[0],), daemon=True, name="sed-engine-fork").start()
+        _watch_channel(pair[0])
 
 
 _ctx = None
@@ -713,8 +766,22 @@ _ctx_pid = None
 
 
 def _reset_lock_in_child():
-    global _lock, _fork_pair, _child_channel
+    global _lock, _fork_pair, _child_channel, _sel_state, _sel_lock
     _lock = threading.Lock()  # a fork taken while another thread held it must not deadlock the child
+    _sel_lock = threading.Lock()
+    st, _sel_state = _sel_state, None  # (the parent's selector thread does not exist here: drop its copies)
+    if st is not None:
+        for x in (st[0], st[1], st[2]):
+            try:
+                x.close()
+            except OSError:
+                pass
+    if _child_channel is not None and _child_channel[1] != os.getpid():
+        # a channel this process's parent got but never used: a grandchild must not hold it open
+        try:
+            _child_channel[0].close()
+        except OSError:
+            pass
     pair, _fork_pair = _fork_pair, None
     if pair is not None:
         pair[0].close()

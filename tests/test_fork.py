@@ -89,3 +89,58 @@ def test_worker_engine_reports_errors_without_a_device(monkeypatch):
         ctx.selftest()
     ctx.close()
     monkeypatch.setattr(sedgpu, "_ctx", None)
+
+
+def _idle_child():
+    pass  # forked, never touches the engine
+
+
+def _grandchild_probe(q):
+    """In a forked child that holds an unused channel: fork a grandchild, which must hold neither the channel object
+    nor its descriptor."""
+    fd = sedgpu._child_channel[0].fileno() if sedgpu._child_channel else -1
+    r, w = os.pipe()
+    pid = os.fork()
+    if pid == 0:
+        ok = sedgpu._child_channel is None
+        try:
+            os.fstat(fd)
+            ok = False  # still open in the grandchild
+        except OSError:
+            pass
+        os.write(w, b"1" if ok else b"0")
+        os._exit(0)
+    os.waitpid(pid, 0)
+    q.put((fd, os.read(r, 1)))
+
+
+def test_fork_channels_share_one_selector_thread(monkeypatch):
+    """Forks of a HIP process get channels watched by one selector thread: children that never use the engine get
+    no serving thread (their channels are closed when they exit), and a child's unused channel is closed in its own
+    forks."""
+    import threading
+    import time
+    monkeypatch.setattr(sedgpu, "_hip_pid", os.getpid())
+    monkeypatch.setattr(sedgpu, "_ctx", _fake_parent_context())
+    monkeypatch.setattr(sedgpu, "_ctx_pid", os.getpid())
+    monkeypatch.delenv("SED_FORK_ENGINE", raising=False)
+    serving = lambda: sum(t.name == "sed-engine-fork" for t in threading.enumerate())
+    before = serving()
+    fork = mp.get_context("fork")
+    procs = [fork.Process(target=_idle_child) for _ in range(4)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    q = fork.Queue()
+    p = fork.Process(target=_grandchild_probe, args=(q,))
+    p.start()
+    fd, ok = q.get(timeout=60)
+    p.join(timeout=60)
+    assert fd >= 0 and ok == b"1"
+    time.sleep(0.3)
+    names = [t.name for t in threading.enumerate()]
+    assert names.count("sed-engine-channels") == 1
+    assert serving() <= before  # no child made a request
+    sedgpu._ctx.ptr = None

@@ -790,6 +790,38 @@ def test_fp64_split_full_matrix(gpu, tables):
             assert (float(D[n, m]), bool(M[n, m] >> 3)) == (o["dist"], bool(o["is_int"])), (user, n, m)
 
 
+def test_fp64_split_forced_over_segments_and_r2_fallback(gpu, tables):
+    """An fp64 batch of > 256 wave pairs takes the 16-lane segments on the automatic route; SED_OPT_SPLIT = 1 forces
+    the fp64 SPLIT route over them (no segment pairs), and rows per lane 2 outside SPLIT (SED_OPT_SPLIT = 2) falls back
+    to the automatic R instead of failing.  Results identical on every route, the oracle's on a sample."""
+    pairs = _random_pairs(9500, 290, IUPAC, 1, 300)
+    pairs += _random_pairs(9501, 6, IUPAC, 257, 600, related=True)
+    table = tables[False]
+    plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs], [plan.encode(y) for _, y in pairs])
+    try:
+        b = sedgpu.Batch(gpu, packed, True)
+        assert b.segment_pairs > 0 and b.split_tasks == 0
+        b.close()
+        gpu.set_option(sedgpu.SED_OPT_SPLIT, 1)
+        b = sedgpu.Batch(gpu, packed, True)
+        assert b.segment_pairs == 0 and b.split_tasks > 0 and b.rows_per_lane == 2
+        b.close()
+        gpu.set_option(sedgpu.SED_OPT_SPLIT, 2)
+        gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 2)
+        b = sedgpu.Batch(gpu, packed, True)
+        assert b.split_tasks == 0 and b.rows_per_lane in (4, 8)
+        b.close()
+    finally:
+        gpu.set_option(sedgpu.SED_OPT_SPLIT, 0)
+        gpu.set_option(sedgpu.SED_OPT_ROWS_PER_LANE, 0)
+    got = gpu_run(gpu, table, pairs)
+    assert gpu_run(gpu, table, pairs, split=1) == got
+    assert gpu_run(gpu, table, pairs, split=2, R=2) == got
+    _oracle_check(table, pairs[::7] + pairs[-6:], got[::7] + got[-6:])
+
+
 
 @pytest.mark.parametrize("table_name", ["costs.json", "int_literals", "frac_indel"])
 def test_fp64_segments_vs_oracle(gpu, tables, table_name):

@@ -28,10 +28,12 @@ def main():
     ctx = sedgpu.Context(0)
     rng = np.random.default_rng(5)
     lines = []
-    sizes = [(int(x.split("x")[0]), int(x.split("x")[1])) for x in os.environ.get(
+    # P x n [x m] (m = n when omitted)
+    sizes = [tuple(int(v) for v in x.split("x")) for x in os.environ.get(
         "SED_SPLIT_SIZES", "16x1000,64x500,64x1000,64x2000,128x1000,128x2000,256x500,256x1000,256x2000").split(",")]
-    for P, L in sizes:
-        pairs = [("".join(rng.choice(NUC, size=L)), "".join(rng.choice(NUC, size=L))) for _ in range(P)]
+    for size in sizes:
+        P, L, M = size[0], size[1], size[2] if len(size) > 2 else size[1]
+        pairs = [("".join(rng.choice(NUC, size=L)), "".join(rng.choice(NUC, size=M))) for _ in range(P)]
         plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
         ctx.set_costs(plan)
         packed = sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs], [plan.encode(b) for _, b in pairs])
@@ -54,7 +56,7 @@ def main():
                 ts = sorted(ts[1:])
                 row.append("split %d %7.2f ms (tasks %d)" % (split, ts[len(ts) // 2] * 1e3, tasks))
             ctx.set_option(sedgpu.SED_OPT_SPLIT, 0)
-            lines.append("P %3d  %4d^2  %-8s " % (P, L, "script" if script else "distance") + "  ".join(row))
+            lines.append("P %3d  %4d x %4d  %-8s " % (P, L, M, "script" if script else "distance") + "  ".join(row))
             print(lines[-1], flush=True)
     ctx.close()
     if OUT:
