@@ -417,17 +417,28 @@ template <bool B> struct BoolTag { static constexpr bool value = B; };
 // The stripe kernel's group: lane 0's top values from the chunk's LDS slots (ltop, broadcast reads),
 // each lane's str2 selectors from the wave's LDS selector ring at its own column (lsel: this group's
 // first step for this lane, doubled ring so the G reads never wrap).
-template <int R, bool TB, bool LEN, bool CAP, bool CK = false, bool DOT = false, bool COLLECT = !CK>
+// PF (SED_CK_TVPF, the CK forward's unrolled chunk loop): the group's first {top, selector} pair arrives in tvpf, read
+// at the previous group's start, and this group reads the next group's first pair with its own, so its first step's
+// dots start without waiting on an LDS round trip (the last group of a chunk reads one entry past it, unused).
+template <int R, bool TB, bool LEN, bool CAP, bool CK = false, bool DOT = false, bool COLLECT = !CK, bool PF = false>
 __device__ __forceinline__ void i32_group(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                           uint32_t &bottom, uint32_t &selv, const uint32_t *__restrict__ ltop,
                                           const uint32_t *__restrict__ lsel, uint32_t &outc, uint32_t (&W)[4],
                                           const int s0, const int lane, const int cap_step, const int cap_lane,
-                                          const int cap_row, uint32_t &cap, uint32_t (&rcv)[Grp<R>::G]) {
+                                          const int cap_row, uint32_t &cap, uint32_t (&rcv)[Grp<R>::G],
+                                          uint2 *tvpf = nullptr) {
     constexpr int G = Grp<R>::G;
     uint2 tv[G];
     const uint32_t *lp = ltop + (s0 & 63);  // G divides 64: a group never wraps the chunk
+    if constexpr (PF) {
+        tv[0] = *tvpf;
 #pragma unroll
-    for (int u = 0; u < G; ++u) tv[u] = make_uint2(lp[u], lsel[u]);
+        for (int u = 1; u < G; ++u) tv[u] = make_uint2(lp[u], lsel[u]);
+        *tvpf = make_uint2(lp[G], lsel[G]);
+    } else {
+#pragma unroll
+        for (int u = 0; u < G; ++u) tv[u] = make_uint2(lp[u], lsel[u]);
+    }
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         const int s = s0 + u;
@@ -453,6 +464,9 @@ template <int R> struct I32Waves { static constexpr int value = R >= 32 ? 4 : (R
 #endif
 #ifndef SED_CK_GUNROLL
 #define SED_CK_GUNROLL 2  // groups per iteration of the CK chunk loop
+#endif
+#ifndef SED_CK_TVPF
+#define SED_CK_TVPF 0  // CK forward: each group's first LDS pair read a group ahead (i32_group PF; A/B)
 #endif
 #ifdef SED_I32_WAVES_PER_EU
 #define SED_I32_WAVES(R) SED_I32_WAVES_PER_EU
@@ -709,11 +723,13 @@ void sed_wf_i32_kernel(const sed_pair_desc *__restrict__ pd, int npairs, const i
                 }
             };
             if constexpr (FASTC) {
+                uint2 tvpf = make_uint2(lch[0], lsel[0]);  // (SED_CK_TVPF: the first group's first pair)
 #pragma unroll SED_CK_GUNROLL
                 for (int g = 0; g < 64 / G; ++g) {
                     const int s0 = 64 * c + g * G;  // (s0 & 63 folds to g * G)
-                    i32_group<R, TB, LEN, false, CK, DOT>(V, cv, top_prev, bottom, selv, lch, lsel + g * G, outc, W, s0, lane,
-                                                     cap_step, cap_lane, cap_row, cap, rcv);
+                    i32_group<R, TB, LEN, false, CK, DOT, !CK, (bool)SED_CK_TVPF>(V, cv, top_prev, bottom, selv, lch,
+                                                     lsel + g * G, outc, W, s0, lane, cap_step, cap_lane, cap_row, cap,
+                                                     rcv, &tvpf);
                     if (s0 < SG) stores(s0);
                 }
                 s = 64 * (c + 1);  // lane 63's bottom cells of the whole chunk are in outc (!CK)
@@ -2222,10 +2238,11 @@ __global__ __launch_bounds__(256) void sed_tb_stripemap_kernel(const sed_pair_de
 // Band maps (round 5, SED_TBMAP_BANDS = 1, the default): the map kernel above gives one lane a whole stripe, a
 // chain of up to ~700 dependent LDS steps at about one wave per SIMD (config 2: 104 us).  Here a lane walks one
 // 64-row band (band g: rows 64g + 1 .. 64g + 64, from its last row, or from the sink in the sink's band) for every
-// band of stripes 1 .. K-1 and every column: 4x (R = 4) the lanes at 1/4 the chain, each workgroup staging only its
-// band's 64/R forward lanes of the code groups (1/4 the LDS, so many workgroups per CU).  band map entry
-// bm[(g - NB) * (m + 1) + x] = {exit column at row 64g, ops}, or unknown; it follows the stripe map's K (m + 1)
-// entries.  sed_tb_bandcompose_kernel then chains a stripe's NB bands into the stripe map the emit kernel reads.
+// band 1 .. nbt-1 (stripe 0's upper bands too, for the banded emit) and every column: 4x (R = 4) the lanes at 1/4 the
+// chain, each workgroup staging only its band's 64/R forward lanes of the code groups (1/4 the LDS, so many
+// workgroups per CU).  band map entry bm[(g - 1) * (m + 1) + x] = {exit column at row 64g, ops}, or unknown; it
+// follows the stripe map's K (m + 1) entries.  sed_tb_bandcompose_kernel then chains a stripe's NB bands into the
+// stripe map, and the emit kernel composes both.
 template <int R>
 __global__ __launch_bounds__(256) void sed_tb_bandmap_kernel(const sed_pair_desc *__restrict__ pd,
                                                              const uint32_t *__restrict__ tb,
@@ -2248,10 +2265,10 @@ __global__ __launch_bounds__(256) void sed_tb_bandmap_kernel(const sed_pair_desc
     if (n == 0 || m == 0) return;
     const int K = (n + ROWS - 1) / ROWS;
     if (K < 3) return;  // walked whole by the emit kernel
-    const int nx = m + 1, nxc = (nx + 255) / 256, nbt = (n + 63) / 64;  // bands NB .. nbt-1 are mapped
+    const int nx = m + 1, nxc = (nx + 255) / 256, nbt = (n + 63) / 64;  // bands 1 .. nbt-1 are mapped
     const int blk = blockIdx.x;
-    if (blk >= (nbt - NB) * nxc) return;
-    const int g = NB + blk / nxc, x0 = (blk % nxc) * 256;
+    if (blk >= (nbt - 1) * nxc) return;
+    const int g = 1 + blk / nxc, x0 = (blk % nxc) * 256;
     const int k = g / NB, t0 = (g % NB) * NL;  // the band's stripe and first forward lane
     const int SG = (m + 63 + G - 1) / G * G;
     const uint64_t stripe_words = (uint64_t)(SG / G) * 256u;
@@ -2299,7 +2316,7 @@ __global__ __launch_bounds__(256) void sed_tb_bandmap_kernel(const sed_pair_desc
             cnt = 0;
         }
     }
-    uint32_t *mp = map + (uint32_t)d.map_off + 2u * ((uint32_t)K * (uint32_t)nx + (uint32_t)(g - NB) * (uint32_t)nx + (uint32_t)(x0 + tid));
+    uint32_t *mp = map + (uint32_t)d.map_off + 2u * ((uint32_t)K * (uint32_t)nx + (uint32_t)(g - 1) * (uint32_t)nx + (uint32_t)(x0 + tid));
     mp[0] = (uint32_t)j;
     mp[1] = cnt;
 }
@@ -2336,7 +2353,7 @@ __global__ __launch_bounds__(256) void sed_tb_bandcompose_kernel(const sed_pair_
     const uint32_t *bm = mp + 2u * (uint32_t)K * nx;
     uint32_t cnt = 0;
     for (; g >= k * NB; --g) {
-        const uint32_t e = 2u * ((uint32_t)(g - NB) * nx + (uint32_t)x);
+        const uint32_t e = 2u * ((uint32_t)(g - 1) * nx + (uint32_t)x);
         const uint32_t xn = bm[e];
         if (xn == 0xFFFFFFFFu) {
             x = -1;
@@ -2354,11 +2371,11 @@ __global__ __launch_bounds__(256) void sed_tb_bandcompose_kernel(const sed_pair_
 // unknown); wave-uniform, codes read one word per step
 template <int R>
 __device__ __forceinline__ uint2 ck_count_walk(const sed_pair_desc &d, const uint32_t *__restrict__ tb, const uint64_t pat,
-                                               const int k, int i, int j) {
+                                               const int k, int i, int j, int top = -1) {
     constexpr int ROWS = 64 * R, G = Grp<R>::G, LG = CodeCursor<R>::LG, LR = CodeCursor<R>::LR, P = Ladder<R>::P;
     const int SG = (d.m + 63 + G - 1) / G * G;
     const uint32_t *tbk = tb + d.tb_off + (uint64_t)k * (uint64_t)(SG / G) * 256u;
-    const int top = k * ROWS;
+    if (top < 0) top = k * ROWS;  // (else a band's top row inside stripe k)
     uint32_t cnt = 0;
     while (i > top) {
         if (j == 0) {
@@ -2428,6 +2445,82 @@ __global__ __launch_bounds__(64) void sed_tb_stripeemit_kernel(const sed_pair_de
         }
     }
     const int istop = (Keff == 1 || kme == 0) ? 0 : kme * ROWS;
+    uint32_t bad = 0;
+    const uint32_t q = window_walk<R, true>(d, i0, j0, istop, qhi, lane, tb, ops + d.ops_off, pat, bad);
+    if ((bad || q != qhi - cnt) && lane == 0) res[pair].err = SED_ERR_TB_LENGTH;
+}
+
+// Banded emit (round 6, SED_TB_BANDEMIT = 1, the default): one wave per (pair, 64-row band) instead of per stripe, so
+// a wave walks one band's segment of the path (~1/R of a stripe's).  The wave composes the stripe maps from the sink
+// down to its band's stripe, then that stripe's band maps down to its band (entries the maps left unknown are walked
+// here, ck_count_walk), and walks its segment to the band's top row (band 0: to the origin) with the window walk,
+// ORing its script words into the zeroed buffer as the stripe emit does.
+#ifndef SED_TB_BANDEMIT
+#define SED_TB_BANDEMIT 1
+#endif
+template <int R>
+__global__ __launch_bounds__(64) void sed_tb_bandemit_kernel(const sed_pair_desc *__restrict__ pd,
+                                                             const uint32_t *__restrict__ tb,
+                                                             sed_result *__restrict__ res,
+                                                             uint32_t *__restrict__ ops,
+                                                             const uint32_t *__restrict__ map, const uint64_t pat) {
+    constexpr int ROWS = 64 * R, NB = R;
+    const int lane = threadIdx.x;
+    const int pair = __builtin_amdgcn_readfirstlane(blockIdx.x), gme = __builtin_amdgcn_readfirstlane(blockIdx.y);
+    const sed_pair_desc d = pd[pair];
+    if (d.lane) return;
+    const int n = d.n, m = d.m;
+    const int K = n > 0 ? (n + ROWS - 1) / ROWS : 1;
+    const bool multi = K >= 3 && m > 0;  // pairs of one or two stripes: one segment, the whole walk (band 0's wave)
+    const int nbt = multi ? (n + 63) / 64 : 1;
+    if (gme >= nbt) return;
+    const uint32_t L = (uint32_t)__builtin_amdgcn_readfirstlane(res[pair].len);
+    int i0 = n, j0 = m;
+    uint32_t qhi = L, cnt = L;  // cnt: the ops of this segment
+    if (multi) {
+        const uint32_t nx = (uint32_t)m + 1u;
+        const uint32_t *mp = map + (uint32_t)d.map_off;
+        const uint32_t *bm = mp + 2u * (uint32_t)K * nx;
+        const int kme = gme / NB;
+        uint32_t x = (uint32_t)m;
+        for (int kk = K - 1; kk > kme; --kk) {  // whole stripes above this band's: from the sink's
+            const uint32_t e = kk == K - 1 ? 2u * ((uint32_t)(K - 1) * nx) : 2u * ((uint32_t)kk * nx + x);
+            uint32_t xn = mp[e], c = mp[e + 1u];
+            if (xn == 0xFFFFFFFFu) {
+                const uint2 w = ck_count_walk<R>(d, tb, pat, kk, i0, (int)x);
+                xn = w.x;
+                c = w.y;
+            }
+            qhi -= c;
+            x = xn;
+            i0 = kk * ROWS;
+        }
+        for (int g = (i0 - 1) / 64; g >= gme; --g) {  // bands of this stripe from its entry: the last one is this band's
+            uint32_t xn, c;
+            if (g == 0) {  // band 0: to the origin, whatever is left
+                xn = 0u;
+                c = qhi;
+            } else {
+                const uint32_t e = 2u * ((uint32_t)(g - 1) * nx + x);
+                xn = bm[e];
+                c = bm[e + 1u];
+                if (xn == 0xFFFFFFFFu) {
+                    const uint2 w = ck_count_walk<R>(d, tb, pat, kme, i0, (int)x, 64 * g);
+                    xn = w.x;
+                    c = w.y;
+                }
+            }
+            if (g == gme) {
+                cnt = c;
+                break;
+            }
+            qhi -= c;
+            x = xn;
+            i0 = 64 * g;
+        }
+        j0 = (int)x;
+    }
+    const int istop = multi ? 64 * gme : 0;
     uint32_t bad = 0;
     const uint32_t q = window_walk<R, true>(d, i0, j0, istop, qhi, lane, tb, ops + d.ops_off, pat, bad);
     if ((bad || q != qhi - cnt) && lane == 0) res[pair].err = SED_ERR_TB_LENGTH;
@@ -3204,7 +3297,8 @@ hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops) {
 hipError_t sed_launch_traceback_stripes(const sed_launch &L, uint32_t *ops, uint32_t *map, int items, int kmax) {
     // items: map workgroups x 256 of the largest pair, and at least every pair's script words; >= one block
     // (the compose grid: (K-2)(m+1)+1 threads per pair, at most items / 256 / R + 1 blocks, sed_runtime.cpp)
-    const dim3 gmap((max(items, 1) + 255) / 256, L.npairs), gemit(L.npairs, max(kmax, 1)),
+    const bool bandemit = SED_TBMAP_BANDS && SED_TB_BANDEMIT;
+    const dim3 gmap((max(items, 1) + 255) / 256, L.npairs), gemit(L.npairs, max(kmax, 1) * (bandemit ? L.R : 1)),
         gcomp((max(items, 1) + 255) / 256 / max(L.R, 1) + 1, L.npairs);
     switch (L.R) {
 #define CASE(RR)                                                                                                 \
@@ -3216,8 +3310,12 @@ hipError_t sed_launch_traceback_stripes(const sed_launch &L, uint32_t *ops, uint
         } else {                                                                                                 \
             hipExtLaunchKernelGGL((sed_tb_stripemap_kernel<RR>), gmap, dim3(256), 0, L.stream, L.ev0, nullptr, 0, L.pd, L.tb, map, ops, pat); \
         }                                                                                                        \
-        hipExtLaunchKernelGGL((sed_tb_stripeemit_kernel<RR>), gemit, dim3(64), 0, L.stream, nullptr, L.ev1, 0, L.pd, L.tb, L.res, ops, map, \
-                           pat);                                                                                 \
+        if (bandemit)                                                                                            \
+            hipExtLaunchKernelGGL((sed_tb_bandemit_kernel<RR>), gemit, dim3(64), 0, L.stream, nullptr, L.ev1, 0, L.pd, L.tb, L.res, ops, \
+                                  map, pat);                                                                     \
+        else                                                                                                     \
+            hipExtLaunchKernelGGL((sed_tb_stripeemit_kernel<RR>), gemit, dim3(64), 0, L.stream, nullptr, L.ev1, 0, L.pd, L.tb, L.res, ops, \
+                                  map, pat);                                                                     \
         break;                                                                                                   \
     }
         CASE(2) CASE(4)

@@ -566,6 +566,28 @@ int choose_R_f64(const int32_t *len_a, const int32_t *len_b, int npairs, bool la
     return cost[1] < cost[0] ? 8 : 4;
 }
 
+// fp64 batches of several pairs: does the SPLIT route (R = 2) beat one wave per pair?  A SPLIT workgroup holds its slot
+// for its pair's whole stripe chain, m + 63 steps plus ~64 steps of lag per stripe above it, so a batch whose stripes
+// outnumber the resident workgroups (~256) runs in rounds, and long narrow pairs (n >> m) spend most of each round
+// waiting on the lag.  The lone waves (one per pair, all resident) take the f64_cost units of their stripes.  Fitted to
+// 32 batches of 16..256 pairs, 300..4000 rows, 100..2000 columns, scripts and distances (tools/fp64_split_batch.py,
+// profiles/r06/fp64_split): the model picks the faster route in all 32; SPLIT lost up to 2.7x on 256 pairs of
+// 2000 x 100 (1.34 against 0.49 ms) and won up to 3.8x on 64 pairs of 2000^2 (0.95 against 3.65 ms).
+bool f64_split_pays(const int32_t *len_a, const int32_t *len_b, int npairs, bool script) {
+    double lone = 0, lat_max = 0, slots = 0;
+    for (int p = 0; p < npairs; ++p) {
+        const int n = len_a[p], m = len_b[p];
+        if (n <= 0 || m <= 0) continue;
+        lone = std::max(lone, std::min(f64_cost(n, m, 4, 64), f64_cost(n, m, 8, 64)));
+        const double ns = (double)((n + 127) / 128), lat = (double)m + 63.0 + 64.0 * ns;
+        lat_max = std::max(lat_max, lat);
+        slots += ns * lat;
+    }
+    const double t_split = (script ? 0.318 : 0.138) + (script ? 7.40e-5 : 6.53e-5) * std::max(lat_max, slots / 256.0);
+    const double t_lone = (script ? 0.359 : 0.140) + (script ? 5.44e-5 : 5.09e-5) * lone;
+    return t_split < t_lone;
+}
+
 // the next run's SPLIT epoch, zeroing the hand-off words first when no word may carry a tag of its own (see split_epoch)
 hipError_t next_split_epoch(sed_batch *b, hipStream_t s, uint32_t *epoch) {
     *epoch = b->split_epoch % 32767u + 1u;
@@ -705,7 +727,8 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
         // step outweighs the twice as many hand-offs (per call, 500^2: 150 us at R = 4, tools/fp64_call_scaling.py)
         // A lane pair past 256 cells also goes SPLIT: 30^2 distance-only took 45 us per call on the lane kernel,
         // 32 us SPLIT (10^2: 27 against 33 us)
-        split = (c->opt_split == 1 || (npairs <= 256 && (nwave_f64 > 0 || lane_cells_f64 > 256.0))) &&
+        split = (c->opt_split == 1 || (npairs <= 256 && (nwave_f64 > 0 || lane_cells_f64 > 256.0) &&
+                                       (npairs == 1 || f64_split_pays(len_a, len_b, npairs, (flags & SED_WANT_SCRIPT) != 0)))) &&
                 (!c->opt_R || c->opt_R == 2 || c->opt_R == 4);
         if (split) R = c->opt_R ? c->opt_R : 2;
         // (automatic route: its hand-off words, 24 B per column and stripe, stay under 4 GB)
@@ -820,7 +843,7 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
             // (fp64: D, L and T planes; SPLIT: three 64-bit {tag, D low | D high | L key and T} words)
             if (nstripes > 1) bndw += (nchunks + 2) * SW * (packed ? (split ? 2 : 1) : (split ? 6 : 4)) * (split ? nstripes : 1);
             if (b->tbpar && nstripes >= 3) {  // {exit column, ops} per stripe and column, then per 64-row band and column
-                const uint64_t nbands = ((uint64_t)nn + 63) / 64 - R;  // the bands of stripes 1 .. K-1
+                const uint64_t nbands = ((uint64_t)nn + 63) / 64 - 1;  // bands 1 .. nbt-1 (the banded emit's)
                 mapw += (nstripes + nbands) * (uint64_t)(mm + 1) * 2;
                 // band map: workgroups of 256 columns per band (a superset of the stripe map kernel's middle
                 // stripes + sink; the compose kernel's grid is derived from it, sed_launch_traceback_stripes)

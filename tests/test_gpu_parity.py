@@ -822,6 +822,31 @@ def test_fp64_split_forced_over_segments_and_r2_fallback(gpu, tables):
     _oracle_check(table, pairs[::7] + pairs[-6:], got[::7] + got[-6:])
 
 
+@pytest.mark.parametrize("script", [True, False])
+def test_fp64_split_gate(gpu, tables, script):
+    """The automatic fp64 SPLIT route of <= 256 pairs is gated on its cost model (sed_runtime.cpp: f64_split_pays):
+    128 long narrow pairs (2000 x 100, 16 stripes each, whose chains hold the resident workgroups mostly waiting on the
+    stripe lag) run one wave per pair; 16 pairs of 1000^2 run SPLIT.  Identical results on both routes, the oracle's
+    on a sample."""
+    table = tables[False]
+    rng = np.random.default_rng(9600 + script)
+    for shape, count, want_split in (((2000, 100), 128, False), ((1000, 1000), 16, True)):
+        pairs = [("".join(rng.choice(list(IUPAC), size=shape[0])), "".join(rng.choice(list(IUPAC), size=shape[1])))
+                 for _ in range(count)]
+        plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
+        gpu.set_costs(plan)
+        b = sedgpu.Batch(gpu, sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs], [plan.encode(y) for _, y in pairs]),
+                         script)
+        try:
+            assert (b.split_tasks > 0) == want_split, (shape, b.split_tasks)
+        finally:
+            b.close()
+        got = gpu_run(gpu, table, pairs, script=script)
+        assert gpu_run(gpu, table, pairs, script=script, split=1) == got
+        assert gpu_run(gpu, table, pairs, script=script, split=2) == got
+        _oracle_check(table, pairs[::16], got[::16])
+
+
 
 @pytest.mark.parametrize("table_name", ["costs.json", "int_literals", "frac_indel"])
 def test_fp64_segments_vs_oracle(gpu, tables, table_name):
