@@ -149,6 +149,15 @@ int sed_run_batch(sed_ctx *ctx,
 int sed_run_pair(sed_ctx *ctx, const uint8_t *codes_a, int32_t n, const uint8_t *codes_b, int32_t m, uint32_t flags,
                  double *out_dist, uint8_t *out_is_int, int32_t *out_len, uint32_t *out_ops);
 
+/* sed_run_pair in two halves (round 6): sed_pair_submit uploads the pair and enqueues its kernels, then returns; the
+ * caller may do host work while the device computes (the drop-in module builds the edit-script records of
+ * generate_es, StringEditDistance.py:274-334, for the GUI's wagnerFisher -> create_paths -> generate_es call,
+ * gui.py:360,385-391); sed_pair_wait then waits and writes the results exactly as sed_run_pair would.  The inputs may
+ * be freed once submit returns.  One pair in flight per context: until sed_pair_wait, sed_set_costs, sed_run_batch,
+ * sed_run_pair, sed_full_matrix and another submit fail with SED_E_STATE. */
+int sed_pair_submit(sed_ctx *ctx, const uint8_t *codes_a, int32_t n, const uint8_t *codes_b, int32_t m, uint32_t flags);
+int sed_pair_wait(sed_ctx *ctx, double *out_dist, uint8_t *out_is_int, int32_t *out_len, uint32_t *out_ops);
+
 /* Device-resident batch: upload once, run many times (bench), fetch results. */
 sed_batch *sed_batch_create(sed_ctx *ctx,
                             const uint8_t *codes_a, const int64_t *off_a, const int32_t *len_a,

@@ -210,6 +210,7 @@ class DPMatrix:
         self._final = None
         self._full = None
         self._script = None
+        self._skel = None  # generate_es records built during the script run, for its canonical path (_run)
         self._cells = {}
         self._edges = {}
         self._rows = {}
@@ -224,7 +225,18 @@ class DPMatrix:
     def _run(self, want_script):
         ctx = sedgpu.context()
         ctx.set_costs(self._plan)
-        d, is_int, ln, ops = ctx.run_pair(self._bcodes[0], self._bcodes[1], want_script, no_len=not want_script)
+        a, b = self._bcodes
+        if want_script and self.n + self.m >= _SKEL_MIN and hasattr(ctx, "submit_pair"):
+            # the GUI's call (wagnerFisher -> create_paths -> generate_es, gui.py:360,385-391): the edit script's
+            # records (at least max(n, m) of them) are built while the device computes the script, and generate_es
+            # of this matrix's canonical path only fills in their values (tools/es_build_bench.py: ~1/4 of the build)
+            ctx.submit_pair(a, b, True)
+            try:
+                self._skel = _sedhost.es_skeleton(max(self.n, self.m))
+            finally:
+                d, is_int, ln, ops = ctx.wait_pair()
+        else:
+            d, is_int, ln, ops = ctx.run_pair(a, b, want_script, no_len=not want_script)
         self._final = int(d) if is_int else d
         if want_script:
             self._script = sedgpu.unpack_ops(ops, (0,), 0, int(ln))
@@ -310,6 +322,9 @@ class DPMatrix:
     def __repr__(self):
         return '[' + ', '.join(repr(r) for r in self) + ']'
 
+
+# script calls of at least this many symbols (n + m) build their generate_es records during the device run (_run)
+_SKEL_MIN = 512
 
 # One-deep predictor of the caller's pattern: True when the matrix of the previous wagnerFisher call
 # was asked for its script (the GUI: wagnerFisher -> create_paths -> generate_es).  The next call then
@@ -523,7 +538,13 @@ def generate_es(path, str1, str2):
     es = []
     if ops is not None and len(ops) == len(path) - 1:
         if type(str1) is str and type(str2) is str:
-            return _sedhost.es_from_ops(np.asarray(ops, np.uint8).tobytes(), str1, str2)
+            codes = np.asarray(ops, np.uint8).tobytes()
+            dp = getattr(path, '_dp', None)
+            skel = dp._skel if isinstance(dp, DPMatrix) else None
+            if skel is not None and ops is dp._script and str1 == dp.str1 and str2 == dp.str2:
+                dp._skel = None  # (each call returns new records: the next one builds its own)
+                return _sedhost.es_fill(skel[0], skel[1], codes, str1, str2)
+            return _sedhost.es_from_ops(codes, str1, str2)
         for op, nxt in zip(ops, path[1:]):
             es.append(_op_record(_OPNAME[op], str1, str2, nxt.i, nxt.j))
         return es

@@ -79,6 +79,7 @@ struct sed_ctx {
     void *pin = nullptr;
     size_t pin_cap = 0;
     bool pin_busy = false;  // a copy from / to `pin` may still be in flight on `stream`
+    bool pair_pending = false;  // sed_pair_submit enqueued the scratch batch; sed_pair_wait has not fetched it
 
     int fail(int code, const char *fmt, ...) {
         char buf[512];
@@ -1708,6 +1709,7 @@ int sed_set_option(sed_ctx *c, int key, int value) {
 int sed_set_costs(sed_ctx *c, int K, const double *sub, const uint8_t *sub_int, double ins, int ins_is_int,
                   double del, int del_is_int) {
     if (!c) return SED_E_ARG;
+    if (c->pair_pending) return c->fail(SED_E_STATE, "a submitted pair has not been waited for");
     if (K < 1 || K > 255 || !sub || !sub_int) return c->fail(SED_E_ARG, "bad cost table (K=%d)", K);
     if (!std::isfinite(ins) || !std::isfinite(del)) return c->fail(SED_E_ARG, "non-finite insert/delete cost");
     for (int e = 0; e < K * K; ++e)
@@ -1990,6 +1992,7 @@ int sed_run_batch(sed_ctx *c, const uint8_t *codes_a, const int64_t *off_a, cons
                   double *out_dist, uint8_t *out_is_int, int32_t *out_len, uint32_t *out_ops,
                   const int64_t *ops_off) {
     if (!c) return SED_E_ARG;
+    if (c->pair_pending) return c->fail(SED_E_STATE, "a submitted pair has not been waited for");
     (void)hipSetDevice(c->device);
     if (!c->scratch) {
         c->scratch = new sed_batch();
@@ -2043,9 +2046,41 @@ int sed_run_pair(sed_ctx *c, const uint8_t *codes_a, int32_t n, const uint8_t *c
                          (flags & SED_WANT_SCRIPT) && out_ops ? &off : nullptr);
 }
 
+int sed_pair_submit(sed_ctx *c, const uint8_t *codes_a, int32_t n, const uint8_t *codes_b, int32_t m, uint32_t flags) {
+    if (!c) return SED_E_ARG;
+    if (c->pair_pending) return c->fail(SED_E_STATE, "a submitted pair has not been waited for");
+    if (n < 0 || m < 0 || (n && !codes_a) || (m && !codes_b)) return c->fail(SED_E_ARG, "bad pair arguments");
+    (void)hipSetDevice(c->device);
+    if (!c->scratch) {
+        c->scratch = new sed_batch();
+        c->scratch->ctx = c;
+        c->scratch->time_every = 0;
+    }
+    static const uint8_t none = 0;
+    const int64_t off = 0;
+    int rc = fill_batch(c->scratch, n ? codes_a : &none, &off, &n, m ? codes_b : &none, &off, &m, 1,
+                        flags & ~(uint32_t)SED_PIPELINE);
+    if (rc == SED_OK) rc = run_batch(c->scratch);
+    c->pair_pending = rc == SED_OK;
+    return rc;
+}
+
+int sed_pair_wait(sed_ctx *c, double *out_dist, uint8_t *out_is_int, int32_t *out_len, uint32_t *out_ops) {
+    if (!c) return SED_E_ARG;
+    if (!c->pair_pending) return c->fail(SED_E_STATE, "no pair submitted");
+    c->pair_pending = false;
+    (void)hipSetDevice(c->device);
+    const int64_t off = 0;
+    int32_t len = 0;
+    const bool script = (c->scratch->flags & SED_WANT_SCRIPT) != 0;
+    return fetch_results(c->scratch, out_dist, out_is_int, out_len ? out_len : &len, script ? out_ops : nullptr,
+                         script && out_ops ? &off : nullptr);
+}
+
 int sed_full_matrix(sed_ctx *c, const uint8_t *codes_a, int32_t n, const uint8_t *codes_b, int32_t m, double *D,
                     uint8_t *M) {
     if (!c) return SED_E_ARG;
+    if (c->pair_pending) return c->fail(SED_E_STATE, "a submitted pair has not been waited for");
     if (n < 0 || m < 0 || !D || !M || (n && !codes_a) || (m && !codes_b)) return c->fail(SED_E_ARG, "bad arguments");
     (void)hipSetDevice(c->device);
     if (!c->have_costs) return c->fail(SED_E_STATE, "sed_set_costs() was not called");

@@ -555,6 +555,122 @@ static PyObject *es_from_ops(PyObject *self, PyObject *args) {
     return r;
 }
 
+/* ------------------------------------------------------------------ ES skeletons
+ * es_skeleton(count) -> (records, sides): `count` generate_es records whose values are still None, built ahead of the
+ * op codes (the drop-in module builds them while the device computes the script), and a bytes object holding each
+ * record's source and destination dict (borrowed pointers into the records) for es_fill.
+ * es_fill(records, sides, ops, str1, str2) -> records: es_from_ops' values written into the first len(ops) records
+ * (records past len(ops) are dropped; if there are fewer, the rest are built here).  The result equals
+ * es_from_ops(ops, str1, str2). */
+static int fill_side(PyObject *d, PyObject *s, Py_ssize_t len, Py_ssize_t i) {
+    PyObject *ch = char_at(s, len, i);
+    if (!ch) return -1;
+    PyObject *idx = int_of(i);
+    const int rc = (!idx || PyDict_SetItem(d, K_CHARACTER, ch) || PyDict_SetItem(d, K_INDEX, idx)) ? -1 : 0;
+    Py_DECREF(ch);
+    Py_XDECREF(idx);
+    return rc;
+}
+
+static PyObject *es_skeleton_impl(PyObject *self, PyObject *args) {
+    Py_ssize_t count;
+    if (!PyArg_ParseTuple(args, "n", &count)) return NULL;
+    if (count < 0) count = 0;
+    PyObject *list = PyList_New(count), *sides = PyBytes_FromStringAndSize(NULL, 2 * count * (Py_ssize_t)sizeof(PyObject *));
+    if (!list || !sides) goto fail;
+    PyObject **sp = (PyObject **)PyBytes_AS_STRING(sides);
+    for (Py_ssize_t k = 0; k < count; ++k) {
+        PyObject *src = PyDict_New(), *dst = PyDict_New(), *rec = PyDict_New();
+        if (!src || !dst || !rec || PyDict_SetItem(src, K_CHARACTER, Py_None) || PyDict_SetItem(src, K_INDEX, Py_None) ||
+            PyDict_SetItem(dst, K_CHARACTER, Py_None) || PyDict_SetItem(dst, K_INDEX, Py_None) ||
+            PyDict_SetItem(rec, K_OPERATION, Py_None) || PyDict_SetItem(rec, K_SOURCE, src) ||
+            PyDict_SetItem(rec, K_DESTINATION, dst)) {
+            Py_XDECREF(src);
+            Py_XDECREF(dst);
+            Py_XDECREF(rec);
+            goto fail;
+        }
+        sp[2 * k] = src;  /* (borrowed: the record holds them) */
+        sp[2 * k + 1] = dst;
+        Py_DECREF(src);
+        Py_DECREF(dst);
+        PyList_SET_ITEM(list, k, rec);
+    }
+    PyObject *ret = PyTuple_Pack(2, list, sides);
+    Py_DECREF(list);
+    Py_DECREF(sides);
+    return ret;
+fail:
+    Py_XDECREF(list);
+    Py_XDECREF(sides);
+    return NULL;
+}
+
+static PyObject *es_fill_impl(PyObject *self, PyObject *args) {
+    PyObject *list, *sides, *s1, *s2;
+    Py_buffer ops;
+    if (!PyArg_ParseTuple(args, "O!O!y*UU", &PyList_Type, &list, &PyBytes_Type, &sides, &ops, &s1, &s2)) return NULL;
+    const unsigned char *op = (const unsigned char *)ops.buf;
+    const Py_ssize_t n = ops.len, l1 = PyUnicode_GET_LENGTH(s1), l2 = PyUnicode_GET_LENGTH(s2);
+    Py_ssize_t have = PyList_GET_SIZE(list);
+    if (PyBytes_GET_SIZE(sides) != 2 * have * (Py_ssize_t)sizeof(PyObject *)) {
+        PyErr_SetString(PyExc_ValueError, "es_fill: records and sides differ");
+        goto fail;
+    }
+    if (PyUnicode_READY(s1) < 0 || PyUnicode_READY(s2) < 0 || ints_reserve((l1 > l2 ? l1 : l2) + 1) < 0) goto fail;
+    if (have > n) {  /* drop the records past the script */
+        if (PyList_SetSlice(list, n, have, NULL) < 0) goto fail;
+        have = n;
+    }
+    PyObject *const *sp = (PyObject *const *)PyBytes_AS_STRING(sides);
+    Py_ssize_t r = 0, c = 0;
+    for (Py_ssize_t k = 0; k < n; ++k) {
+        if (op[k] > 2) {
+            PyErr_SetString(PyExc_ValueError, "op code > 2");
+            goto fail;
+        }
+        if (op[k] != 1) ++c;
+        if (op[k] != 0) ++r;
+        PyObject *name = op[k] == 0 ? S_INSERT : (op[k] == 1 ? S_DELETE : S_UPDATE);
+        if (k < have) {
+            if (PyDict_SetItem(PyList_GET_ITEM(list, k), K_OPERATION, name) || fill_side(sp[2 * k], s1, l1, r - 1) ||
+                fill_side(sp[2 * k + 1], s2, l2, c - 1))
+                goto fail;
+        } else {  /* more ops than skeleton records: build the rest */
+            PyObject *src = side(s1, l1, r - 1);
+            if (!src) goto fail;
+            PyObject *dst = side(s2, l2, c - 1);
+            PyObject *rec = dst ? PyDict_New() : NULL;
+            const int bad = !rec || PyDict_SetItem(rec, K_OPERATION, name) || PyDict_SetItem(rec, K_SOURCE, src) ||
+                            PyDict_SetItem(rec, K_DESTINATION, dst) || PyList_Append(list, rec);
+            Py_DECREF(src);
+            Py_XDECREF(dst);
+            Py_XDECREF(rec);
+            if (bad) goto fail;
+        }
+    }
+    PyBuffer_Release(&ops);
+    Py_INCREF(list);
+    return list;
+fail:
+    PyBuffer_Release(&ops);
+    return NULL;
+}
+
+static PyObject *es_skeleton(PyObject *self, PyObject *args) {
+    const int was = PyGC_Disable();
+    PyObject *r = es_skeleton_impl(self, args);
+    if (was) PyGC_Enable();
+    return r;
+}
+
+static PyObject *es_fill(PyObject *self, PyObject *args) {
+    const int was = PyGC_Disable();
+    PyObject *r = es_fill_impl(self, args);
+    if (was) PyGC_Enable();
+    return r;
+}
+
 static PyObject *rev_es(PyObject *self, PyObject *es) {
     const int was = PyGC_Disable();
     PyObject *r = rev_es_impl(self, es);
@@ -742,6 +858,8 @@ static PyMethodDef methods[] = {
     {"length_windows", length_windows, METH_VARARGS, "co-optimal path length windows per cell"},
     {"count_paths", count_paths, METH_VARARGS, "number of co-optimal paths (Python int)"},
     {"es_from_ops", es_from_ops, METH_VARARGS, "generate_es over a canonical op sequence"},
+    {"es_skeleton", es_skeleton, METH_VARARGS, "generate_es records with their values still None, and their side dicts"},
+    {"es_fill", es_fill, METH_VARARGS, "es_from_ops' values written into es_skeleton records"},
     {"rev_es", rev_es, METH_O, "generate_rev_es"},
     {"seq_from_es", seq_from_es, METH_O, "generate_sequence_from_es"},
     {"patching", patching, METH_VARARGS, "patching(es, str1) -> (error_code, str)"},

@@ -97,6 +97,8 @@ SIGNATURES = [
     ("sed_batch_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("sed_run_pair", C.c_int, [C.c_void_p, C.c_char_p, C.c_int32, C.c_char_p, C.c_int32, C.c_uint32, C.c_void_p,
                                C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("sed_pair_submit", C.c_int, [C.c_void_p, C.c_char_p, C.c_int32, C.c_char_p, C.c_int32, C.c_uint32]),
+    ("sed_pair_wait", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("sed_batch_results", C.c_int, [C.c_void_p, _f64p, _u8p, _i32p, C.c_void_p, C.c_void_p]),
     ("sed_batch_dp_launches", C.c_int, [C.c_void_p]),
     ("sed_batch_device_results", C.c_int, [C.c_void_p] + [C.POINTER(C.c_uint64)] * 5),
@@ -153,6 +155,7 @@ class Context:
         self._cost_key = None
         self._cost_plan = None
         self._pair_out = None
+        self._pending = None  # (want_script, script words) of a submit_pair not yet waited for
 
     def close(self):
         # a forked child must not call into the parent's HIP context (it would destroy or hang on it)
@@ -243,6 +246,31 @@ class Context:
                                     C.addressof(r[1]), C.addressof(r[2]), ops_ptr)
         if rc != 0:
             self._check(rc, "sed_run_pair")
+        return r[0].value, r[1].value, r[2].value, ops
+
+    def submit_pair(self, codes_a, codes_b, want_script, no_len=False):
+        """run_pair's first half (sed_pair_submit): the pair's kernels are enqueued and this returns at once;
+        wait_pair() returns what run_pair would have."""
+        if self._pid != os.getpid():
+            self._check(0, "sed_pair_submit")
+        flags = SED_WANT_SCRIPT if want_script else (SED_NO_LEN if no_len else 0)
+        rc = self._lib.sed_pair_submit(self.ptr, codes_a, len(codes_a), codes_b, len(codes_b), flags)
+        if rc != 0:
+            self._check(rc, "sed_pair_submit")
+        self._pending = (want_script, (len(codes_a) + len(codes_b) + 15) // 16)
+
+    def wait_pair(self):
+        """(dist, is_int, len, ops u32[] | None) of the pair submit_pair enqueued (sed_pair_wait)."""
+        want_script, words = self._pending
+        self._pending = None
+        r = self._pair_out
+        if r is None:
+            r = self._pair_out = (C.c_double(), C.c_uint8(), C.c_int32())
+        ops = np.zeros(max(1, words), np.uint32) if want_script else None
+        rc = self._lib.sed_pair_wait(self.ptr, C.addressof(r[0]), C.addressof(r[1]), C.addressof(r[2]),
+                                     ops.ctypes.data if want_script else None)
+        if rc != 0:
+            self._check(rc, "sed_pair_wait")
         return r[0].value, r[1].value, r[2].value, ops
 
     def full_matrix(self, codes_a, codes_b):

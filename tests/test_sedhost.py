@@ -98,6 +98,27 @@ def test_es_from_ops_matches_records(SED):
         _sedhost.es_from_ops(bytes([0]), "", "A")  # str1[-1] of an empty string, as the reference
 
 
+def test_es_skeleton_fill_equals_es_from_ops():
+    """The drop-in module builds generate_es' records during the device run (es_skeleton) and fills their values after
+    it (es_fill): equal to es_from_ops whatever the skeleton's size (fewer, as many or more records than ops), with
+    independent dicts per record, also on non-ASCII strings (the slow character path)."""
+    rng = random.Random(4)
+    for trial in range(300):
+        al = "ACGUN" if trial % 10 else "ACGéU"
+        s1 = "".join(rng.choice(al) for _ in range(rng.randint(1, 40)))
+        s2 = "".join(rng.choice(al) for _ in range(rng.randint(1, 40)))
+        ops = [2] * min(len(s1), len(s2)) + [0] * max(0, len(s2) - len(s1)) + [1] * max(0, len(s1) - len(s2))
+        rng.shuffle(ops)
+        want = _sedhost.es_from_ops(bytes(ops), s1, s2)
+        recs, sides = _sedhost.es_skeleton(rng.choice([0, 1, max(len(s1), len(s2)), len(ops), len(ops) + 5]))
+        got = _sedhost.es_fill(recs, sides, bytes(ops), s1, s2)
+        assert got == want and got is recs
+        assert len({id(r["source"]) for r in got} | {id(r["destination"]) for r in got}) == 2 * len(got)
+    with pytest.raises(IndexError):
+        recs, sides = _sedhost.es_skeleton(1)
+        _sedhost.es_fill(recs, sides, bytes([0]), "", "A")
+
+
 def _rand_side(rng):
     d = {}
     keys = ["character", "index"]

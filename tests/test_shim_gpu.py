@@ -195,6 +195,42 @@ def test_script_hint_runs_agree(SED):
     assert SED.wagnerFisher("ACGU", "AGU")._script is None  # nobody asked for the last script: distance-only again
 
 
+def test_gui_call_builds_es_records_during_the_run(SED):
+    """The GUI's call (wagnerFisher -> create_paths -> generate_es, gui.py:360,385-391) on pairs of >= 512 symbols
+    submits the pair (sed_pair_submit), builds generate_es' records while the device runs and fills them after
+    (sed_pair_wait, _sedhost.es_fill): the records equal es_from_ops', a second generate_es returns new ones, and the
+    context refuses another call while a pair is in flight (SED_E_STATE)."""
+    import _sedhost
+    import sedcost
+    import sedgpu
+    import synth
+    for n, m, user in ((700, 650, True), (200, 200, False), (4096, 4096, True)):
+        s1, s2 = synth.pair_strings(n + m, n, m)
+        SED._script_hint = True
+        dp = SED.wagnerFisher(s1, s2, user)
+        assert (dp._skel is not None) == (n + m >= SED._SKEL_MIN)
+        p0 = SED.create_paths(dp)[0]
+        es = SED.generate_es(p0, s1, s2)
+        assert dp._skel is None
+        want = _sedhost.es_from_ops(np.asarray(p0.ops, np.uint8).tobytes(), s1, s2)
+        assert es == want and len(es) == len(p0.ops)
+        es2 = SED.generate_es(p0, s1, s2)
+        assert es2 == es and es2 is not es and es2[0] is not es[0]
+        assert SED.patching(es, s1) == (0, s2)
+    ctx = sedgpu.context()
+    plan = sedcost.pair_plan(SED._table(False), "ACGUACGU", "ACGGU")
+    ctx.set_costs(plan)
+    a, b = plan.encode_bytes("ACGUACGU"), plan.encode_bytes("ACGGU")
+    ctx.submit_pair(a, b, True)
+    try:
+        assert ctx._lib.sed_pair_submit(ctx.ptr, a, len(a), b, len(b), 1) == -6  # SED_E_STATE: one pair in flight
+        with pytest.raises(sedgpu.SedError, match="waited for"):
+            ctx.run_pair(a, b, False)
+    finally:
+        got = ctx.wait_pair()
+    assert got[:3] == ctx.run_pair(a, b, True)[:3]
+
+
 def _ref_search_collection(query, vector_type, collection, method, return_dict=None, callback=None):
     """IRMethods.search_collection (IRMethods.py:443-477) for method == wf_score: one wagnerFisher per
     document through the drop-in module, exactly as the unchanged caller does."""

@@ -10,4 +10,7 @@ cat $O/dot_chain.txt
 timeout -k 10 200 python3 tools/call_breakdown.py > $O/call_breakdown.txt 2>&1
 timeout -k 10 200 python3 tools/call_latency.py > $O/call_latency.txt 2>&1
 cat $O/call_breakdown.txt $O/call_latency.txt
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 tools/script_calls.py > $O/kt.log 2>&1
+ls -la $O/kt
+cp $O/kt/*.csv $O/ 2>/dev/null || true
 echo finished
