@@ -38,10 +38,34 @@ struct sed_result {
 // starts its op accumulator at 0, so the bits past the last op inside the last op word are 0 already; this zeroes the
 // spare words after it (lanes lane, lane + stride, ...), so the packed buffer is a function of the scripts alone,
 // whatever the buffer held before (sed.h).  Every script-writing kernel calls it once per pair.
+#ifndef SED_PAD_ZERO
+#define SED_PAD_ZERO 1  // (0: A/B builds only; the padding is then whatever the buffer held)
+#endif
 __device__ __forceinline__ void zero_script_tail(uint32_t *__restrict__ out, int len, int n, int m, int lane,
                                                  int stride) {
+    if (!SED_PAD_ZERO) return;
     const int end = (n + m + 15) >> 4;
     for (int w = ((len > 0 ? len : 0) + 15) / 16 + lane; w < end; w += stride) out[w] = 0u;
+}
+
+// The same for the lane-per-pair walks, where each lane owns a pair: the wave stores every active lane's spare words
+// [ceil(len/16), ceil((n+m)/16)) pair by pair as one coalesced run, its active lanes side by side.  (Each lane storing
+// its own pair's words one after another scattered every store instruction over 64 pairs: config 3's per-cell-code
+// traceback took 1.68-1.91 instead of 0.75 ms, profiles/r06/pad_ab.)  Lanes that left the kernel own no pair here.
+__device__ __forceinline__ void zero_script_tails_wave(uint32_t *__restrict__ ops, uint64_t off, int len, int n, int m) {
+    if (!SED_PAD_ZERO) return;
+    const uint64_t act = __ballot(1);
+    const int rank = __popcll(act & ((1ull << (threadIdx.x & 63)) - 1ull)), nact = __popcll(act);
+    const int w0 = ((len > 0 ? len : 0) + 15) >> 4, w1 = (n + m + 15) >> 4;
+    uint64_t todo = __ballot(w0 < w1);
+    while (todo) {
+        const int l = __builtin_ctzll(todo);
+        todo &= todo - 1ull;
+        const int a = __builtin_amdgcn_readlane(w0, l), b = __builtin_amdgcn_readlane(w1, l);
+        const uint64_t o = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off, l) |
+                           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(off >> 32), l) << 32);
+        for (int w = a + rank; w < b; w += nact) ops[o + (uint64_t)w] = 0u;
+    }
 }
 
 // Integer kernel constants (offset-key space, see sed_kernels.hip):

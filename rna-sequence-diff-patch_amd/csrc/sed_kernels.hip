@@ -1902,7 +1902,8 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
     const int SG = (m + SW - 1 + G - 1) / G * G;
     const uint64_t stripe_words = (uint64_t)(SG / G) * (SW * 4u);
     uint32_t *out = ops + d.ops_off;
-    int q = res[pair].len;  // ops in the script; written from position q-1 down to 0
+    const int L0 = res[pair].len;
+    int q = L0;  // ops in the script; written from position q-1 down to 0
     int i = n, j = m;
     uint32_t acc = 0, bad = 0;
     auto emit = [&](uint32_t op) {
@@ -1957,7 +1958,7 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
     while (j > 0) { emit(0u); --j; }
     while (i > 0) { emit(1u); --i; }
     if (bad || q != 0) res[pair].err = SED_ERR_TB_LENGTH;
-    zero_script_tail(out, res[pair].len, n, m, 0, 1);
+    zero_script_tails_wave(ops, d.ops_off, L0, n, m);
 }
 
 

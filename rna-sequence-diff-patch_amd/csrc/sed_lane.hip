@@ -131,7 +131,7 @@ __global__ __launch_bounds__(256) void sed_lane_i32_kernel(const sed_pair_desc *
             j -= (op != 1);
             --k;
         }
-        zero_script_tail(po, L, n, m, 0, 1);
+        zero_script_tails_wave(ops, d.ops_off, L, n, m);
     }
 }
 
