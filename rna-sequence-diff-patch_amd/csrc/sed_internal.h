@@ -34,6 +34,7 @@ struct sed_result {
 #define SED_ERR_TB_GUARD 4       // traceback: more tile visits than any path can need
 #define SED_ERR_TB_LENGTH 5      // traceback: the walk's op count differs from the sink's L
 
+#ifdef __HIPCC__  // (device helpers: the runtime, compiled by g++, does not see them)
 // Script padding.  A pair's script region holds ceil((n+m)/16) words; its ops fill ceil(len/16) of them.  Every walk
 // starts its op accumulator at 0, so the bits past the last op inside the last op word are 0 already; this zeroes the
 // spare words after it (lanes lane, lane + stride, ...), so the packed buffer is a function of the scripts alone,
@@ -67,6 +68,7 @@ __device__ __forceinline__ void zero_script_tails_wave(uint32_t *__restrict__ op
         for (int w = a + rank; w < b; w += nact) ops[o + (uint64_t)w] = 0u;
     }
 }
+#endif  // __HIPCC__
 
 // Integer kernel constants (offset-key space, see sed_kernels.hip):
 //   costrow[a]   byte b = (cost(a -> b) - insert - delete - 1) & 0xFF  (32-bit keys)
