@@ -1905,6 +1905,9 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
     const int L0 = res[pair].len;
     int q = L0;  // ops in the script; written from position q-1 down to 0
     int i = n, j = m;
+    // the padding past the script first: zeroed after the walk instead, config 3's traceback span is 1.65-1.90 against
+    // 0.70-0.76 ms (step 2.60-2.76 against 2.57-2.58 ms; none at all: 2.56-2.57 ms, profiles/r06/pad_ab)
+    zero_script_tails_wave(ops, d.ops_off, L0, n, m);
     uint32_t acc = 0, bad = 0;
     auto emit = [&](uint32_t op) {
         if (q <= 0) {  // the walk is longer than the sink's L: never write below the pair's script
@@ -1958,7 +1961,6 @@ __global__ __launch_bounds__(64) void sed_traceback_kernel(const sed_pair_desc *
     while (j > 0) { emit(0u); --j; }
     while (i > 0) { emit(1u); --i; }
     if (bad || q != 0) res[pair].err = SED_ERR_TB_LENGTH;
-    zero_script_tails_wave(ops, d.ops_off, L0, n, m);
 }
 
 
@@ -2075,9 +2077,9 @@ __global__ __launch_bounds__(64) void sed_traceback_window_kernel(const sed_pair
     if (d.lane) return;  // scripted by sed_lane.hip
     const uint32_t q0 = (uint32_t)__builtin_amdgcn_readfirstlane(res[pair].len);
     uint32_t bad = 0;
+    zero_script_tail(ops + d.ops_off, (int)q0, d.n, d.m, lane, 64);  // (before the walk, as sed_traceback_kernel)
     const uint32_t q = window_walk<R, false>(d, d.n, d.m, 0, q0, lane, tb, ops + d.ops_off, pat, bad);
     if ((bad | q) && lane == 0) res[pair].err = SED_ERR_TB_LENGTH;
-    zero_script_tail(ops + d.ops_off, (int)q0, d.n, d.m, lane, 64);
 }
 
 
@@ -2857,6 +2859,9 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
     int visit = 0;  // debug dumps: 136 words per tile visit (entry keys, initial keys, coordinates)
 #endif
     uint32_t *out = ops + d.ops_off;
+#ifndef SED_TB_DEBUG
+    zero_script_tail(out, (int)q0, n, m, lane, 64);  // (before the walk, as sed_traceback_kernel)
+#endif
     uint32_t q = q0, err = 0;
     uint64_t acc = 0;  // the last 32 ops, the latest (position q) in bits 1:0
     auto emit = [&](uint32_t op) {  // sink -> origin (trailing border runs)
@@ -2933,7 +2938,6 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
     if (lane == 0) out[((n + m + 15) >> 4) + 63] = err | ((uint32_t)visit << 8);  // (debug: no error, the dumps stay)
 #else
     if (err && lane == 0) res[pair].err = (uint8_t)err;
-    zero_script_tail(out, (int)q0, n, m, lane, 64);
 #endif
 }
 

@@ -111,6 +111,7 @@ __global__ __launch_bounds__(256) void sed_lane_i32_kernel(const sed_pair_desc *
     res[pair] = r;
     if constexpr (TB) {
         // canonical path, sink -> origin; op k of the script (origin -> sink) at bits 2(k&15) of word k>>4
+        zero_script_tails_wave(ops, d.ops_off, L, n, m);  // (before the walk, as sed_traceback_kernel)
         uint32_t *po = ops + d.ops_off;
         int i = n, j = m, k = L - 1;
         uint32_t w = 0;
@@ -131,7 +132,6 @@ __global__ __launch_bounds__(256) void sed_lane_i32_kernel(const sed_pair_desc *
             j -= (op != 1);
             --k;
         }
-        zero_script_tails_wave(ops, d.ops_off, L, n, m);
     }
 }
 
