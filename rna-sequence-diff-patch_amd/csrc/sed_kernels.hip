@@ -2564,11 +2564,12 @@ __global__ __launch_bounds__(64) void sed_tb_bandemit_kernel(const sed_pair_desc
 // The walk of one tile from state S; returns the state of the first cell it did not take (outside the
 // tile: above it, left of its band's window, or at column 0 for C0), low 16 bits.  One loop per code word with a
 // single exit test: the next state's word bits (S & SED_TB_WORD) must still be the word's tag.
-template <bool C0>  // C0: chunk-0 tile, whose window reaches the column-0 border: stop at j = 0
-__device__ __forceinline__ uint32_t ck_walk(const uint32_t (&W)[8], uint32_t S, uint32_t &q, uint64_t &acc,
+template <bool C0, int NW>  // C0: chunk-0 tile, whose window reaches the column-0 border: stop at j = 0
+__device__ __forceinline__ uint32_t ck_walk(const uint32_t (&W)[NW], uint32_t S, uint32_t &q, uint64_t &acc,
                                             uint32_t &err, uint32_t *__restrict__ out, int jcol) {
+    static_assert(NW <= 15, "the step field (S bits 7..14) and the word tags need a free bit 15");
 #pragma unroll
-    for (int w = 7; w >= 0; --w) {
+    for (int w = NW - 1; w >= 0; --w) {
         const uint32_t tag = (uint32_t)w << 11;
         if ((S & SED_TB_WORD) == tag) {
             // Every op moves the walk at least one step left, so one word yields at most 16 ops.  Inside the loop
@@ -2617,7 +2618,10 @@ __device__ __forceinline__ uint32_t ck_walk(const uint32_t (&W)[8], uint32_t S, 
 #ifndef SED_CK_VHOLD
 #define SED_CK_VHOLD 1
 #endif
-#define SED_CK_SELB (64 + 132)
+// NW code words per lane cover sweep steps 0 .. 16 NW - 1: 8 for one chunk's tile (127 steps), 12 for a wide window
+// of two chunks (191 steps); topb holds 16 NW + 4 words, each band's selector copy 64 more
+#define SED_CK_NX(NW) (16 * (NW) + 4)
+#define SED_CK_SELB(NW) (64 + SED_CK_NX(NW))
 template <int R> struct CkVHold { static constexpr bool value = SED_CK_VHOLD && R == 16; };
 // lanes 0 .. n-1 have reached their window at sweep step sig (sig0(r) = r - r/R + G - 1 is nondecreasing)
 template <int R> constexpr int ck_active_lanes(int sig) {
@@ -2644,6 +2648,14 @@ template <int R> constexpr int ck_band_start(int sig) {
     for (int b = 1; b < G; ++b)
         if (sig == (R - 1) * b + G - 1) return b;
     return 0;
+}
+
+// f(integral_constant<int, I>) for I = B .. E-1, expanded at compile time
+template <int B, int E, class F> __device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
 }
 
 // a word at a 32-bit byte offset from a uniform base: the scalar-base (saddr) load form, no 64-bit lane address
@@ -2704,11 +2716,12 @@ __device__ __forceinline__ CkPairCtx ck_pair_ctx(const sed_pair_desc &d, const i
 // One tile visit: tile (stripe k, band group Q, chunk c) recomputed from its checkpoints up to sweep step sig_end (FULL:
 // all 128 steps), the codes in W (lane r's code of step sigma in W[sigma >> 4], bits 2 (sigma & 15)); returns the lanes'
 // keys after the last step (the entry keys).
-template <int R, bool WAVE, bool FULL>
+template <int R, bool WAVE, bool FULL, int NW>
 __device__ __forceinline__ uint32_t ck_tile_sweep(const CkPairCtx &px, const int lane, const sed_i32_params &prm,
                                                   uint32_t *__restrict__ topb, uint32_t *__restrict__ selb, const int k,
                                                   const int Q, const int c, const int sig_end, uint32_t &one,
-                                                  uint32_t (&W)[8], uint32_t &vinit) {
+                                                  uint32_t (&W)[NW], uint32_t &vinit) {
+    constexpr int NX = SED_CK_NX(NW), SELB = SED_CK_SELB(NW), NH = (NX + 63) / 64;
     constexpr int ROWS = 64 * R, G = Grp<R>::G;  // a tile: G forward lanes (bands) of R rows
     constexpr int LR = R == 4 ? 2 : R == 8 ? 3 : 4;
     constexpr bool VHOLD = CkVHold<R>::value;
@@ -2735,12 +2748,13 @@ __device__ __forceinline__ uint32_t ck_tile_sweep(const CkPairCtx &px, const int
     // previous pair there)
     const bool above = Q >= 1 || k >= 1;  // (uniform) else row 0: the border
     const int kr = Q >= 1 ? k : k - 1, tr = Q >= 1 ? G * Q - 1 : 63, s0r = Q >= 1 ? 64 * c - G - 1 : 64 * c + 63 - G;
-    uint32_t rk[3] = {0, 0, 0}, wb[3];
+    uint32_t rk[NH], wb[NH];
     const uint32_t *rbase = px.rcp + sed_ck_row_word(R, max(kr, 0), ngroups, 0, tr);  // (uniform; read when above)
 #pragma unroll
-    for (int h = 0; h < 3; ++h) {
+    for (int h = 0; h < NH; ++h) {
         const int x = lane + 64 * h;
-        if (h < 2 || x < 132) {
+        rk[h] = 0u;
+        if (64 * (h + 1) <= NX || x < NX) {
             if (above) {
                 const uint32_t s = (uint32_t)min(max(s0r + x, 0), SG - 1);
                 rk[h] = ld_byte_off(rbase, ((s >> (6 - LR)) * (uint32_t)SED_CK_RW + (s & (uint32_t)(G - 1))) * 4u);
@@ -2761,9 +2775,9 @@ __device__ __forceinline__ uint32_t ck_tile_sweep(const CkPairCtx &px, const int
     }
     tp += 1u;  // diagonals carry the +1 of the delete candidate they were taken from
 #pragma unroll
-    for (int h = 0; h < 3; ++h) {
+    for (int h = 0; h < NH; ++h) {
         const int x = lane + 64 * h;
-        if (h < 2 || x < 132) {
+        if (64 * (h + 1) <= NX || x < NX) {
             const uint32_t v = (above && J0 - G + x >= 1) ? ck_to_tb(rk[h], prm) : SED_KB;
             topb[x] = v + 1u;
             const int col = J0 - (G - 1) + x;  // column of lane 0 at step x
@@ -2771,7 +2785,7 @@ __device__ __forceinline__ uint32_t ck_tile_sweep(const CkPairCtx &px, const int
             const uint32_t sv = col < 1 ? SED_SEL_SENT : i32_sel((wb[h] >> ((ci & 15) * 2)) & 3u);
             if constexpr (VHOLD) {  // band b's copy: the sentinel left of its window (x < G - 1 - b)
 #pragma unroll
-                for (int b = 0; b < G; ++b) selb[b * SED_CK_SELB + 64 + x] = x < G - 1 - b ? SED_SEL_SENT : sv;
+                for (int b = 0; b < G; ++b) selb[b * SELB + 64 + x] = x < G - 1 - b ? SED_SEL_SENT : sv;
             } else {
                 selb[64 + x] = sv;
             }
@@ -2798,8 +2812,8 @@ __device__ __forceinline__ uint32_t ck_tile_sweep(const CkPairCtx &px, const int
     vinit = V;
 #endif
     uint32_t tprev = dpp_shr1_add(topb[G - 1], V, one);  // diagonal of step G-1 (+1)
-    const uint32_t *selp = selb + (VHOLD ? band * SED_CK_SELB : 0) + 64 - lane;  // lane r's selector at step sigma
-    const int w_end = FULL ? 7 : sig_end >> 4;  // FULL: every word, whole
+    const uint32_t *selp = selb + (VHOLD ? band * SELB : 0) + 64 - lane;  // lane r's selector at step sigma
+    const int w_end = FULL ? NW - 1 : sig_end >> 4;  // FULL: every word, whole
     auto step = [&](const int sig, uint32_t &wv, const uint32_t topin, const uint32_t selv) {
         if (sig < G - 1) return;  // every lane holds
         const int bs = ck_band_start<R>(sig);  // folds to a constant in the unrolled sweep
@@ -2819,11 +2833,13 @@ __device__ __forceinline__ uint32_t ck_tile_sweep(const CkPairCtx &px, const int
         wv = __builtin_amdgcn_alignbit(mm, wv, 2);
         tprev = topv;
     };
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-        if (w > w_end) break;  // the path never needs later steps
+    // (the words expand through static_for: a #pragma unroll over 12 words gives up, and the steps' constants with it)
+    static_for<0, NW>([&](auto wc) {
+        constexpr int w = decltype(wc)::value;
+        if (w > w_end) return;  // the path never needs later steps
         if (!FULL && w == w_end) {  // up to the entry step exactly: the lanes then hold the entry keys
-            // the word's LDS inputs first, so the per-step exits do not serialise an LDS round trip per step
+            // the word's LDS inputs first (the compiler sinks them into the steps anyway; pinning them ahead of the exits
+            // with an asm use measured the same, profiles/r06/ck_wide)
             uint32_t tw[16], sw[16];
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
@@ -2841,11 +2857,11 @@ __device__ __forceinline__ uint32_t ck_tile_sweep(const CkPairCtx &px, const int
             for (int u = 0; u < 16; ++u) step(16 * w + u, W[w], topb[16 * w + u + 1], selp[16 * w + u]);
         }
         if (w < 4) W[w] |= px.hm[w];
-    }
+    });
     return V;
 }
 
-template <int R, bool WAVE>
+template <int R, bool WAVE, int NW>
 __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const int pair, const uint32_t q0,
                                                   const int lane, const uint32_t *__restrict__ seqa,
                                                   const uint32_t *__restrict__ seqb, const uint32_t *__restrict__ ck,
@@ -2885,12 +2901,18 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
                 break;
             }
             const int k = (i - 1) / ROWS, t = ((i - 1) % ROWS) / R, Q = t / G;
-            const int c = (j - 1 + t) >> 6;
-            const int J0 = 64 * c - G * Q + 1, rowbase = k * ROWS + 64 * Q;
+            const int ce = (j - 1 + t) >> 6;            // the entry cell's chunk
+            const int rowbase = k * ROWS + 64 * Q;
             const int re = i - rowbase - 1;             // the entry cell's tile row
-            const int sig_end = (j - J0 + G - 1) + re;  // the entry cell's sweep step (<= 126)
-            uint32_t W[8], vinit = 0;
-            const uint32_t ent = ck_tile_sweep<R, WAVE, false>(px, lane, prm, topb, selb, k, Q, c, sig_end, one, W, vinit);
+            // NW = 12: a window of two chunks (ce - 1, ce) when the entry step x inside its chunk is below re, i.e. when
+            // a diagonal path would leave chunk ce through its left edge before the tile's top: the path then crosses
+            // the row group in one visit instead of two, 151 against 93 sweep steps per visit but half the visits
+            // (22.3 -> 17.1 VALU per emitted op on config 4's pairs, tools/tb_window_model.py)
+            const int c = (NW > 8 && ce >= 1 && ((j - 1 + t) & 63) < re) ? ce - 1 : ce;
+            const int J0 = 64 * c - G * Q + 1;
+            const int sig_end = (j - J0 + G - 1) + re;  // the entry cell's sweep step (<= 16 NW - 2)
+            uint32_t W[NW], vinit = 0;
+            const uint32_t ent = ck_tile_sweep<R, WAVE, false, NW>(px, lane, prm, topb, selb, k, Q, c, sig_end, one, W, vinit);
             (void)vinit;
 #ifdef SED_TB_DEBUG
             if (visit < 32) {  // debug builds only (pair 0; its script words, 64 spare, then 136 words per visit v)
@@ -2916,8 +2938,8 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
             // ---- walk inside the tile ----
             const uint32_t qin = q;
             const uint32_t S0 = (uint32_t)re | ((uint32_t)sig_end << 7);
-            const uint32_t S = c == 0 ? ck_walk<true>(W, S0, q, acc, err, out, j)
-                                      : ck_walk<false>(W, S0, q, acc, err, out, j);
+            const uint32_t S = c == 0 ? ck_walk<true, NW>(W, S0, q, acc, err, out, j)
+                                      : ck_walk<false, NW>(W, S0, q, acc, err, out, j);
             if (err) break;
             if (q == qin) {  // no progress: give up rather than spin
                 err = SED_ERR_TB_STALL;
@@ -2941,16 +2963,23 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
 #endif
 }
 
-// waves per SIMD the checkpoint traceback is compiled for (A/B: SED_CKTB_WAVES; 1 = the compiler's choice), and its
+// waves per SIMD the checkpoint traceback is compiled for (A/B: SED_CKTB_WAVES; 1 = the compiler's choice: 128 VGPRs and
+// 4 waves with the two-chunk windows, whose c4 traceback span was 3.2-3.3 against 2.06 ms at 5 waves / 96 VGPRs, no
+// spills; profiles/r06/ck_wide), and its
 // waves' issue priority against the other part's forward waves on the same SIMD (SED_CKTB_PRIO, s_setprio).  At
 // priority 1 the traceback's waves issue ahead of the forward's when both are ready, so a part's traceback ends
 // sooner beside the other part's forward and the step's tracebacks-only tail shrinks from ~0.5 to ~0.13 ms: c4
 // 9.74-9.79 against 9.91-9.98 ms at 0, 3 interleaved rounds (profiles/r05/s15; 3 is no different from 1)
 #ifndef SED_CKTB_WAVES
-#define SED_CKTB_WAVES 1
+#define SED_CKTB_WAVES 5
 #endif
 #ifndef SED_CKTB_PRIO
 #define SED_CKTB_PRIO 1
+#endif
+// code words per lane of the checkpoint traceback's sweep: 12 = two-chunk windows where they pay (ck_traceback_pair), 8 =
+// one chunk per visit
+#ifndef SED_CKTB_NW
+#define SED_CKTB_NW 12
 #endif
 template <int R>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SED_CKTB_WAVES))) void sed_traceback_ck_kernel(const sed_pair_desc *__restrict__ pd, int npairs,
@@ -2968,14 +2997,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SED_CKTB_WAV
 #ifdef SED_TB_DEBUG
     if (pair != 0) return;
 #endif
-    constexpr int NSEL = CkVHold<R>::value ? Grp<R>::G : 1;
-    __shared__ uint32_t topb[132], selb[NSEL * SED_CK_SELB];
+    constexpr int NSEL = CkVHold<R>::value ? Grp<R>::G : 1, NW = SED_CKTB_NW;
+    __shared__ uint32_t topb[SED_CK_NX(NW)], selb[NSEL * SED_CK_SELB(NW)];
     if constexpr (NSEL > 1) {
-        for (int x = lane; x < NSEL * SED_CK_SELB; x += 64) selb[x] = SED_SEL_SENT;  // (entries below 64: before column 1)
+        for (int x = lane; x < NSEL * SED_CK_SELB(NW); x += 64) selb[x] = SED_SEL_SENT;  // (entries below 64: before column 1)
         __syncthreads();
     }
     const uint32_t q0 = (uint32_t)__builtin_amdgcn_readfirstlane(res[pair].len);
-    ck_traceback_pair<R, false>(d, pair, q0, lane, seqa, seqb, ck, res, ops, prm, topb, selb);
+    ck_traceback_pair<R, false, NW>(d, pair, q0, lane, seqa, seqb, ck, res, ops, prm, topb, selb);
 }
 
 // ---------------------------------------------------------------------------
@@ -3010,12 +3039,12 @@ __global__ __launch_bounds__(64) void sed_ck_codes_kernel(const sed_pair_desc *_
     if (tile >= nstripes * R * nchunks) return;
     const int c = tile % nchunks, kq = tile / nchunks, Q = kq % R, k = kq / R;
     const uint64_t codew = (uint64_t)nstripes * (uint64_t)(SG / G) * 256u;  // the pair's per-cell code words
-    __shared__ uint32_t topb[132], selb[SED_CK_SELB], wl[64 * 9], win[64 * 5];
+    __shared__ uint32_t topb[SED_CK_NX(8)], selb[SED_CK_SELB(8)], wl[64 * 9], win[64 * 5];
     const CkPairCtx px = ck_pair_ctx<R>(d, lane, seqa, seqb, tb, codew);
     uint32_t one = 1u;
     asm volatile("" : "+v"(one));
     uint32_t W[8], vinit = 0;
-    (void)ck_tile_sweep<R, false, true>(px, lane, prm, topb, selb, k, Q, c, 127, one, W, vinit);
+    (void)ck_tile_sweep<R, false, true, 8>(px, lane, prm, topb, selb, k, Q, c, 127, one, W, vinit);
     // this lane's window: 64 codes from sweep step s0 (bit 2 s0 of W[0..7])
     const int b = lane >> 2, rr = lane & 3;
     const uint32_t s0 = (uint32_t)(G - 1 + (R - 1) * b + rr);
