@@ -2754,7 +2754,9 @@ __device__ __forceinline__ uint32_t ck_tile_sweep(const CkPairCtx &px, const int
     for (int h = 0; h < NH; ++h) {
         const int x = lane + 64 * h;
         rk[h] = 0u;
-        if (64 * (h + 1) <= NX || x < NX) {
+        // (a visit reads the top row and selectors of steps <= sig_end + 1 only: the blocks past it are skipped, a
+        // uniform branch; the entry word's reads past sig_end see unused words)
+        if ((FULL || 64 * h <= sig_end + 1) && (64 * (h + 1) <= NX || x < NX)) {
             if (above) {
                 const uint32_t s = (uint32_t)min(max(s0r + x, 0), SG - 1);
                 rk[h] = ld_byte_off(rbase, ((s >> (6 - LR)) * (uint32_t)SED_CK_RW + (s & (uint32_t)(G - 1))) * 4u);
@@ -2777,7 +2779,7 @@ __device__ __forceinline__ uint32_t ck_tile_sweep(const CkPairCtx &px, const int
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
         const int x = lane + 64 * h;
-        if (64 * (h + 1) <= NX || x < NX) {
+        if ((FULL || 64 * h <= sig_end + 1) && (64 * (h + 1) <= NX || x < NX)) {
             const uint32_t v = (above && J0 - G + x >= 1) ? ck_to_tb(rk[h], prm) : SED_KB;
             topb[x] = v + 1u;
             const int col = J0 - (G - 1) + x;  // column of lane 0 at step x
