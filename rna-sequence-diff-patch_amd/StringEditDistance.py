@@ -32,6 +32,7 @@ There is no CPU fallback for the DP: without libsed.so or a HIP device the
 functions raise sedgpu.SedError.
 """
 import json
+import sys
 from collections import deque
 
 import numpy as np
@@ -232,7 +233,7 @@ class DPMatrix:
             # of this matrix's canonical path only fills in their values (tools/es_build_bench.py: ~1/4 of the build)
             ctx.submit_pair(a, b, True)
             try:
-                self._skel = _sedhost.es_skeleton(max(self.n, self.m))
+                self._skel = _skeleton(max(self.n, self.m), self.n + self.m)
             finally:
                 d, is_int, ln, ops = ctx.wait_pair()
         else:
@@ -325,6 +326,28 @@ class DPMatrix:
 
 # script calls of at least this many symbols (n + m) build their generate_es records during the device run (_run)
 _SKEL_MIN = 512
+
+# generate_es lists of those calls, kept (a reference each) until no one else holds them: the next script call's
+# device window then reuses one as its records (es_recycle: its values are overwritten) or releases it, instead of
+# the caller paying for ~13 000 dict deallocations when it drops a 4096^2 script (gui.py:386-388 clears the previous
+# call's scripts; a loop rebinds its variable).  A list the caller still holds is kept and looked at again.
+_retired = deque()
+_RETIRE_MAX = 3
+
+
+def _skeleton(count, most):
+    """Records for the next script's generate_es (at least `count`): a retired list no one else holds and with at most
+    `most` records (no surplus to drop after the run), reused, else new ones (es_skeleton).  The other retired lists
+    no one holds any more are released here, while the device computes."""
+    skel = None
+    for _ in range(len(_retired)):
+        lst = _retired.popleft()
+        if sys.getrefcount(lst) > 2:  # (this name and getrefcount's argument: anything more is the caller's)
+            _retired.append(lst)
+        elif skel is None and len(lst) <= most:
+            skel = _sedhost.es_recycle(lst, count)
+        del lst
+    return skel if skel is not None else _sedhost.es_skeleton(count)
 
 # One-deep predictor of the caller's pattern: True when the matrix of the previous wagnerFisher call
 # was asked for its script (the GUI: wagnerFisher -> create_paths -> generate_es).  The next call then
@@ -543,7 +566,11 @@ def generate_es(path, str1, str2):
             skel = dp._skel if isinstance(dp, DPMatrix) else None
             if skel is not None and ops is dp._script and str1 == dp.str1 and str2 == dp.str2:
                 dp._skel = None  # (each call returns new records: the next one builds its own)
-                return _sedhost.es_fill(skel[0], skel[1], codes, str1, str2)
+                es = _sedhost.es_fill(skel[0], skel[1], codes, str1, str2)
+                _retired.append(es)
+                while len(_retired) > _RETIRE_MAX:
+                    _retired.popleft()
+                return es
             return _sedhost.es_from_ops(codes, str1, str2)
         for op, nxt in zip(ops, path[1:]):
             es.append(_op_record(_OPNAME[op], str1, str2, nxt.i, nxt.j))

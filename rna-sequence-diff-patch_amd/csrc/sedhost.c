@@ -657,6 +657,68 @@ fail:
     return NULL;
 }
 
+/* es_recycle(records, count) -> (records, sides) | None: a previous generate_es list, which the caller has checked no
+ * one else holds, reused as the next call's skeleton: every record an exact dict held only by the list, with exactly
+ * the keys operation, source, destination in that order, each side an exact dict held only by its record with exactly
+ * character, index in that order (rev_es' records share side dicts: those lists are refused).  Records are appended up
+ * to `count`.  The values stay until es_fill overwrites them.  None when any record does not qualify. */
+static int side_reusable(PyObject *d) {
+    Py_ssize_t pos = 0;
+    PyObject *k, *v;
+    if (!PyDict_CheckExact(d) || Py_REFCNT(d) != 1 || PyDict_GET_SIZE(d) != 2) return 0;
+    if (!PyDict_Next(d, &pos, &k, &v) || k != K_CHARACTER) return 0;
+    if (!PyDict_Next(d, &pos, &k, &v) || k != K_INDEX) return 0;
+    return 1;
+}
+static PyObject *es_recycle_impl(PyObject *self, PyObject *args) {
+    PyObject *list;
+    Py_ssize_t count;
+    if (!PyArg_ParseTuple(args, "O!n", &PyList_Type, &list, &count)) return NULL;
+    const Py_ssize_t have = PyList_GET_SIZE(list), total = have > count ? have : count;
+    PyObject *sides = PyBytes_FromStringAndSize(NULL, 2 * total * (Py_ssize_t)sizeof(PyObject *));
+    if (!sides) return NULL;
+    PyObject **sp = (PyObject **)PyBytes_AS_STRING(sides);
+    for (Py_ssize_t i = 0; i < have; ++i) {
+        PyObject *rec = PyList_GET_ITEM(list, i), *k, *op, *src, *dst;
+        Py_ssize_t pos = 0;
+        if (!PyDict_CheckExact(rec) || Py_REFCNT(rec) != 1 || PyDict_GET_SIZE(rec) != 3 ||
+            !PyDict_Next(rec, &pos, &k, &op) || k != K_OPERATION || !PyDict_Next(rec, &pos, &k, &src) ||
+            k != K_SOURCE || !PyDict_Next(rec, &pos, &k, &dst) || k != K_DESTINATION || src == dst ||
+            !side_reusable(src) || !side_reusable(dst)) {
+            Py_DECREF(sides);
+            Py_RETURN_NONE;
+        }
+        sp[2 * i] = src;
+        sp[2 * i + 1] = dst;
+    }
+    for (Py_ssize_t i = have; i < total; ++i) {  /* (as es_skeleton) */
+        PyObject *src = PyDict_New(), *dst = PyDict_New(), *rec = PyDict_New();
+        if (!src || !dst || !rec || PyDict_SetItem(src, K_CHARACTER, Py_None) || PyDict_SetItem(src, K_INDEX, Py_None) ||
+            PyDict_SetItem(dst, K_CHARACTER, Py_None) || PyDict_SetItem(dst, K_INDEX, Py_None) ||
+            PyDict_SetItem(rec, K_OPERATION, Py_None) || PyDict_SetItem(rec, K_SOURCE, src) ||
+            PyDict_SetItem(rec, K_DESTINATION, dst) || PyList_Append(list, rec)) {
+            Py_XDECREF(src);
+            Py_XDECREF(dst);
+            Py_XDECREF(rec);
+            Py_DECREF(sides);
+            return NULL;
+        }
+        sp[2 * i] = src;
+        sp[2 * i + 1] = dst;
+        Py_DECREF(src);
+        Py_DECREF(dst);
+        Py_DECREF(rec);
+    }
+    return PyTuple_Pack(2, list, sides);
+}
+
+static PyObject *es_recycle(PyObject *self, PyObject *args) {
+    const int was = PyGC_Disable();
+    PyObject *r = es_recycle_impl(self, args);
+    if (was) PyGC_Enable();
+    return r;
+}
+
 static PyObject *es_skeleton(PyObject *self, PyObject *args) {
     const int was = PyGC_Disable();
     PyObject *r = es_skeleton_impl(self, args);
@@ -860,6 +922,7 @@ static PyMethodDef methods[] = {
     {"es_from_ops", es_from_ops, METH_VARARGS, "generate_es over a canonical op sequence"},
     {"es_skeleton", es_skeleton, METH_VARARGS, "generate_es records with their values still None, and their side dicts"},
     {"es_fill", es_fill, METH_VARARGS, "es_from_ops' values written into es_skeleton records"},
+    {"es_recycle", es_recycle, METH_VARARGS, "a previous generate_es list no one else holds, as an es_skeleton"},
     {"rev_es", rev_es, METH_O, "generate_rev_es"},
     {"seq_from_es", seq_from_es, METH_O, "generate_sequence_from_es"},
     {"patching", patching, METH_VARARGS, "patching(es, str1) -> (error_code, str)"},

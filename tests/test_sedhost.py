@@ -119,6 +119,43 @@ def test_es_skeleton_fill_equals_es_from_ops():
         _sedhost.es_fill(recs, sides, bytes([0]), "", "A")
 
 
+def test_es_recycle_reuses_only_unshared_records():
+    """es_recycle takes a previous generate_es list as the next skeleton only when every record and side dict is held by
+    the list alone, unmodified in shape: filled again, it equals es_from_ops of the new script (also with fewer or more
+    records than ops); a record or side held elsewhere (rev_es shares side dicts), an added key or a reordered record is
+    refused (None)."""
+    rng = random.Random(5)
+
+    def script(k):
+        s1 = "".join(rng.choice("ACGU") for _ in range(rng.randint(1, 30)))
+        s2 = "".join(rng.choice("ACGU") for _ in range(rng.randint(1, 30)))
+        ops = [2] * min(len(s1), len(s2)) + [0] * max(0, len(s2) - len(s1)) + [1] * max(0, len(s1) - len(s2))
+        rng.shuffle(ops)
+        return bytes(ops), s1, s2
+
+    for trial in range(200):
+        ops, s1, s2 = script(trial)
+        old = _sedhost.es_from_ops(*script(trial))
+        count = rng.choice([0, 1, len(ops), len(ops) + 7])
+        got = _sedhost.es_recycle(old, count)
+        assert got is not None and got[0] is old and len(old) >= count
+        assert _sedhost.es_fill(got[0], got[1], ops, s1, s2) == _sedhost.es_from_ops(ops, s1, s2)
+    ops, s1, s2 = script(0)
+    base = _sedhost.es_from_ops(ops, s1, s2)
+    held = base[len(base) // 2]
+    assert _sedhost.es_recycle(base, 0) is None  # a record held outside the list
+    del held
+    assert _sedhost.es_recycle(base, 0) is not None
+    rev = _sedhost.rev_es(base)
+    assert _sedhost.es_recycle(base, 0) is None  # side dicts shared with the reversed script
+    del rev
+    base[0]["extra"] = 1
+    assert _sedhost.es_recycle(base, 0) is None
+    del base[0]["extra"]
+    base[0]["source"] = base[0].pop("source")  # same keys, another order
+    assert _sedhost.es_recycle(base, 0) is None
+
+
 def _rand_side(rng):
     d = {}
     keys = ["character", "index"]

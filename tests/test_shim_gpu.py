@@ -231,6 +231,37 @@ def test_gui_call_builds_es_records_during_the_run(SED):
     assert got[:3] == ctx.run_pair(a, b, True)[:3]
 
 
+def test_gui_calls_recycle_released_scripts(SED):
+    """Repeated GUI calls (gui.py:385-391 drops the previous call's scripts, edit_scripts.clear()) reuse a released
+    generate_es list as the next call's records (StringEditDistance._skeleton, _sedhost.es_recycle: its records still
+    carry the old values until generate_es fills them): every call's records equal es_from_ops', and a list the caller
+    still holds (one with its reversal too) is never reused nor changed."""
+    import _sedhost
+    import synth
+
+    def want(p0, s1, s2):
+        return _sedhost.es_from_ops(np.asarray(p0.ops, np.uint8).tobytes(), s1, s2)
+
+    held, reused = [], []
+    shapes = [(700, 650), (640, 700), (600, 610), (700, 700), (650, 600), (4096, 4096), (4000, 4090), (700, 690),
+              (690, 700), (700, 700)]
+    for k, (n, m) in enumerate(shapes):
+        s1, s2 = synth.pair_strings(3000 + k, n, m)
+        SED._script_hint = True
+        dp = SED.wagnerFisher(s1, s2, True)
+        reused.append(dp._skel is not None and dp._skel[0][0]["operation"] is not None)  # (new records hold None)
+        p0 = SED.create_paths(dp)[0]
+        es = SED.generate_es(p0, s1, s2)
+        assert es == want(p0, s1, s2)
+        if k in (1, 4):  # kept by the caller, with a deep copy of its values (and for k = 4 its reversal)
+            copy = [dict(r, source=dict(r["source"]), destination=dict(r["destination"])) for r in es]
+            held.append((es, copy, SED.generate_rev_es(es) if k == 4 else None))
+        del es, p0, dp
+    assert sum(reused) >= 5, reused
+    for es, copy, _ in held:
+        assert es == copy
+
+
 def _ref_search_collection(query, vector_type, collection, method, return_dict=None, callback=None):
     """IRMethods.search_collection (IRMethods.py:443-477) for method == wf_score: one wagnerFisher per
     document through the drop-in module, exactly as the unchanged caller does."""
