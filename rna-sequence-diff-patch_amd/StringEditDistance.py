@@ -333,6 +333,7 @@ _SKEL_MIN = 512
 # call's scripts; a loop rebinds its variable).  A list the caller still holds is kept and looked at again.
 _retired = deque()
 _RETIRE_MAX = 3
+_RETIRE_RECORDS = 1 << 16  # (longer scripts are not kept: at most ~3 x 20 MB of dicts held past their use)
 
 
 def _skeleton(count, most):
@@ -567,9 +568,10 @@ def generate_es(path, str1, str2):
             if skel is not None and ops is dp._script and str1 == dp.str1 and str2 == dp.str2:
                 dp._skel = None  # (each call returns new records: the next one builds its own)
                 es = _sedhost.es_fill(skel[0], skel[1], codes, str1, str2)
-                _retired.append(es)
-                while len(_retired) > _RETIRE_MAX:
-                    _retired.popleft()
+                if len(es) <= _RETIRE_RECORDS:
+                    _retired.append(es)
+                    while len(_retired) > _RETIRE_MAX:
+                        _retired.popleft()
                 return es
             return _sedhost.es_from_ops(codes, str1, str2)
         for op, nxt in zip(ops, path[1:]):
