@@ -271,7 +271,7 @@ int64_t gcd64(int64_t a, int64_t b) {
 // kap: kappa[a][b] (>= 1); maxmin: the largest min(n, m) of the batch's wave pairs.
 // Ladder mode (lad_amin > 0, lad_beta): the factorisation of A*K + lad_beta*J for the per-cell-code kernels'
 // ladder keys with A >= lad_amin and A < 2^16 (dot_ladder below); no ordering bound or decode constants.
-DotKeys dot_keys(const int64_t kap[4][4], int64_t maxmin, int64_t lad_amin = 0, int64_t lad_beta = 0) {
+DotKeys dot_keys_search(const int64_t kap[4][4], int64_t maxmin, int64_t lad_amin, int64_t lad_beta) {
     const bool lad = lad_amin > 0;
     const int64_t beta = lad ? lad_beta : 1;
     DotKeys dk;
@@ -421,6 +421,31 @@ DotKeys dot_keys(const int64_t kap[4][4], int64_t maxmin, int64_t lad_amin = 0, 
         return dk;
     }
     return dk;
+}
+// dot_keys_search walks the factorisation's scale a down from ~16 000 / |num| with byte searches at every step (~75 us
+// for user_costs on the build host): per-call batches (the GUI's script calls) would pay it before every launch, so
+// the last few results are kept per thread, keyed by the whole input.
+DotKeys dot_keys(const int64_t kap[4][4], int64_t maxmin, int64_t lad_amin = 0, int64_t lad_beta = 0) {
+    struct Memo {
+        int64_t kap[4][4], maxmin, amin, beta;
+        DotKeys dk;
+        bool used;
+    };
+    static thread_local Memo memo[4] = {};
+    static thread_local int next = 0;
+    for (Memo &e : memo)
+        if (e.used && e.maxmin == maxmin && e.amin == lad_amin && e.beta == lad_beta &&
+            std::memcmp(e.kap, kap, sizeof(e.kap)) == 0)
+            return e.dk;
+    Memo &e = memo[next];
+    next = (next + 1) & 3;
+    std::memcpy(e.kap, kap, sizeof(e.kap));
+    e.maxmin = maxmin;
+    e.amin = lad_amin;
+    e.beta = lad_beta;
+    e.dk = dot_keys_search(kap, maxmin, lad_amin, lad_beta);
+    e.used = true;
+    return e.dk;
 }
 
 int next_pow2(int x) {
@@ -1022,11 +1047,24 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
     if (packed) {
         ha.assign(aw + pad_words, 0);
         hb.assign(bw + pad_words, 0);
+        // 16 codes per word, each word built in a register (an OR into memory per code was ~1 ns per symbol)
+        auto pack2 = [](const uint8_t *src, int len, uint32_t *dst) {
+            const int full = len >> 4;
+            for (int w = 0; w < full; ++w) {
+                const uint8_t *q = src + 16 * w;
+                uint32_t v = 0;
+                for (int k = 0; k < 16; ++k) v |= (uint32_t)q[k] << (2 * k);
+                dst[w] = v;
+            }
+            if (len & 15) {
+                uint32_t v = 0;
+                for (int k = 0; k < (len & 15); ++k) v |= (uint32_t)src[16 * full + k] << (2 * k);
+                dst[full] = v;
+            }
+        };
         for (int p = 0; p < npairs; ++p) {
-            const uint8_t *pa = codes_a + off_a[p], *pb = codes_b + off_b[p];
-            uint32_t *qa = ha.data() + b->pd[p].a_off, *qb = hb.data() + b->pd[p].b_off;
-            for (int i = 0; i < len_a[p]; ++i) qa[i >> 4] |= (uint32_t)pa[i] << (2 * (i & 15));
-            for (int j = 0; j < len_b[p]; ++j) qb[j >> 4] |= (uint32_t)pb[j] << (2 * (j & 15));
+            pack2(codes_a + off_a[p], len_a[p], ha.data() + b->pd[p].a_off);
+            pack2(codes_b + off_b[p], len_b[p], hb.data() + b->pd[p].b_off);
         }
     } else {
         ha8.assign(aw + 64, 0);
