@@ -2145,12 +2145,13 @@ template <int R> struct CodeCursor {  // per-lane reader of one pair's per-cell 
 #ifndef SED_TBMAP_RUN
 #define SED_TBMAP_RUN 96
 #endif
-// Band-map walks stop (entry unknown, left to the emit kernel's fallback walk) after 96 + 64 ceil(m / n) steps: the
+// Band-map walks stop (entry unknown, left to the emit kernel's fallback walk) after 64 + 64 ceil(m / n) steps: the
 // canonical path crosses a 64-row band in 64 steps plus its inserts, while a wave's time is its longest lane, and the
 // lanes far from the path run left for 200-340 steps (config 2's pair: median walk 65 steps, 99th percentile 283,
-// tools/tbmap_walks.py).  0: no step limit (A/B)
+// tools/tbmap_walks.py).  SED_TBMAP_CAP: the base (96: map 36.3 against 33.9 us at R = 4, 32.7 against 26.8 at R = 2,
+// profiles/r06/tbmap_cap/step23); 0: no step limit (A/B)
 #ifndef SED_TBMAP_CAP
-#define SED_TBMAP_CAP 1
+#define SED_TBMAP_CAP 64
 #endif
 template <int R>
 __global__ __launch_bounds__(256) void sed_tb_stripemap_kernel(const sed_pair_desc *__restrict__ pd,
@@ -2303,7 +2304,7 @@ __global__ __launch_bounds__(256) void sed_tb_bandmap_kernel(const sed_pair_desc
     if (!live) return;
     const int top = 64 * g;  // row top belongs to band g - 1
     uint32_t cnt = 0, run = 0;  // run: consecutive inserts
-    const uint32_t cap = SED_TBMAP_CAP ? 96u + 64u * (uint32_t)((m + n - 1) / n) : 0xFFFFFFFFu;
+    const uint32_t cap = SED_TBMAP_CAP ? (uint32_t)SED_TBMAP_CAP + 64u * (uint32_t)((m + n - 1) / n) : 0xFFFFFFFFu;
     for (;;) {  // the stripe map kernel's loop on the band's staged lanes
         const int rr = i - 1, t = (rr >> LR) & 63, r = rr & (R - 1);
         const int s = j - 1 + t;
