@@ -604,6 +604,36 @@ def test_split_checkpoint_codes_route(gpu, tables, user, dot):
 
 
 @pytest.mark.parametrize("user", [False, True])
+def test_split_band_map_unknown_entries(gpu, tables, user):
+    """Stripe-parallel walks whose band maps leave entries unknown (sed_tb_bandmap_kernel: a walk past 64 + 64 ceil(m/n)
+    steps, a run of more than 96 inserts, or past the staged columns), so the banded emit kernel walks them itself:
+    pairs with a block of 300-700 symbols inserted or deleted in the middle, m = 3n and n = 3m, against the oracle,
+    with padding checked (the ops buffer compared whole)."""
+    rng = np.random.default_rng(5600 + user)
+    A, B = [], []
+    for n, ins, at in ((2048, 400, 1000), (1500, 700, 200), (3000, 300, 2600)):
+        a = rng.integers(0, 4, size=n).astype(np.uint8)
+        mid = rng.integers(0, 4, size=ins).astype(np.uint8)
+        b = np.concatenate([a[:at], mid, a[at:]])
+        mut = rng.random(len(b)) < 0.05  # point mutations around the block
+        b[mut] = rng.integers(0, 4, size=int(mut.sum())).astype(np.uint8)
+        A += [a, b]
+        B += [b, a]  # the insert block as inserts, then as deletes
+    for n, m in ((700, 2100), (2100, 700), (1024, 4000)):
+        A.append(rng.integers(0, 4, size=n).astype(np.uint8))
+        B.append(rng.integers(0, 4, size=m).astype(np.uint8))
+    plan = _plan(tables[user])
+    gpu.set_costs(plan)
+    packed = sedgpu.PackedPairs(A, B)
+    b, (d, ii, ln, ops) = _batch_run(gpu, packed, True, runs=2)
+    try:
+        assert b.rows_per_lane == 4 and b.traceback_mode == 4  # the SPLIT checkpoint route with the stripe-parallel walk
+    finally:
+        b.close()
+    _check_all(plan, packed, d, ii, ln, ops, script=True)
+
+
+@pytest.mark.parametrize("user", [False, True])
 def test_split_checkpoint_window_walk(gpu, tables, user):
     """SPLIT script batches of 65..256 pairs: the SPLIT checkpoint forward and the tile-parallel code recompute, then
     the window walk (sed_traceback_window_kernel) over the plain op codes (tb_ladder off), since the stripe-parallel
