@@ -144,12 +144,17 @@ def test_module_fuzz_vs_pyref():
     t_end = time.monotonic() + float(os.environ.get("SED_FUZZ_MODULE_SECONDS", "8"))
     t_note = time.monotonic() + 20.0
     runs = 0
+    kept = []  # long scripts the 'caller' holds (some with their reversal): never reused, never changed
     while time.monotonic() < t_end or runs < 20:
         if time.monotonic() > t_note:  # (progress for long budgets)
             print("module fuzz: %d pairs" % runs, flush=True)
             t_note += 20.0
         user = bool(rng.random() < 0.5)
         al = list("ACGU") if rng.random() < 0.5 else iupac
+        if rng.random() < 0.05:  # a long pair: the script-list build / reuse path (n + m >= 512), vs the C oracle
+            _long_module_case(SED, rng, al, tables[user], user, kept)
+            runs += 1
+            continue
         n, m = int(rng.integers(0, 48)), int(rng.integers(0, 48))
         s1 = "".join(rng.choice(al, size=n))
         s2 = "".join(c if rng.random() > 0.2 else rng.choice(al) for c in s1)[:m] if rng.random() < 0.5 else \
@@ -168,4 +173,35 @@ def test_module_fuzz_vs_pyref():
             assert SED.patching(SED.generate_rev_es(got_es), s2) == (0, s1), (s1, s2, user)
             assert SED.patching(got_es, s1) == (0, s2), (s1, s2, user)
         runs += 1
+    for es, copy, _ in kept:
+        assert es == copy
     print("module fuzz: %d pairs" % runs)
+
+
+def _long_module_case(SED, rng, al, table, user, kept):
+    """One GUI-style call on a pair of 260..900 symbols a side (the records are built during the device run and a
+    released previous list may be reused, StringEditDistance._skeleton): the records must equal es_from_ops of the C
+    oracle's script; the result is sometimes kept (with a deep copy, sometimes with its reversal) and kept ones are
+    sometimes released, so the reuse sees held, shared and released lists."""
+    import _sedhost
+    import oracle
+    import sedcost
+    n, m = (int(x) for x in rng.integers(260, 900, size=2))
+    s1 = "".join(rng.choice(al, size=n))
+    s2 = "".join(c if rng.random() > 0.15 else rng.choice(al) for c in s1)[:m] if rng.random() < 0.5 else \
+        "".join(rng.choice(al, size=m))
+    plan = sedcost.pair_plan(table, s1, s2)
+    want = oracle.pair(oracle.Costs.from_plan(plan), np.frombuffer(plan.encode_bytes(s1), np.uint8),
+                       np.frombuffer(plan.encode_bytes(s2), np.uint8))
+    SED._script_hint = True
+    dp = SED.wagnerFisher(s1, s2, user)
+    got = dp[len(dp) - 1][len(dp[0]) - 1].value
+    assert got == want["dist"], (n, m, user)
+    es = SED.generate_es(SED.create_paths(dp)[0], s1, s2)
+    assert es == _sedhost.es_from_ops(want["ops"].tobytes(), s1, s2), (n, m, user)
+    if rng.random() < 0.3:
+        copy = [dict(r, source=dict(r["source"]), destination=dict(r["destination"])) for r in es]
+        kept.append((es, copy, SED.generate_rev_es(es) if rng.random() < 0.5 else None))
+    if kept and rng.random() < 0.3:
+        es0, copy0, _ = kept.pop(int(rng.integers(0, len(kept))))
+        assert es0 == copy0
