@@ -2980,7 +2980,8 @@ __device__ __forceinline__ void ck_traceback_pair(const sed_pair_desc &d, const 
 // waves' issue priority against the other part's forward waves on the same SIMD (SED_CKTB_PRIO, s_setprio).  At
 // priority 1 the traceback's waves issue ahead of the forward's when both are ready, so a part's traceback ends
 // sooner beside the other part's forward and the step's tracebacks-only tail shrinks from ~0.5 to ~0.13 ms: c4
-// 9.74-9.79 against 9.91-9.98 ms at 0, 3 interleaved rounds (profiles/r05/s15; 3 is no different from 1)
+// 9.74-9.79 against 9.91-9.98 ms at 0, 3 interleaved rounds (profiles/r05/s15; 3 is no different from 1).  With the
+// two-chunk windows: 0 9.70-9.74 against 9.55-9.60 ms; 2 and 3 within noise of 1 over 4 rounds (profiles/r06/ckprio)
 #ifndef SED_CKTB_WAVES
 #define SED_CKTB_WAVES 5
 #endif
