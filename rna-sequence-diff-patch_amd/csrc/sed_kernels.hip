@@ -2823,6 +2823,14 @@ __device__ __forceinline__ uint32_t ck_tile_sweep(const CkPairCtx &px, const int
     vinit = V;
 #endif
     uint32_t tprev = dpp_shr1_add(topb[G - 1], V, one);  // diagonal of step G-1 (+1)
+    // the top row's reads through one opaque base register and immediate offsets (else every constant address became a
+    // VGPR of its own: 28 preloaded at the kernel's start, one more v_mov per two steps of an entry word)
+    const uint32_t *topr = topb;
+    {
+        uint32_t z = 0u;
+        asm volatile("" : "+v"(z));
+        topr += z;
+    }
     const uint32_t *selp = selb + (VHOLD ? band * SELB : 0) + 64 - lane;  // lane r's selector at step sigma
     const int w_end = FULL ? NW - 1 : sig_end >> 4;  // FULL: every word, whole
     auto step = [&](const int sig, uint32_t &wv, const uint32_t topin, const uint32_t selv) {
@@ -2854,7 +2862,7 @@ __device__ __forceinline__ uint32_t ck_tile_sweep(const CkPairCtx &px, const int
             uint32_t tw[16], sw[16];
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
-                tw[u] = topb[16 * w + u + 1];
+                tw[u] = topr[16 * w + u + 1];
                 sw[u] = selp[16 * w + u];
             }
 #pragma unroll
@@ -2865,7 +2873,7 @@ __device__ __forceinline__ uint32_t ck_tile_sweep(const CkPairCtx &px, const int
             W[w] >>= 2u * (15u - ((uint32_t)sig_end & 15u));  // step u's code to bits 2u, 2u+1
         } else {
 #pragma unroll
-            for (int u = 0; u < 16; ++u) step(16 * w + u, W[w], topb[16 * w + u + 1], selp[16 * w + u]);
+            for (int u = 0; u < 16; ++u) step(16 * w + u, W[w], topr[16 * w + u + 1], selp[16 * w + u]);
         }
         if (w < 4) W[w] |= px.hm[w];
     });
@@ -3088,6 +3096,7 @@ __global__ __launch_bounds__(64) void sed_ck_codes_kernel(const sed_pair_desc *_
     *reinterpret_cast<uint4 *>(gp) = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+#ifndef SED_CKTB_TU  // (sed_cktb.hip compiles this file for the checkpoint traceback's launcher alone)
 // ---------------------------------------------------------------------------
 // Self-test of the cross-lane primitives the kernels rely on.
 // ---------------------------------------------------------------------------
@@ -3303,18 +3312,6 @@ hipError_t sed_launch_ck_codes(const sed_launch &L, int max_tiles, const sed_i32
     return hipGetLastError();
 }
 
-hipError_t sed_launch_traceback_ck(const sed_launch &L, uint32_t *ops, const sed_i32_params &prm) {
-    const dim3 grid(L.npairs), block(64);
-    const uint32_t *a = (const uint32_t *)L.seqa, *b = (const uint32_t *)L.seqb;
-    switch (L.R) {
-    case 4: SED_LAUNCH(sed_traceback_ck_kernel<4>, grid, block, 0, L, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
-    case 8: SED_LAUNCH(sed_traceback_ck_kernel<8>, grid, block, 0, L, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
-    case 16: SED_LAUNCH(sed_traceback_ck_kernel<16>, grid, block, 0, L, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
 hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops) {
     // up to one pair per CU: a wave-uniform walk per pair over windows of blocks; beyond: one lane per pair
     const bool uni = L.npairs <= 256;
@@ -3375,3 +3372,18 @@ hipError_t sed_launch_selftest(uint32_t *d_out, hipStream_t stream) {
     hipLaunchKernelGGL(sed_selftest_kernel, dim3(1), dim3(64), 0, stream, d_out);
     return hipGetLastError();
 }
+#else
+// the checkpoint traceback, in its own translation unit (sed_cktb.hip: built with private arrays kept out of vector
+// registers, so a visit's code words stay separate registers)
+hipError_t sed_launch_traceback_ck(const sed_launch &L, uint32_t *ops, const sed_i32_params &prm) {
+    const dim3 grid(L.npairs), block(64);
+    const uint32_t *a = (const uint32_t *)L.seqa, *b = (const uint32_t *)L.seqb;
+    switch (L.R) {
+    case 4: SED_LAUNCH(sed_traceback_ck_kernel<4>, grid, block, 0, L, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
+    case 8: SED_LAUNCH(sed_traceback_ck_kernel<8>, grid, block, 0, L, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
+    case 16: SED_LAUNCH(sed_traceback_ck_kernel<16>, grid, block, 0, L, L.pd, L.npairs, a, b, L.tb, L.res, ops, prm); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+#endif

@@ -4,5 +4,5 @@
 set -e
 cd "$(dirname "$0")/../../rna-sequence-diff-patch_amd/csrc"
 for u in 4 8; do
-  make -s OBJ=sed_kernels_u$u.o OUT=../../tools/ab_libs/libsed_u$u.so EXTRA="-DSED_CK_GUNROLL=$u" ../../tools/ab_libs/libsed_u$u.so
+  make -s OBJ=sed_kernels_u$u.o CKTB_OBJ=sed_cktb_u$u.o OUT=../../tools/ab_libs/libsed_u$u.so EXTRA="-DSED_CK_GUNROLL=$u" ../../tools/ab_libs/libsed_u$u.so
 done

@@ -4,5 +4,5 @@
 # priority 1 (iupac, timing)
 set -e
 cd "$(dirname "$0")/../../rna-sequence-diff-patch_amd/csrc"
-make -s OBJ=sed_kernels_sp2.o OUT=../../tools/ab_libs/libsed_sp2.so EXTRA="-DSED_SPLIT_PRIO=2" ../../tools/ab_libs/libsed_sp2.so
-make -s OBJ=sed_kernels_fp1.o OUT=../../tools/ab_libs/libsed_fp1.so EXTRA="-DSED_F64_PRIO=1" ../../tools/ab_libs/libsed_fp1.so
+make -s OBJ=sed_kernels_sp2.o CKTB_OBJ=sed_cktb_sp2.o OUT=../../tools/ab_libs/libsed_sp2.so EXTRA="-DSED_SPLIT_PRIO=2" ../../tools/ab_libs/libsed_sp2.so
+make -s OBJ=sed_kernels_fp1.o CKTB_OBJ=sed_cktb_fp1.o OUT=../../tools/ab_libs/libsed_fp1.so EXTRA="-DSED_F64_PRIO=1" ../../tools/ab_libs/libsed_fp1.so

@@ -4,5 +4,5 @@
 set -e
 cd "$(dirname "$0")/../../rna-sequence-diff-patch_amd/csrc"
 for w in 6 8; do
-  make -s OBJ=sed_kernels_w$w.o OUT=../../tools/ab_libs/libsed_w$w.so EXTRA="-DSED_CKTB_WAVES=$w" ../../tools/ab_libs/libsed_w$w.so
+  make -s OBJ=sed_kernels_w$w.o CKTB_OBJ=sed_cktb_w$w.o OUT=../../tools/ab_libs/libsed_w$w.so EXTRA="-DSED_CKTB_WAVES=$w" ../../tools/ab_libs/libsed_w$w.so
 done
