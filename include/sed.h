@@ -82,7 +82,7 @@ enum {
                                    cap (tests: several counter-fetched pairs per wave) */
 #define SED_OPT_DOT 10          /* checkpoint batches of the stripe kernel and CHAIN batches: 0 auto (dot keys when
                                    the cost table's update addends factor over signed bytes and the pairs fit the
-                                   bound), 2 never */
+                                   bound), 2 never, 3 (tests) CHAIN ladder dot keys on the 3-bit ladder only */
 #define SED_OPT_BITPAR 11       /* distance-only batches under unit costs (insert = delete = 1, every mismatch 1): lane
                                    pairs (m <= 32) run one per lane bit-parallel; in fp64 batches (e.g. costs.json with N)
                                    the lane pairs whose symbols all have unit costs among themselves: 0 auto (on),
@@ -175,12 +175,15 @@ int sed_batch_segment_pairs(const sed_batch *b);      /* fp64 wave pairs run in 
 int sed_batch_split_tasks(const sed_batch *b);        /* SPLIT: workgroups (pair, stripe) per run, 0 = not SPLIT */
 /* The byte factorisation behind SED_OPT_DOT, without a device (tests): for the 4 x 4 table sub (a -> b, row-major)
  * and insert/delete costs, the dot keys for pairs with min(n, m) <= maxmin (ladder_maxsum = 0) or the ladder dot
- * keys for n + m <= ladder_maxsum.  out[0..3] = row vectors, out[4..7] = column vectors (4 signed bytes each),
- * out[8] = decode shift / ladder sentinel byte, out[9] = decode multiplier.  Returns A (> 0), 0 when the table has
- * no such factorisation, or SED_E_ARG. */
+ * keys for n + m <= ladder_maxsum (the wide ladder's, L unit 16, for min(n, m) <= maxmin (or ladder_maxsum when
+ * maxmin is 0) where it exists, else the 3-bit ladder's, unit 8).
+ * out[0..3] = row vectors, out[4..7] = column vectors (4 signed bytes each), out[8] = decode shift / ladder sentinel
+ * byte, out[9] = decode multiplier / ladder L unit.  Returns A (> 0), 0 when the table has no such factorisation,
+ * or SED_E_ARG. */
 int sed_dot_factor(const double *sub, double ins, double del, int maxmin, int ladder_maxsum, uint32_t *out);
 int sed_batch_dot_keys(const sed_batch *b);           /* bit 0: the checkpoint forward kernel runs dot keys, bit 1: the
-                                                         CHAIN kernel runs ladder dot keys (SED_OPT_DOT) */
+                                                         CHAIN kernel runs ladder dot keys (SED_OPT_DOT), bit 2: over
+                                                         the wide ladder (L unit 16) */
 int sed_batch_traceback_mode(const sed_batch *b);     /* 0 no script, 1 per-cell codes, 2 checkpoints (SED_OPT_TB),
                                                          3 per-cell codes walked stripe-parallel (<= 64 pairs, R = 4),
                                                          4 SPLIT checkpoints recomputed into per-cell codes

@@ -91,8 +91,9 @@ struct sed_i32_params {
     uint32_t dot;  // 1: the CK forward kernel runs dot keys, the CK traceback converts them
     uint32_t dotA, dotkmax, dotM, dotS;
     uint32_t dotrow[4], dotcol[4];
-    // Ladder dot keys (CHAIN kernel with the L field): V = D*ladA + 8L over the ladder, the update addend of a d = -1
-    // row -(ladA*kappa + 7) = dot4(ladrow[a], ladcol[b]) (sed_kernels.hip: i32_step LDOT)
+    // Ladder dot keys (CHAIN kernel with the L field): V = D*ladA + 8L over the ladder (lad = 1) or D*ladA + 16L over
+    // the wide ladder (lad = 2), the update addend of a d = -1 row -(ladA*kappa + 7) (+ 15) = dot4(ladrow[a],
+    // ladcol[b]) (sed_kernels.hip: i32_step LDOT)
     uint32_t lad, ladA, ladsent;
     uint32_t ladrow[4], ladcol[4];
 };
@@ -127,6 +128,7 @@ struct sed_launch {
     int R;
     hipStream_t stream;
     bool tb_ladder;     // traceback codes of the integer kernels carry the row's ladder rung (sed_kernels.hip)
+    bool tb_wide;       // ... of the wide ladder (ladder dot keys, LadderW: the CHAIN kernel's LDOT batches)
     bool ck;            // integer R = 16 wave kernel: tb holds checkpoints, the traceback recomputes tiles
     // timing events carried by the launches themselves (hipExtLaunchKernelGGL: timestamps on the dispatch
     // packet, no marker packet between kernels): the launcher's first kernel records ev0 at its start, its last

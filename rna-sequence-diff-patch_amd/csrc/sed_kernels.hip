@@ -224,6 +224,15 @@ template <int R> struct Ladder {
     static constexpr uint64_t pat = P == 16 ? 0x1234501230123450ull : (P == 8 ? 0x10123450ull : 0x1230ull);
     static constexpr int rung(int i) { return (int)((pat >> (4 * (i & (P - 1)))) & 0xF); }
 };
+// The wide ladder of the ladder dot keys (LDOT = 2, the CHAIN kernel): rung + op in the low 4 bits (V = D*A + 16L + op,
+// the host keeps 16 min(n, m) + 15 < A and A a multiple of 16), rungs up to 13, so the rung runs down through a whole period
+// with one jump (P = 8: rows 1..7 on rungs 7..1; P = 16: 13..0 and two jumps): 1 jump row in 8 instead of 2, each a
+// delete add and an update add fewer.  Same P, so the tracebacks read it through their runtime pattern alone.
+template <int R> struct LadderW {
+    static constexpr int P = R >= 16 ? 16 : R;
+    static constexpr uint64_t pat = P == 16 ? 0x10123456789ABCD0ull : (P == 8 ? 0x12345670ull : 0x1230ull);
+    static constexpr int rung(int i) { return (int)((pat >> (4 * (i & (P - 1)))) & 0xF); }
+};
 
 // One column step of a lane's R rows.  tv = {top, sel} of this step's column
 // for lane 0 (the stripe's top row and str2 symbol): every lane reads the same
@@ -234,7 +243,7 @@ template <int R> struct Ladder {
 // TOPC: lane 0's top is the row-0 constant, which its top_prev already holds (single-stripe pairs: the CHAIN
 // kernel), so the DPP move writes over top_prev in place instead of over a copy of tv.x.
 template <int R, bool TB, bool LEN, bool COLLECT = true, bool SELL = false, bool TOPC = false, bool DOT = false,
-          bool LDOT = false>
+          int LDOT = 0>
 __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                          uint32_t &bottom, uint32_t &selv, const uint2 tv, uint32_t &outc,
                                          uint32_t (&W)[4], const int u) {
@@ -245,12 +254,14 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
     // row 0's update candidate from top_prev, before the DPP move overwrites top_prev in place (TOPC): the
     // empty asm makes the move's `old` depend on it, so top_prev needs no copy
     if constexpr (LEN && LDOT) {
-        // ladder keys with the update addend as one v_dot4 (ladder dot keys, sed_runtime.cpp: dot_ladder): the
-        // addend of a row whose rung steps down by one (d = -1, 13 of 16 rows) is -(A*kappa + 7) = the dot of the
-        // row's and the column's byte vectors (column vectors negated by the host); a row with another step adds
-        // d + 1 to it, which is where the perm took its inline constant d - 6.  Candidates run 4 rows ahead of the
-        // min chain (dot_add).  Per cell: v_dot4, v_min3, v_and_or, v_alignbit = 4 VALU (5 with the perm).
-        using Lad = Ladder<R>;
+        // ladder keys with the update addend as one v_dot4 (ladder dot keys, sed_runtime.cpp): the addend of a row
+        // whose rung steps down by one (d = -1) is -(A*kappa + 7) over the 3-bit ladder (LDOT = 1: V = D*A + 8L) or
+        // -(A*kappa + 15) over the wide one (LDOT = 2: V = D*A + 16L, LadderW) = the dot of the row's and the column's
+        // byte vectors (column vectors negated by the host); a row with another step adds d + 1 to it, which is where
+        // the perm took its inline constant d - 6.  Candidates run 4 rows ahead of the min chain (dot_add).  Per cell:
+        // v_dot4, v_min3, v_and_or, v_alignbit = 4 VALU (5 with the perm), plus two adds on a jump row.
+        using Lad = std::conditional_t<LDOT == 2, LadderW<R>, Ladder<R>>;
+        constexpr uint32_t LOW = LDOT == 2 ? 15u : 7u;  // the rung + op field
         constexpr int AH = R < 4 ? R : 4;
         uint32_t cand[R];
         cand[0] = dot_add(cv[0], selv, top_prev);
@@ -269,7 +280,7 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
                 const int k = u * R + r;
                 W[k >> 4] = __builtin_amdgcn_alignbit(mm, W[k >> 4], 2);
             }
-            up = (mm & ~7u) | (uint32_t)c;
+            up = (mm & ~LOW) | (uint32_t)c;
             V[r] = up;
         }
         top_prev = topv;
@@ -332,11 +343,12 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
 
 // Column-0 state of rows row0+1 .. row0+R (row0 = multiple of P) and of row0, the diagonal of the
 // first column.
-template <int R, bool LEN, bool DOT = false>
+template <int R, bool LEN, bool DOT = false, bool WIDE = false>
 __device__ __forceinline__ void i32_reset(uint32_t (&V)[R], uint32_t &top_prev) {
     top_prev = LEN ? SED_KB3 : DOT ? SED_KB_DOT : SED_KB;
 #pragma unroll
-    for (int r = 0; r < R; ++r) V[r] = LEN ? SED_KB3 + (uint32_t)Ladder<R>::rung(r + 1) : DOT ? SED_KB_DOT : SED_KB;
+    for (int r = 0; r < R; ++r)
+        V[r] = LEN ? SED_KB3 + (uint32_t)(WIDE ? LadderW<R>::rung(r + 1) : Ladder<R>::rung(r + 1)) : DOT ? SED_KB_DOT : SED_KB;
 }
 // row 0 (D = j*insert, L = j) in offset keys
 template <bool LEN, bool DOT = false> __device__ __forceinline__ uint32_t i32_row0() {
@@ -351,13 +363,18 @@ __device__ __forceinline__ uint2 dot_split(uint32_t w, const sed_i32_params &prm
     const uint32_t X = __umulhi(k, prm.dotM) >> (prm.dotS - 32u);  // dotM carries kmax (one v_mul_hi, full-rate rest)
     return make_uint2(X, k - __umul24(prm.dotA, X));
 }
-template <int R, bool LEN, bool WANT_L = false, bool DOT = false, bool LDOT = false>
+template <int R, bool LEN, bool WANT_L = false, bool DOT = false, int LDOT = 0>
 __device__ __forceinline__ int2 i32_decode(uint32_t w, int n, int m, const sed_i32_params &prm) {
-    if constexpr (LEN && LDOT) {  // V = D*A + 8L (the host keeps 8 (n + m) + 7 < A): one division per pair
-        const uint32_t v = w - SED_KB3 - (uint32_t)Ladder<R>::rung(n) + (uint32_t)n * (prm.del * prm.ladA + 8u) +
-                           (uint32_t)m * (prm.ins * prm.ladA + 8u);
-        const uint32_t D = v / prm.ladA;
-        return make_int2((int)D, (int)((v - D * prm.ladA) >> 3));
+    if constexpr (LEN && LDOT) {  // V = D*A + uL: one division per pair
+        // u = 8: the host keeps 8 (n + m) + 7 < A; u = 16 (the wide ladder): 16 min(n, m) + 15 < A, and L is read inside
+        // its window [max(n, m), n + m] (the candidates of a cell differ in L by at most min(n, m), so that bound keeps
+        // their order)
+        constexpr uint32_t U = LDOT == 2 ? 16u : 8u;
+        const uint32_t rg = (uint32_t)(LDOT == 2 ? LadderW<R>::rung(n) : Ladder<R>::rung(n));
+        const uint32_t v = w - SED_KB3 - rg + (uint32_t)n * (prm.del * prm.ladA + U) + (uint32_t)m * (prm.ins * prm.ladA + U);
+        const uint32_t lo = LDOT == 2 ? U * (uint32_t)max(n, m) : 0u;
+        const uint32_t D = (v - lo) / prm.ladA;
+        return make_int2((int)D, (int)((v - D * prm.ladA) / U));
     } else if constexpr (DOT) {  // D = n*delete + m*insert - X, L = n + m - U
         const uint2 xu = dot_split(w, prm);
         return make_int2((int)((uint32_t)n * prm.del + (uint32_t)m * prm.ins - xu.x), n + m - (int)xu.y);
@@ -1010,7 +1027,7 @@ __device__ __forceinline__ chain_pair_state chain_load(const sed_pair_desc *__re
 // Lane 0's top value is row 0 (single-stripe pairs); every lane reads its str2 selector from the wave's
 // selector ring by global column s - t (lsel: this lane's column at the group's first step), which always
 // belongs to the pair the lane is working on: lane t is on the pair starting at T exactly when s - t >= T.
-template <int R, bool TB, bool LEN, bool SW, bool GEN, bool CK, bool LDOT = false>
+template <int R, bool TB, bool LEN, bool SW, bool GEN, bool CK, int LDOT = 0>
 __device__ __forceinline__ void i32_chain_group(uint32_t (&V)[R], uint32_t (&cv)[R], const uint32_t (&cvn)[R],
                                                 const uint32_t (&Vb)[R], const uint32_t tpb, uint32_t &top_prev,
                                                 uint32_t &bottom, uint32_t &selv, const uint32_t *__restrict__ lsel,
@@ -1047,7 +1064,7 @@ __device__ __forceinline__ void i32_chain_group(uint32_t (&V)[R], uint32_t (&cv)
     }
 }
 
-template <int R, bool TB, bool LEN, bool CK, bool LDOT = false>
+template <int R, bool TB, bool LEN, bool CK, int LDOT = 0>
 __device__ __forceinline__ void chain_store_result(sed_result *__restrict__ res, int pair, uint32_t cap, int n,
                                                    int m, int seq, const sed_i32_params &prm) {
     const int2 dl = i32_decode<R, LEN, CK, false, LDOT>(cap, n, m, prm);
@@ -1067,7 +1084,7 @@ template <int R> struct ChainWaves { static constexpr int value = R >= 16 ? 4 : 
 // CK: distance keys, and checkpoints instead of codes (the stripe kernel's layout, one stripe per pair).  At every
 // chunk end all lanes are on the pair lane 0 is on (a lane switches at most 63 steps after lane 0), so the column
 // checkpoints go to that pair; a row-checkpoint group of a switch window goes to both pairs, like the codes.
-template <int R, bool TB, bool LEN, bool CK = false, bool LDOT = false>
+template <int R, bool TB, bool LEN, bool CK = false, int LDOT = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainWaves<R>::value))) void
 sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__restrict__ chain_pairs,
                         const int32_t *__restrict__ chain_off, int nchains, uint32_t *__restrict__ counter,
@@ -1105,7 +1122,7 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
 
     // per-lane constants: column-0 state of this lane's rows (the same for every pair)
     uint32_t Vb[R], tpb;
-    i32_reset<R, LEN>(Vb, tpb);
+    i32_reset<R, LEN, false, LDOT == 2>(Vb, tpb);
     auto rows_of = [&](int pair, uint32_t (&out)[R]) {
         const uint32_t *pa = seqa + pd[pair].a_off;
 #pragma unroll
@@ -3145,7 +3162,7 @@ static hipError_t launch_i32_R(const sed_launch &L, const sed_i32_params &prm) {
     return hipGetLastError();
 }
 
-template <int R, bool TB, bool LEN, bool CK = false, bool LDOT = false>
+template <int R, bool TB, bool LEN, bool CK = false, int LDOT = 0>
 static hipError_t launch_chain_R(const sed_launch &L, const sed_i32_params &prm) {
     SED_LAUNCH((sed_wf_i32_chain_kernel<R, TB, LEN, CK, LDOT>), dim3((L.nchains + 3) / 4), dim3(256), 0, L, L.pd,
                        L.chain_pairs, L.chain_off, L.nchains, L.chain_counter, L.chain_base, L.chain_list,
@@ -3166,9 +3183,12 @@ hipError_t sed_launch_i32_chain(const sed_launch &L, const sed_i32_params &prm, 
     switch (L.R) {
 #define CASE(RR)                                                                                   \
     case RR:                                                                                       \
+        if (prm.lad == 2 && len)                                                                   \
+            return tb ? launch_chain_R<RR, true, true, false, 2>(L, prm)                          \
+                      : launch_chain_R<RR, false, true, false, 2>(L, prm);                         \
         if (prm.lad && len)                                                                        \
-            return tb ? launch_chain_R<RR, true, true, false, true>(L, prm)                       \
-                      : launch_chain_R<RR, false, true, false, true>(L, prm);                      \
+            return tb ? launch_chain_R<RR, true, true, false, 1>(L, prm)                          \
+                      : launch_chain_R<RR, false, true, false, 1>(L, prm);                         \
         return tb ? launch_chain_R<RR, true, true>(L, prm)                                         \
                   : (len ? launch_chain_R<RR, false, true>(L, prm) : launch_chain_R<RR, false, false>(L, prm));
         CASE(4) CASE(8) CASE(16)
@@ -3319,7 +3339,7 @@ hipError_t sed_launch_traceback(const sed_launch &L, uint32_t *ops) {
     switch (L.R) {
 #define CASE(RR)                                                                                                 \
     case RR: {                                                                                                   \
-        const uint64_t pat = L.tb_ladder ? Ladder<RR>::pat : 0ull;                                               \
+        const uint64_t pat = L.tb_ladder ? (L.tb_wide ? LadderW<RR>::pat : Ladder<RR>::pat) : 0ull;                                               \
         if (uni)                                                                                                 \
             SED_LAUNCH((sed_traceback_window_kernel<RR>), dim3(grid), dim3(64), 0, L, L.pd,       \
                                L.npairs, L.tb, L.res, ops, pat);                                                \
@@ -3346,7 +3366,7 @@ hipError_t sed_launch_traceback_stripes(const sed_launch &L, uint32_t *ops, uint
     switch (L.R) {
 #define CASE(RR)                                                                                                 \
     case RR: {                                                                                                   \
-        const uint64_t pat = L.tb_ladder ? Ladder<RR>::pat : 0ull;                                               \
+        const uint64_t pat = L.tb_ladder ? (L.tb_wide ? LadderW<RR>::pat : Ladder<RR>::pat) : 0ull;                                               \
         if (SED_TBMAP_BANDS) {                                                                                   \
             hipExtLaunchKernelGGL((sed_tb_bandmap_kernel<RR>), gmap, dim3(256), 0, L.stream, L.ev0, nullptr, 0, L.pd, L.tb, map, ops, pat); \
             hipLaunchKernelGGL((sed_tb_bandcompose_kernel<RR>), gcomp, dim3(256), 0, L.stream, L.pd, map);          \

@@ -71,7 +71,7 @@ struct sed_ctx {
                                 // eligible pair, 2 never
     int opt_splitck = 0;        // SED_OPT_SPLITCK: 0 auto (on), 2 never (SPLIT script batches keep the per-cell-code forward)
     int opt_zc = 0;             // SED_OPT_ZEROCOPY: 0 auto (small batches write results into pinned host memory), 2 never
-    int opt_dot = 0;            // SED_OPT_DOT: 0 auto, 2 never (checkpoint batches keep the perm-based distance keys)    // SED_OPT_CHAIN_WAVES: cap on the persistent waves of dynamic CHAIN mode
+    int opt_dot = 0;            // SED_OPT_DOT: 0 auto, 2 never (checkpoint batches keep the perm-based distance keys), 3 no wide ladder    // SED_OPT_CHAIN_WAVES: cap on the persistent waves of dynamic CHAIN mode
     int opt_debug_corrupt = 0;  // SED_OPT_DEBUG_CORRUPT: pair + 1 whose sink-tile checkpoint is overwritten
     DevBuf selftest;
     sed_batch *scratch = nullptr;
@@ -345,10 +345,10 @@ DotKeys dot_keys_search(const int64_t kap[4][4], int64_t maxmin, int64_t lad_ami
     for (int64_t a = a_hi; a >= 1; --a) {
         const int64_t A = den * a;
         if (lad ? A < lad_amin : A * kmin <= maxmin * (kmax - kmin)) break;  // fails for every smaller a too
-        // ladder keys keep the rung c(i) and the op in the low 3 bits of W = A*(D - i*delete - j*insert) + 8*(L - i - j)
-        // + B + c(i): A must be a multiple of 8, or the D part leaks into them (a random GUI table found this:
-        // insert 2 / delete 1 factored with A = 8835, and its scripts came out wrong)
-        if (lad && (A >= 65536 || (A & 7))) continue;
+        // ladder keys keep the rung c(i) and the op in the low 3 (wide: 4) bits of W = A*(D - i*delete - j*insert) +
+        // u*(L - i - j) + B + c(i), u = 8 (16): A must be a multiple of u, or the D part leaks into them (a random GUI
+        // table found this: insert 2 / delete 1 factored with A = 8835, and its scripts came out wrong)
+        if (lad && (A >= 65536 || (A & lad_beta))) continue;  // (lad_beta + 1 = the L unit, 8 or 16)
         const int64_t J = num * a + beta;
         int64_t x = 0, y = 0;
         for (int64_t t = 1; t <= 127 && !x; ++t)
@@ -394,10 +394,11 @@ DotKeys dot_keys_search(const int64_t kap[4][4], int64_t maxmin, int64_t lad_ami
                 dk.row[i] = rw;
                 dk.col[i] = cw;
             }
-            // the virtual-column sentinel {s, 0, 0, 0} adds s x in [8, 490]: above every ladder jump, and below the
-            // 512 the border leaves to 2^32 (sed_kernels.hip: SED_KB3)
-            const int64_t sx = x > 0 ? (8 + x - 1) / x : 0;
-            dk.ok = x > 0 && sx * x <= 490;
+            // the virtual-column sentinel {s, 0, 0, 0} adds s x in [u, 490] (wide: [16, 480]): above every ladder jump
+            // (at most +5, wide +13), and below the 512 the border leaves to 2^32 (sed_kernels.hip: SED_KB3)
+            const int64_t lo = lad_beta + 1, hi = lad_beta == 15 ? 480 : 490;
+            const int64_t sx = x > 0 ? (lo + x - 1) / x : 0;
+            dk.ok = x > 0 && sx * x <= hi;
             dk.S = (uint32_t)sx;
             return dk;
         }
@@ -1232,18 +1233,29 @@ int fill_batch(sed_batch *b, const uint8_t *codes_a, const int64_t *off_a, const
             }
         }
         // ladder dot keys: the CHAIN kernel's ladder keys (L field, with or without codes) with the update addend
-        // as one v_dot4.  V = D*A + 8L needs 8 (n + m) + 7 < A < 2^16 (the L field below the D unit), and the
-        // factorisation of A*K + 7J (the d = -1 rows' constant -6 + d = -7) must fit bytes.
+        // as one v_dot4.  V = D*A + uL needs A < 2^16 and the factorisation of A*K + (u - 1)J (the d = -1 rows'
+        // constant) in bytes: u = 16 over the wide ladder (sed_kernels.hip: LadderW, ip.lad = 2) with 16 min(n, m) + 15
+        // < A, else u = 8 over the 3-bit one (ip.lad = 1) with 8 (n + m) + 7 < A (the L field below the D unit).
         b->lad = false;
         if (b->nchains > 0 && !b->ck && (want_tb || !(flags & SED_NO_LEN)) && c->K == 4 && c->opt_dot != 2) {
-            int64_t kap[4][4], maxsum = 0;
+            int64_t kap[4][4], maxsum = 0, maxmin = 0;
             for (int a = 0; a < 4; ++a)
                 for (int bb = 0; bb < 4; ++bb) kap[a][bb] = (int64_t)ip.ins + ip.del - (int64_t)c->sub[a * 4 + bb];
             for (int p = 0; p < npairs; ++p)
-                if (!b->pd[p].lane) maxsum = std::max<int64_t>(maxsum, (int64_t)len_a[p] + len_b[p]);
-            const DotKeys lk = dot_keys(kap, 0, 8 * maxsum + 8, 7);
+                if (!b->pd[p].lane) {
+                    maxsum = std::max<int64_t>(maxsum, (int64_t)len_a[p] + len_b[p]);
+                    maxmin = std::max<int64_t>(maxmin, std::min(len_a[p], len_b[p]));
+                }
+            // the wide ladder first (one jump row in 8; its sink decode reads L inside [max(n, m), n + m], so A > 16
+            // min(n, m) + 15 keeps the keys apart), the 3-bit one where that does not fit bytes
+            DotKeys lk = c->opt_dot == 3 ? DotKeys{} : dot_keys(kap, 0, 16 * maxmin + 16, 15);  // (3: tests)
+            uint32_t lad = 2;
+            if (!lk.ok) {
+                lk = dot_keys(kap, 0, 8 * maxsum + 8, 7);
+                lad = 1;
+            }
             if (lk.ok) {
-                ip.lad = 1;
+                ip.lad = lad;
                 ip.ladA = lk.A;
                 ip.ladsent = lk.S;  // (ladder mode: the sentinel's byte 0)
                 for (int a = 0; a < 4; ++a) {
@@ -1411,6 +1423,7 @@ int run_batch(sed_batch *b) {
     L.R = b->R;
     L.stream = ds;
     L.tb_ladder = b->mode == SED_MODE_I32 && !b->split_ck;  // (split_ck codes are the plain ops)
+    L.tb_wide = b->lad && b->ip.lad == 2;  // (a ladder-dot batch is a CHAIN batch: every wave pair's codes come from the LDOT kernel)
     L.ck = b->ck;
     L.tasks = b->split ? (const int2 *)b->p_tasks : nullptr;
     L.ntasks = b->split ? b->ntasks : 0;
@@ -1720,7 +1733,7 @@ int sed_set_option(sed_ctx *c, int key, int value) {
         c->opt_scaled = value;
         return SED_OK;
     }
-    if (key == SED_OPT_DOT && (value == 0 || value == 2)) {
+    if (key == SED_OPT_DOT && (value == 0 || value == 2 || value == 3)) {
         c->opt_dot = value;
         return SED_OK;
     }
@@ -1812,18 +1825,28 @@ int sed_dot_factor(const double *sub, double ins, double del, int maxmin, int la
             if (v != (double)(int64_t)v) return 0;  // integer tables only (the packed-integer kernels' domain)
             kap[a][bb] = (int64_t)v;
         }
-    const DotKeys dk = ladder_maxsum > 0 ? dot_keys(kap, 0, 8 * (int64_t)ladder_maxsum + 8, 7) : dot_keys(kap, maxmin);
+    // ladder: the wide ladder's factorisation where it exists, else the 3-bit one (as batch creation); out[9] = the L unit
+    // (the wide ladder's bound is on min(n, m): maxmin, or ladder_maxsum when maxmin is 0)
+    const int64_t lmin = maxmin > 0 ? std::min<int64_t>(maxmin, ladder_maxsum) : ladder_maxsum;
+    DotKeys dk = ladder_maxsum > 0 ? dot_keys(kap, 0, 16 * lmin + 16, 15) : dot_keys(kap, maxmin);
+    uint32_t unit = 16;
+    if (ladder_maxsum > 0 && !dk.ok) {
+        dk = dot_keys(kap, 0, 8 * (int64_t)ladder_maxsum + 8, 7);
+        unit = 8;
+    }
     if (!dk.ok) return 0;
     for (int a = 0; a < 4; ++a) {
         out[a] = dk.row[a];
         out[4 + a] = dk.col[a];
     }
     out[8] = dk.S;  // decode shift (dot keys) or sentinel byte (ladder)
-    out[9] = dk.M;
+    out[9] = ladder_maxsum > 0 ? unit : dk.M;  // decode multiplier (dot keys) or the L unit (ladder)
     return (int)dk.A;
 }
 
-int sed_batch_dot_keys(const sed_batch *b) { return b ? (b->dot ? 1 : 0) | (b->lad ? 2 : 0) : SED_E_ARG; }
+int sed_batch_dot_keys(const sed_batch *b) {
+    return b ? (b->dot ? 1 : 0) | (b->lad ? 2 : 0) | (b->lad && b->ip.lad == 2 ? 4 : 0) : SED_E_ARG;
+}
 
 int sed_batch_chain_stats(sed_batch *b, int32_t *fetched, int32_t *max_per_wave) {
     if (!b) return SED_E_ARG;

@@ -403,6 +403,11 @@ class Batch:
         return (self._lib.sed_batch_dot_keys(self.ptr) & 2) == 2
 
     @property
+    def ladder_wide(self):
+        """True when those ladder dot keys run over the wide ladder (V = D*A + 16L, one jump row in 8)."""
+        return (self._lib.sed_batch_dot_keys(self.ptr) & 4) == 4
+
+    @property
     def traceback_mode(self):
         """0 distance only, 1 per-cell traceback codes, 2 checkpoints + recompute (SED_OPT_TB), 3 per-cell codes walked
         stripe-parallel, 4 SPLIT checkpoints recomputed into per-cell codes (SED_OPT_SPLITCK)."""
@@ -849,7 +854,8 @@ if __name__ == "__main__" and len(sys.argv) == 5 and sys.argv[1] == "--engine-wo
 
 def dot_factor(sub, ins, dele, maxmin=0, ladder_maxsum=0):
     """The byte factorisation behind SED_OPT_DOT (no device needed): (A, rows, cols, aux) or None.
-    sub: 4 x 4 costs (row symbol -> column symbol); rows/cols: 4 x 4 signed bytes."""
+    sub: 4 x 4 costs (row symbol -> column symbol); rows/cols: 4 x 4 signed bytes; aux = (decode shift, multiplier),
+    or for the ladder keys (ladder_maxsum > 0) (sentinel byte, L unit: 16 on the wide ladder, else 8)."""
     out = np.zeros(10, np.uint32)
     A = load().sed_dot_factor(np.ascontiguousarray(sub, np.float64).ravel(), float(ins), float(dele), int(maxmin),
                               int(ladder_maxsum), out)

@@ -134,9 +134,9 @@ def test_dynamic_chain_config3_route(gpu, tables, user):
                 assert b.traceback_mode == (0 if not script else 2 if tb == 2 else 1)
                 fetched, per_wave = b.chain_stats()
                 assert fetched == nwave and per_wave >= 2, (fetched, nwave, per_wave)
-                # costs.json's addends factor over bytes with A > 8 (n + m): the ladder keys run on v_dot4
-                # (user_costs' would need A > 8 * 1212 with kappa up to 5: no byte factorisation that large)
-                assert b.ladder_dot_keys == (not user and tb != 2)
+                # costs.json's addends factor over bytes with A > 16 min(n, m): the ladder keys run on v_dot4 over
+                # the wide ladder (user_costs' would need A > 16 * 512 with kappa up to 5: no byte factorisation)
+                assert b.ladder_dot_keys == (not user and tb != 2) and b.ladder_wide == b.ladder_dot_keys
         finally:
             b.close()
         _check_all(plan, packed, d, ii, ln, ops, script=script, no_len=no_len)
@@ -144,19 +144,21 @@ def test_dynamic_chain_config3_route(gpu, tables, user):
             ref = (d, ii, ln, ops)
         elif script:
             _same((d, ii, ln, ops), ref, packed.ops_off)  # checkpoints against per-cell codes, whole buffers
-    # the ladder dot keys against the perm ladder on the same batch (SED_OPT_DOT = 2)
+    # the wide-ladder dot keys against the perm ladder (SED_OPT_DOT = 2) and the 3-bit ladder's dot keys (3) on the
+    # same batch, whole buffers
     if not user:
-        gpu.set_option(sedgpu.SED_OPT_DOT, 2)
-        try:
-            b, (d2, ii2, ln2, ops2) = _batch_run(gpu, packed, True)
+        for dot, lad in ((2, False), (3, True)):
+            gpu.set_option(sedgpu.SED_OPT_DOT, dot)
             try:
-                assert not b.ladder_dot_keys and b.chains == 5120
+                b, (d2, ii2, ln2, ops2) = _batch_run(gpu, packed, True)
+                try:
+                    assert b.ladder_dot_keys == lad and not b.ladder_wide and b.chains == 5120
+                finally:
+                    b.close()
             finally:
-                b.close()
-        finally:
-            gpu.set_option(sedgpu.SED_OPT_DOT, 0)
-        _check_all(plan, packed, d2, ii2, ln2, ops2)
-        _same((d2, ii2, ln2, ops2), ref, packed.ops_off)
+                gpu.set_option(sedgpu.SED_OPT_DOT, 0)
+            _check_all(plan, packed, d2, ii2, ln2, ops2)
+            _same((d2, ii2, ln2, ops2), ref, packed.ops_off)
 
 
 def test_dynamic_chain_capped_waves(gpu, tables):
