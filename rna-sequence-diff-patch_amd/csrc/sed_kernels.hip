@@ -246,7 +246,7 @@ template <int R, bool TB, bool LEN, bool COLLECT = true, bool SELL = false, bool
           int LDOT = 0>
 __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[R], uint32_t &top_prev,
                                          uint32_t &bottom, uint32_t &selv, const uint2 tv, uint32_t &outc,
-                                         uint32_t (&W)[4], const int u) {
+                                         uint32_t (&W)[4], const int u, const uint32_t jv = 0u) {
     using Lad = Ladder<R>;
     if constexpr (SELL) selv = tv.y;
     else selv = dpp_shr1(tv.y, selv);  // perm selector of this column's str2 symbol
@@ -262,20 +262,27 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
         // v_dot4, v_min3, v_and_or, v_alignbit = 4 VALU (5 with the perm), plus two adds on a jump row.
         using Lad = std::conditional_t<LDOT == 2, LadderW<R>, Ladder<R>>;
         constexpr uint32_t LOW = LDOT == 2 ? 15u : 7u;  // the rung + op field
+        // the wide ladder's jump is row 0 of every lane (i = 1 mod P): its delete and update inputs, the cell above
+        // the band and the diagonal, both take d + 1 = J0, which the DPP move from lane t - 1 adds itself (one
+        // v_add_u32_dpp with jv = J0 instead of v_mov_b32_dpp), so top_prev carries it too (i32_reset: tpb)
+        constexpr bool BIAS = LDOT == 2;
+        constexpr uint32_t J0 = (uint32_t)(Lad::rung(1) - Lad::rung(0) + 1);
         constexpr int AH = R < 4 ? R : 4;
         uint32_t cand[R];
         cand[0] = dot_add(cv[0], selv, top_prev);
 #pragma unroll
         for (int r = 1; r < AH; ++r) cand[r] = dot_add(cv[r], selv, V[r - 1]);
-        const uint32_t topv = dpp_shr1(TOPC ? top_prev : tv.x, bottom);
+        const uint32_t topv = BIAS ? dpp_shr1_add(TOPC ? top_prev : tv.x + J0, bottom, jv)
+                                   : dpp_shr1(TOPC ? top_prev : tv.x, bottom);
         uint32_t up = topv;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (r + AH < R) cand[r + AH] = dot_add(cv[r + AH], selv, V[r + AH - 1]);
             dot_fence(cand[r]);
             const int c = Lad::rung(r + 1), d = c - Lad::rung(r);  // compile-time after unrolling
-            const uint32_t upd = d == -1 ? cand[r] : cand[r] + (uint32_t)(d + 1);
-            const uint32_t mm = umin3(V[r], d == -1 ? up : up + (uint32_t)(d + 1), upd);
+            const bool plain = d == -1 || (BIAS && r == 0);          // (BIAS: row 0's inputs carry d + 1)
+            const uint32_t upd = plain ? cand[r] : cand[r] + (uint32_t)(d + 1);
+            const uint32_t mm = umin3(V[r], plain ? up : up + (uint32_t)(d + 1), upd);
             if constexpr (TB) {
                 const int k = u * R + r;
                 W[k >> 4] = __builtin_amdgcn_alignbit(mm, W[k >> 4], 2);
@@ -345,7 +352,9 @@ __device__ __forceinline__ void i32_step(uint32_t (&V)[R], const uint32_t (&cv)[
 // first column.
 template <int R, bool LEN, bool DOT = false, bool WIDE = false>
 __device__ __forceinline__ void i32_reset(uint32_t (&V)[R], uint32_t &top_prev) {
-    top_prev = LEN ? SED_KB3 : DOT ? SED_KB_DOT : SED_KB;
+    // (WIDE: top_prev carries row 0's jump, i32_step LDOT = 2)
+    top_prev = LEN ? SED_KB3 + (WIDE ? (uint32_t)(LadderW<R>::rung(1) - LadderW<R>::rung(0) + 1) : 0u)
+                   : DOT ? SED_KB_DOT : SED_KB;
 #pragma unroll
     for (int r = 0; r < R; ++r)
         V[r] = LEN ? SED_KB3 + (uint32_t)(WIDE ? LadderW<R>::rung(r + 1) : Ladder<R>::rung(r + 1)) : DOT ? SED_KB_DOT : SED_KB;
@@ -1034,7 +1043,7 @@ __device__ __forceinline__ void i32_chain_group(uint32_t (&V)[R], uint32_t (&cv)
                                                 uint32_t &outc, uint32_t (&W)[4], const int s0, const int lane,
                                                 const int Tcur, const int csA, const int clA, const int crA,
                                                 uint32_t &capA, const int csB, const int clB, const int crB,
-                                                uint32_t &capB, uint32_t (&rcv)[Grp<R>::G]) {
+                                                uint32_t &capB, uint32_t (&rcv)[Grp<R>::G], const uint32_t jv) {
     constexpr int G = Grp<R>::G;
     uint2 tv[G];
 #pragma unroll
@@ -1042,7 +1051,7 @@ __device__ __forceinline__ void i32_chain_group(uint32_t (&V)[R], uint32_t (&cv)
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         const int s = s0 + u;
-        i32_step<R, TB, LEN, false, true, true, false, LDOT>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u);
+        i32_step<R, TB, LEN, false, true, true, false, LDOT>(V, cv, top_prev, bottom, selv, tv[u], outc, W, u, jv);
         if constexpr (CK) rcv[u] = V[R - 1];  // the band's bottom row (row checkpoints), before any switch
         if constexpr (GEN) {
             const bool hA = (s == csA) && (lane == clA), hB = (s == csB) && (lane == clB);
@@ -1123,6 +1132,8 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
     // per-lane constants: column-0 state of this lane's rows (the same for every pair)
     uint32_t Vb[R], tpb;
     i32_reset<R, LEN, false, LDOT == 2>(Vb, tpb);
+    uint32_t jv = (uint32_t)(LadderW<R>::rung(1) - LadderW<R>::rung(0) + 1);  // (LDOT = 2: the DPP move's add, a VGPR)
+    asm volatile("" : "+v"(jv));
     auto rows_of = [&](int pair, uint32_t (&out)[R]) {
         const uint32_t *pa = seqa + pd[pair].a_off;
 #pragma unroll
@@ -1190,7 +1201,7 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
                 const int s = s0 + g * G;
                 i32_chain_group<R, TB, LEN, false, false, CK, LDOT>(
                     V, cv, cvn, Vb, tpb, top_prev, bottom, selv, lsel0 + g * G, outc, W, s, lane, -(1 << 30), prv.cap_step,
-                    prv.cap_lane, prv.cap_row, capA, cur.cap_step, cur.cap_lane, cur.cap_row, capB, rcv);
+                    prv.cap_lane, prv.cap_row, capA, cur.cap_step, cur.cap_lane, cur.cap_row, capB, rcv, jv);
                 if constexpr (TB) {
                     uint32_t lo = (uint32_t)lane * 16u;
                     asm volatile("" : "+v"(lo));
@@ -1216,7 +1227,7 @@ sed_wf_i32_chain_kernel(const sed_pair_desc *__restrict__ pd, const int32_t *__r
 #define SED_CGROUP(SW, GEN)                                                                               \
     i32_chain_group<R, TB, LEN, SW, GEN, CK, LDOT>(V, cv, cvn, Vb, tpb, top_prev, bottom, selv, lsel, outc, W, s, lane, \
                                              Tsw, prv.cap_step, prv.cap_lane, prv.cap_row, capA, cur.cap_step,    \
-                                             cur.cap_lane, cur.cap_row, capB, rcv)
+                                             cur.cap_lane, cur.cap_row, capB, rcv, jv)
             if (capg) SED_CGROUP(false, true);
             else if (win) SED_CGROUP(true, false);
             else SED_CGROUP(false, false);
