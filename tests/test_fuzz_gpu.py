@@ -4,7 +4,8 @@ Every iteration draws a cost table (costs.json, user_costs.json or one of the G8
 the table's whole alphabet), a batch size around the routing thresholds (1, 16, 17, 64, 65, 256, 257 ... pairs),
 ragged lengths (empty sides included, now and then a pair past 1000 rows), a flag set (script, distance with length,
 distance only) and a routing override (SPLIT on / off, lane kernels off, rows per lane, fp64 forced, zero-copy off,
-16-lane segments on / off, per-cell codes or checkpoints, SPLIT's ladder-key forward), then compares every pair's distance, typing, length and script with the oracle, and checks that the script
+16-lane segments on / off, per-cell codes or checkpoints, SPLIT's ladder-key forward, CHAIN mode on the wide, 3-bit
+or perm ladder), then compares every pair's distance, typing, length and script with the oracle, and checks that the script
 region's bits past the last op are zero (sed.h)
 (oracle/sed_oracle.c: StringEditDistance.py:92-334).  SED_FUZZ_SECONDS sets the budget (default 20 s) and
 SED_FUZZ_SEED the first seed (default 2026), so the default run is reproducible; a failure names its seed.
@@ -33,6 +34,13 @@ OPTIONS = [
     (sedgpu.SED_OPT_TB, 1), (sedgpu.SED_OPT_TB, 2),
     (sedgpu.SED_OPT_SPLITCK, 2),
     ("mode", 2), ("mode", 3),  # the fp64 kernels forced (simple / full typing)
+    # CHAIN mode forced at R = 8 / 4 (dynamic, or static chains of 3), on the wide-ladder dot keys where the table
+    # factors, the 3-bit ladder's (SED_OPT_DOT = 3) or the perm ladder (2)
+    ((sedgpu.SED_OPT_CHAIN, 1), (sedgpu.SED_OPT_ROWS_PER_LANE, 8)),
+    ((sedgpu.SED_OPT_CHAIN, 1), (sedgpu.SED_OPT_ROWS_PER_LANE, 4)),
+    ((sedgpu.SED_OPT_CHAIN, 3), (sedgpu.SED_OPT_ROWS_PER_LANE, 8)),
+    ((sedgpu.SED_OPT_CHAIN, 1), (sedgpu.SED_OPT_ROWS_PER_LANE, 8), (sedgpu.SED_OPT_DOT, 3)),
+    ((sedgpu.SED_OPT_CHAIN, 1), (sedgpu.SED_OPT_ROWS_PER_LANE, 8), (sedgpu.SED_OPT_DOT, 2)),
 ]
 CELL_CAP = 2.5e7  # oracle work per iteration
 
@@ -68,19 +76,21 @@ def _batch(rng, alphabet):
 def _check(gpu, table, pairs, script, no_len, opt, seed):
     plan = sedcost.build_plan(table, [a for a, _ in pairs], [b for _, b in pairs])
     gpu.set_costs(plan)
-    key, val = opt
-    if key == "mode":
-        gpu.set_mode(val)
-    elif key is not None:
-        gpu.set_option(key, val)
+    settings = list(opt) if isinstance(opt[0], tuple) else [opt]
+    for key, val in settings:
+        if key == "mode":
+            gpu.set_mode(val)
+        elif key is not None:
+            gpu.set_option(key, val)
     try:
         packed = sedgpu.PackedPairs([plan.encode(a) for a, _ in pairs], [plan.encode(b) for _, b in pairs])
         dist, is_int, ln, ops = gpu.run(packed, script, no_len=no_len)
     finally:
-        if key == "mode":
-            gpu.set_mode(0)
-        elif key is not None:
-            gpu.set_option(key, 0)
+        for key, val in settings:
+            if key == "mode":
+                gpu.set_mode(0)
+            elif key is not None:
+                gpu.set_option(key, 0)
     cs = oracle.Costs.from_plan(plan)
     for p, (a, b) in enumerate(pairs):
         o = oracle.pair(cs, plan.encode(a), plan.encode(b), want_ops=script)
